@@ -1,0 +1,157 @@
+/*
+ * libocf -- MI355X (gfx950) kernels for the autoencoder-CF training hot path.
+ *
+ * C ABI only: plain pointers, sizes and POD structs; no framework types.  Every function returns
+ * 0 on success and a non-zero code on failure; ocf_last_error() gives the message (thread-local).
+ * All device pointers are caller-owned (e.g. PyTorch-ROCm tensors passed by data_ptr()); the
+ * library never allocates or synchronises per call.  Work is enqueued on the caller's
+ * hipStream_t (passed as void*), so every entry point is graph-capturable.
+ *
+ * The reference (Epist/omnidirectional_collaborative_filtering, Python 2.7 + TF 1.3 / Keras 2.0.4)
+ * has no FFI of its own: its hot path is the Python pair data_reader / omni_model driven by
+ * train.py.  Each entry point below names the reference code it replaces; INTEGRATION.md shows
+ * the ctypes binding a maintainer would add on the reference side.
+ */
+#ifndef OCF_H_
+#define OCF_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types */
+#define OCF_DT_F32 0
+#define OCF_DT_F16 1
+#define OCF_DT_BF16 2
+
+/* activations (model.py:34 default 'tanh'; train.py:52 'sigmoid') */
+#define OCF_ACTV_LINEAR 0
+#define OCF_ACTV_SIGMOID 1
+#define OCF_ACTV_TANH 2
+#define OCF_ACTV_RELU 3
+
+/* optimizers (train.py:50-51 Adagrad; train_jester.py:61 'rmsprop'; north_star Adam) */
+#define OCF_OPTK_SGD 0
+#define OCF_OPTK_ADAGRAD 1
+#define OCF_OPTK_RMSPROP 2
+#define OCF_OPTK_ADAM 3
+
+/* GEMM epilogues (ocf_gemm) */
+#define OCF_EPI_SLAB 0       /* split-K fp32 partial slabs                                   */
+#define OCF_EPI_BIAS_ACT 1   /* + bias, activation, dropout  (model.py:64-73)                */
+#define OCF_EPI_GRAD_ACT 2   /* * dropout mask * act'(a), bias-grad column partials          */
+#define OCF_EPI_GRAD 3       /* raw weight gradient (data-parallel path)                     */
+#define OCF_EPI_OPTIM 4      /* fused optimizer update of the weight tile (train.py:50-51)  */
+#define OCF_EPI_PREDICT 5    /* y = mask * (acc + b)   (model.py:82-86)                       */
+#define OCF_EPI_MASKED_MSE 6 /* masked MSE loss/grad on bucketed targets (train.py:49)       */
+
+/* Keras 2.0.4 optimizer scalars for one step (host computes lr incl. decay / Adam lr_t). */
+typedef struct OcfOptParams {
+  int kind;
+  float lr, eps, rho, beta2, l2, gscale;
+} OcfOptParams;
+
+/*
+ * ocf_scatter_batch -- replaces data_reader.build_sparse_batch (data_reader.py:95-200, mode 0)
+ * and build_sparse_batch_fixed_split (data_reader.py:202-298, mode 1), dense representation.
+ * Zeroes rows [0, B_pad) of every non-null output, scatters the batch, and (if tile_cnt != NULL)
+ * buckets the target entries by 128-column tile for OCF_EPI_MASKED_MSE.
+ */
+typedef struct OcfScatterArgs {
+  /* source 1: train CSR (mode 0) or eval-input CSR (mode 1) */
+  const int64_t* rp1; const int32_t* col1; const float* val1; const int32_t* dup1;
+  const int32_t* rows1;      /* [B] dataset row of each batch row, -1 = empty (None input)  */
+  const uint8_t* keep1;      /* [nnz of batch] reciprocal-split keep flags (host NumPy RNG)  */
+  const int64_t* boff1;      /* [B+1] batch-local entry offsets of source 1                  */
+  float s0, s1;              /* data_sparsity range; used when keep1 == NULL (device RNG)   */
+  uint64_t seed, stream;
+  int mode;                  /* 0 train, 1 eval                                              */
+  int pass_through;          /* pass_through_input_training (data_reader.py:161)             */
+  /* source 2: eval-target CSR (mode 1) */
+  const int64_t* rp2; const int32_t* col2; const float* val2; const int32_t* dup2;
+  const int32_t* rows2;
+  int B, B_pad, N;
+  float aux;                 /* aux_var_value (train.py:47)                                  */
+  /* dense fp32 outputs [B_pad][ld] (nullable) */
+  float *X, *Min, *Mout, *T, *Mmiss;
+  int64_t ld;
+  /* concatenated layer-0 input [B_pad][xin_ld] in the compute dtype (nullable) */
+  void* xin; int xin_dtype; int64_t xin_ld, xin_block;
+  int feed;                  /* block 1: 0 none, 1 M_in (dropout/both), 2 M_miss (causal), 3 zeros */
+  int both;                  /* block 2 = M_miss (auxilliary_mask_type 'both')               */
+  /* target buckets (nullable) */
+  int* tile_cnt; int* bk_ptr; int* bk_cur; int32_t* bk_rc; float* bk_t; float* bk_m;
+  int n_tiles;
+} OcfScatterArgs;
+
+int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
+
+/* Target buckets from dense target / output-mask arrays (Model.train_on_batch on user arrays). */
+int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,
+                      int* bk_ptr, int* bk_cur, int32_t* bk_rc, float* bk_t, float* bk_m, void* stream);
+
+/* Pack up to three dense fp32 [B][ld_src] inputs into the compute-dtype concatenated layer-0
+ * input (model.py:47-56 concatenate). */
+int ocf_pack_input(const float* s0, const float* s1, const float* s2, int64_t ld_src, int B, int N, void* xin,
+                   int dtype, int64_t xin_ld, int64_t xin_block, int B_pad, void* stream);
+
+/*
+ * ocf_gemm -- one MFMA GEMM  C[M,N] = A[M,K] * B[K,N]  with a fused epilogue.  Replaces the TF
+ * MatMul / BiasAdd / activation / Dropout / Mul / SquaredDifference / Assign ops Keras emits for
+ * model.py:64-86 and train.py:49-51.  a_col: A stored [K][M] (else [M][K]); b_col: B stored [K][N]
+ * (else [N][K]).  M, N multiples of 128; K a multiple of 64 (f16/bf16) or 32 (f32).
+ */
+typedef struct OcfGemmArgs {
+  int compute_dtype;         /* f16 / bf16 MFMA (fp32 accumulate) or f32 MFMA (exact fp32)     */
+  const void* A; int a_dtype; int a_col; int64_t lda;
+  const void* B; int b_dtype; int b_col; int64_t ldb;
+  int M, N, K;
+  int splits;                /* split-K count (OCF_EPI_SLAB only)                               */
+  int order;                 /* tile order: 0 n-fastest, 1 m-fastest                            */
+  int epi;
+  /* epilogue operands (meaning per epilogue; unused ones may be NULL/0) */
+  float* out; int64_t ld_out; int64_t split_stride;          /* SLAB, GRAD, PREDICT          */
+  const float* bias;                                          /* BIAS_ACT, PREDICT, MSE       */
+  int act; float keep; uint64_t seed, stream;                 /* BIAS_ACT, GRAD_ACT           */
+  const uint8_t* mask_in; uint8_t* mask_out;                  /* dropout masks                */
+  float* a_out; void* h_out; int h_dtype;                     /* BIAS_ACT outputs / GRAD_ACT  */
+  const float* a_in;                                          /* GRAD_ACT: forward activation */
+  float* db_part; int64_t ld_db;                              /* GRAD_ACT, MSE               */
+  int m_real, n_real;
+  float* p; float* s1; float* s2; OcfOptParams opt;           /* OPTIM                        */
+  const float* pmask; int64_t ld_pmask;                       /* PREDICT output mask          */
+  const int* bk_ptr; const int32_t* bk_rc; const float* bk_t; const float* bk_m;   /* MSE     */
+  float* stats_part; float* row_sse_part;                     /* MSE                          */
+} OcfGemmArgs;
+
+int ocf_gemm(const OcfGemmArgs* args, void* stream);
+
+/* split-K reductions fused with the layer epilogue (see OCF_EPI_BIAS_ACT / OCF_EPI_GRAD_ACT). */
+int ocf_splitk_bias_act(const float* slabs, int splits, int64_t split_stride, int M, int N, int64_t ld,
+                        const float* bias, int act, float keep, uint64_t seed, uint64_t stream,
+                        const uint8_t* mask_in, uint8_t* mask_out, float* a_out, void* h_out, int h_dtype,
+                        int m_real, int n_real, void* hstream);
+int ocf_splitk_grad_act(const float* slabs, int splits, int64_t split_stride, int M, int N, int64_t ld,
+                        const float* a_in, const uint8_t* mask, float keep, int act, void* d_out, int d_dtype,
+                        float* db, float gscale, int m_real, int n_real, void* hstream);
+
+/* ocf_opt_step -- elementwise Adagrad / RMSprop / Adam / SGD update (Keras 2.0.4 get_updates);
+ * g is multiplied by opt.gscale.  Used for biases and after the data-parallel all-reduce. */
+int ocf_opt_step(float* p, const float* g, float* s1, float* s2, int64_t n, const OcfOptParams* opt, void* stream);
+
+/* bias update from per-row-tile column partials db_part[parts][ld] (fixed summation order). */
+int ocf_bias_opt_from_partials(float* b, const float* db_part, int parts, int64_t ld, int n, float* s1, float* s2,
+                               float* g_out, const OcfOptParams* opt, void* stream);
+
+/* reduce OCF_EPI_MASKED_MSE partials to out[4 + M] = {sse, sae, nnz(T+yhat), 0, row_sse[M]}. */
+int ocf_stats_finalize(const float* stats_part, int n_parts, const float* row_sse_part, int n_tiles, int M,
+                       float* out, void* stream);
+
+int ocf_version(void);
+const char* ocf_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCF_H_ */

@@ -1,0 +1,103 @@
+"""ctypes binding of libocf.so (the C ABI declared in include/ocf.h).
+
+The product path has no CPU fallback: if the shared library is missing or fails to load, every
+entry point raises.  Build it with ``python -m omnidirectional_collaborative_filtering_amd.build``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libocf.so")
+
+DT_F32, DT_F16, DT_BF16 = 0, 1, 2
+ACT = {"linear": 0, None: 0, "sigmoid": 1, "tanh": 2, "relu": 3}
+OPT_SGD, OPT_ADAGRAD, OPT_RMSPROP, OPT_ADAM = 0, 1, 2, 3
+EPI_SLAB, EPI_BIAS_ACT, EPI_GRAD_ACT, EPI_GRAD, EPI_OPTIM, EPI_PREDICT, EPI_MASKED_MSE = range(7)
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F32 = ctypes.c_float
+
+
+class OcfOptParams(ctypes.Structure):
+    _fields_ = [("kind", I32), ("lr", F32), ("eps", F32), ("rho", F32), ("beta2", F32), ("l2", F32),
+                ("gscale", F32)]
+
+
+class OcfScatterArgs(ctypes.Structure):
+    _fields_ = [
+        ("rp1", P), ("col1", P), ("val1", P), ("dup1", P), ("rows1", P), ("keep1", P), ("boff1", P),
+        ("s0", F32), ("s1", F32), ("seed", U64), ("stream", U64), ("mode", I32), ("pass_through", I32),
+        ("rp2", P), ("col2", P), ("val2", P), ("dup2", P), ("rows2", P),
+        ("B", I32), ("B_pad", I32), ("N", I32), ("aux", F32),
+        ("X", P), ("Min", P), ("Mout", P), ("T", P), ("Mmiss", P), ("ld", I64),
+        ("xin", P), ("xin_dtype", I32), ("xin_ld", I64), ("xin_block", I64), ("feed", I32), ("both", I32),
+        ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
+    ]
+
+
+class OcfGemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("compute_dtype", I32),
+        ("A", P), ("a_dtype", I32), ("a_col", I32), ("lda", I64),
+        ("B", P), ("b_dtype", I32), ("b_col", I32), ("ldb", I64),
+        ("M", I32), ("N", I32), ("K", I32), ("splits", I32), ("order", I32), ("epi", I32),
+        ("out", P), ("ld_out", I64), ("split_stride", I64),
+        ("bias", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64),
+        ("mask_in", P), ("mask_out", P), ("a_out", P), ("h_out", P), ("h_dtype", I32), ("a_in", P),
+        ("db_part", P), ("ld_db", I64), ("m_real", I32), ("n_real", I32),
+        ("p", P), ("s1", P), ("s2", P), ("opt", OcfOptParams),
+        ("pmask", P), ("ld_pmask", I64),
+        ("bk_ptr", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("stats_part", P), ("row_sse_part", P),
+    ]
+
+
+# every symbol include/ocf.h declares, with its ctypes signature
+SIGNATURES = {
+    "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
+    "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P]),
+    "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P]),
+    "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
+    "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
+    "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),
+    "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),
+    "ocf_bias_opt_from_partials": (I32, [P, P, I32, I64, I32, P, P, P, ctypes.POINTER(OcfOptParams), P]),
+    "ocf_stats_finalize": (I32, [P, I32, P, I32, I32, P, P]),
+    "ocf_version": (I32, []),
+    "ocf_last_error": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+class OcfError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libocf.so (raises if absent -- there is deliberately no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OcfError("libocf.so not built at %s (run omnidirectional_collaborative_filtering_amd.build)" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise OcfError("%s failed: %s" % (name, lib.ocf_last_error().decode()))
+    return rc

@@ -1,0 +1,354 @@
+// Fused GEMM epilogues.  Each epilogue receives the 2x2 block of 32x32 fp32 accumulators of one
+// wave (C layout of v_mfma_f32_32x32x*: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)).
+#pragma once
+#include "ocf_gemm.h"
+
+namespace ocf {
+
+template <class F>
+__device__ __forceinline__ void for_each_acc(ocf_f16v (&acc)[2][2], const TileCtx& c, F&& f) {
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int m = c.m0 + c.wm + acc_row(bi, r, c.lane);
+        int n = c.n0 + c.wn + acc_col(bj, c.lane);
+        f(m, n, acc[bi][bj][r]);
+      }
+}
+
+// ---- optimizer update (Keras 2.0.4 get_updates, float32 op order) ---------------------
+__device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float& p, float& s1, float& s2) {
+  if (o.l2 != 0.f) g = g + 2.0f * o.l2 * p;
+  switch (o.kind) {
+    case OCF_OPT_ADAGRAD: {           // a += g^2 ; p -= lr*g/(sqrt(a)+eps)
+      float a = s1 + g * g;
+      s1 = a;
+      p = p - (o.lr * g) / (sqrtf(a) + o.eps);
+    } break;
+    case OCF_OPT_RMSPROP: {           // a = rho*a + (1-rho)*g^2
+      float a = o.rho * s1 + (1.0f - o.rho) * (g * g);
+      s1 = a;
+      p = p - (o.lr * g) / (sqrtf(a) + o.eps);
+    } break;
+    case OCF_OPT_ADAM: {              // m,v EMAs; p -= lr_t*m/(sqrt(v)+eps)
+      float m = o.rho * s1 + (1.0f - o.rho) * g;
+      float v = o.beta2 * s2 + (1.0f - o.beta2) * (g * g);
+      s1 = m;
+      s2 = v;
+      p = p - (o.lr * m) / (sqrtf(v) + o.eps);
+    } break;
+    default:
+      p = p - o.lr * g;
+  }
+}
+
+// ---- split-K partial slab: out[split][m][n] --------------------------------------------
+struct EpiSlab {
+  static constexpr int LDS_NEED = 0;
+  struct Params {
+    float* out;
+    int64_t ld;
+    int64_t split_stride;
+  };
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    float* o = p.out + (int64_t)c.split * p.split_stride;
+    for_each_acc(acc, c, [&](int m, int n, float v) { o[(int64_t)m * p.ld + n] = v; });
+  }
+};
+
+// ---- bias + activation + dropout (hidden layers) ----------------------------------------
+struct BiasActParams {
+  const float* bias;
+  int act;
+  float keep;              // 1 - dropout rate (1 = no dropout)
+  uint64_t seed, stream;   // device RNG for dropout (Philox)
+  const uint8_t* mask_in;  // injected dropout mask (nullable)
+  uint8_t* mask_out;       // dropout mask record for backward (nullable)
+  float* a_out;            // pre-dropout activation fp32 (nullable)
+  void* h_out;             // post-dropout activation in compute dtype (nullable)
+  int h_dtype;
+  int64_t ld;
+  int m_real, n_real;
+};
+
+__device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, int n, float v) {
+  int64_t idx = (int64_t)m * p.ld + n;
+  bool live = m < p.m_real && n < p.n_real;
+  float a = live ? act_apply(p.act, v + p.bias[n]) : 0.f;
+  float h = a;
+  if (p.keep < 1.f) {
+    uint8_t mk;
+    if (p.mask_in) mk = p.mask_in[idx];
+    else mk = (uint8_t)floorf(p.keep + philox_uniform(p.seed, p.stream, (uint64_t)idx));
+    h = (a / p.keep) * (float)mk;
+    if (p.mask_out) p.mask_out[idx] = mk;
+  }
+  if (p.a_out) p.a_out[idx] = a;
+  if (p.h_out) {
+    if (p.h_dtype == OCF_F32) reinterpret_cast<float*>(p.h_out)[idx] = h;
+    else if (p.h_dtype == OCF_F16) reinterpret_cast<_Float16*>(p.h_out)[idx] = (_Float16)h;
+    else reinterpret_cast<__bf16*>(p.h_out)[idx] = (__bf16)h;
+  }
+}
+
+struct EpiBiasAct {
+  static constexpr int LDS_NEED = 0;
+  using Params = BiasActParams;
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    for_each_acc(acc, c, [&](int m, int n, float v) { bias_act_store(p, m, n, v); });
+  }
+};
+
+// ---- backward through activation + dropout, with per-m-tile bias-grad column partials ----
+struct GradActParams {
+  const float* a;          // forward activation (pre-dropout) of this layer, fp32
+  const uint8_t* mask;     // dropout mask (nullable)
+  float keep;
+  int act;
+  void* d_out;             // delta in compute dtype (unscaled by gscale)
+  int d_dtype;
+  int64_t ld;
+  float* db_part;          // [M/128][ld] column partial sums (nullable), already * gscale
+  float gscale;
+  int m_real, n_real;
+};
+
+__device__ __forceinline__ float grad_act_value(const GradActParams& p, int m, int n, float v) {
+  int64_t idx = (int64_t)m * p.ld + n;
+  if (!(m < p.m_real && n < p.n_real)) return 0.f;
+  float d = v;
+  if (p.keep < 1.f && p.mask) d = d * ((float)p.mask[idx] / p.keep);
+  return d * act_grad(p.act, p.a[idx]);
+}
+
+__device__ __forceinline__ void store_ct(void* out, int dtype, int64_t idx, float v) {
+  if (dtype == OCF_F32) reinterpret_cast<float*>(out)[idx] = v;
+  else if (dtype == OCF_F16) reinterpret_cast<_Float16*>(out)[idx] = (_Float16)v;
+  else reinterpret_cast<__bf16*>(out)[idx] = (__bf16)v;
+}
+
+struct EpiGradAct {
+  static constexpr int LDS_NEED = 2 * GT_BN * 4;
+  using Params = GradActParams;
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    float colsum[2] = {0.f, 0.f};
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int m = c.m0 + c.wm + acc_row(bi, r, c.lane);
+          int n = c.n0 + c.wn + acc_col(bj, c.lane);
+          float d = grad_act_value(p, m, n, acc[bi][bj][r]);
+          store_ct(p.d_out, p.d_dtype, (int64_t)m * p.ld + n, d);
+          colsum[bj] += d;
+        }
+    if (!p.db_part) return;
+    // combine lane halves (rows 4..7 of each 8) then the two waves sharing wn, fixed order
+#pragma unroll
+    for (int bj = 0; bj < 2; ++bj) colsum[bj] += __shfl_xor(colsum[bj], 32);
+    float* s = reinterpret_cast<float*>(c.lds);
+    __syncthreads();
+    if (c.lane < 32) {
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) s[(c.wm / 64) * GT_BN + c.wn + 32 * bj + c.lane] = colsum[bj];
+    }
+    __syncthreads();
+    if (c.tid < GT_BN) {
+      float v = s[c.tid] + s[GT_BN + c.tid];
+      p.db_part[(int64_t)c.tile_m * p.ld + c.n0 + c.tid] = v * p.gscale;
+    }
+  }
+};
+
+// ---- raw gradient store (data-parallel path: all-reduce before the optimizer) ------------
+struct EpiGradStore {
+  static constexpr int LDS_NEED = 0;
+  struct Params {
+    float* g;
+    int64_t ld;
+    float gscale;
+  };
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    for_each_acc(acc, c, [&](int m, int n, float v) { p.g[(int64_t)m * p.ld + n] = v * p.gscale; });
+  }
+};
+
+// ---- fused optimizer: weight-gradient tile never leaves registers -----------------------
+struct EpiOptim {
+  static constexpr int LDS_NEED = 0;
+  struct Params {
+    float* p;
+    float* s1;
+    float* s2;
+    int64_t ld;
+    OcfOptParams op;
+  };
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    OcfOptParams o = p.op;
+    for_each_acc(acc, c, [&](int m, int n, float v) {
+      int64_t idx = (int64_t)m * p.ld + n;
+      float w = p.p[idx];
+      float a = p.s1 ? p.s1[idx] : 0.f;
+      float b = p.s2 ? p.s2[idx] : 0.f;
+      opt_update(o, v * o.gscale, w, a, b);
+      p.p[idx] = w;
+      if (p.s1) p.s1[idx] = a;
+      if (p.s2) p.s2[idx] = b;
+    });
+  }
+};
+
+// ---- predict: y = mask * (acc + b) (model.py:82-86) -------------------------------------
+struct EpiPredict {
+  static constexpr int LDS_NEED = 0;
+  struct Params {
+    const float* bias;
+    const float* mask;   // dense [M][ld_mask] output mask (nullable = no mask)
+    int64_t ld_mask;
+    float* out;
+    int64_t ld_out;
+    int m_real, n_real;
+  };
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+    for_each_acc(acc, c, [&](int m, int n, float v) {
+      if (m < p.m_real && n < p.n_real) {
+        float y = v + p.bias[n];
+        if (p.mask) y = p.mask[(int64_t)m * p.ld_mask + n] * y;
+        p.out[(int64_t)m * p.ld_out + n] = y;
+      }
+    });
+  }
+};
+
+// ---- masked MSE on the decoder output (train.py:49, model.py:86) ------------------------
+// Target entries of the batch are bucketed by 128-column tile (built by the scatter kernels).
+// Per tile: y = acc + b is staged to LDS; each target entry (row, col, t, m) gives
+//   err = m*y - t            (Keras MSE residual of prediction = mask * y_full)
+//   d   = err * m            (dL/dy_full up to the constant 2/(B*N), folded in later)
+// The dense d tile (zero where no target) is written in the compute dtype for the backward
+// GEMMs, its column sums give the output-bias gradient, and SSE / SAE / count_nonzero(T+yhat)
+// / per-row SSE feed the loss and the train.py metrics.
+struct EpiMaskedMSE {
+  static constexpr int YS = GT_BN + 4;   // LDS row stride (floats) of the staged tile
+  static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 4 * GT_THREADS * 4;
+  struct Params {
+    const float* bias;        // output bias [N]
+    const int* bk_ptr;        // [n_tiles+1]
+    const int* bk_rc;         // (row << 7) | (col & 127)
+    const float* bk_t;        // target value
+    const float* bk_m;        // output-mask value
+    void* d_out;              // dense delta [M][ld_d] compute dtype (nullable: eval)
+    int d_dtype;
+    int64_t ld_d;
+    float* db_part;           // [M/128][ld_db] column sums * gscale (nullable)
+    int64_t ld_db;
+    float gscale;
+    float* stats_part;        // [n_tiles * gm][4]: sse, sae, nnz(T+yhat), unused
+    float* row_sse_part;      // [n_tiles][M] (nullable)
+  };
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape& sh) {
+    float* Y = reinterpret_cast<float*>(c.lds);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(c.lds + GT_BM * YS * 4);
+    float* rsse = reinterpret_cast<float*>(c.lds + GT_BM * YS * 4 + GT_BM * 16);
+    float* red = rsse + GT_BM;
+    // 1. stage y = acc + b
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int ml = c.wm + acc_row(bi, r, c.lane);
+          int nl = c.wn + acc_col(bj, c.lane);
+          Y[ml * YS + nl] = acc[bi][bj][r] + p.bias[c.n0 + nl];
+        }
+    for (int i = c.tid; i < GT_BM * 4; i += GT_THREADS) bits[i] = 0u;
+    if (c.tid < GT_BM) rsse[c.tid] = 0.f;
+    __syncthreads();
+    // 2. target entries of this column tile falling in this row tile
+    float sse = 0.f, sae = 0.f, cnt = 0.f;
+    const int b0 = p.bk_ptr[c.tile_n], b1 = p.bk_ptr[c.tile_n + 1];
+    for (int e = b0 + c.tid; e < b1; e += GT_THREADS) {
+      int rc = p.bk_rc[e];
+      int row = rc >> 7, nl = rc & 127;
+      int ml = row - c.m0;
+      if (ml < 0 || ml >= GT_BM) continue;
+      float m = p.bk_m[e], t = p.bk_t[e];
+      float yhat = m * Y[ml * YS + nl];
+      float err = yhat - t;
+      Y[ml * YS + nl] = err * m;
+      atomicOr(&bits[ml * 4 + (nl >> 5)], 1u << (nl & 31));
+      sse += err * err;
+      sae += fabsf(err);
+      cnt += (t + yhat != 0.f) ? 1.f : 0.f;
+      atomicAdd(&rsse[ml], err * err);
+    }
+    __syncthreads();
+    // 3. dense delta tile (zeros where no target) -> compute dtype, 8 columns per chunk
+    if (p.d_out) {
+      for (int ch = c.tid; ch < GT_BM * (GT_BN / 8); ch += GT_THREADS) {
+        int ml = ch / (GT_BN / 8), c8 = (ch % (GT_BN / 8)) * 8;
+        uint32_t w = bits[ml * 4 + (c8 >> 5)] >> (c8 & 31);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ((w >> j) & 1u) ? Y[ml * YS + c8 + j] : 0.f;
+        int64_t off = (int64_t)(c.m0 + ml) * p.ld_d + c.n0 + c8;
+        if (p.d_dtype == OCF_F32) {
+          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.d_out) + off);
+          o[0] = make_float4(v[0], v[1], v[2], v[3]);
+          o[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else if (p.d_dtype == OCF_F16) {
+          _Float16 h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
+          uint4 u; __builtin_memcpy(&u, h, 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.d_out) + off) = u;
+        } else {
+          __bf16 h[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) h[j] = (__bf16)v[j];
+          uint4 u; __builtin_memcpy(&u, h, 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(p.d_out) + off) = u;
+        }
+      }
+    }
+    // 4. output-bias gradient column partials (fixed order over rows)
+    if (p.db_part && c.tid < GT_BN) {
+      float s = 0.f;
+      const int nl = c.tid;
+      for (int ml = 0; ml < GT_BM; ++ml)
+        if ((bits[ml * 4 + (nl >> 5)] >> (nl & 31)) & 1u) s += Y[ml * YS + nl];
+      p.db_part[(int64_t)c.tile_m * p.ld_db + c.n0 + nl] = s * p.gscale;
+    }
+    // 5. loss / metric partials
+    red[c.tid] = sse;
+    red[GT_THREADS + c.tid] = sae;
+    red[2 * GT_THREADS + c.tid] = cnt;
+    __syncthreads();
+    for (int s = GT_THREADS / 2; s > 0; s >>= 1) {
+      if (c.tid < s) {
+        red[c.tid] += red[c.tid + s];
+        red[GT_THREADS + c.tid] += red[GT_THREADS + c.tid + s];
+        red[2 * GT_THREADS + c.tid] += red[2 * GT_THREADS + c.tid + s];
+      }
+      __syncthreads();
+    }
+    const int gm = sh.M / GT_BM;
+    if (c.tid == 0) {
+      float* sp = p.stats_part + ((int64_t)c.tile_n * gm + c.tile_m) * 4;
+      sp[0] = red[0];
+      sp[1] = red[GT_THREADS];
+      sp[2] = red[2 * GT_THREADS];
+      sp[3] = 0.f;
+    }
+    if (p.row_sse_part && c.tid < GT_BM)
+      p.row_sse_part[(int64_t)c.tile_n * sh.M + c.m0 + c.tid] = rsse[c.tid];
+  }
+};
+
+}  // namespace ocf

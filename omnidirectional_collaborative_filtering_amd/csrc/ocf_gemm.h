@@ -1,0 +1,300 @@
+// LDS-staged MFMA GEMM template for gfx950 (CDNA4), 64-wide waves.
+//
+//   C[M,N] (+)= A[M,K] * B[K,N]      fp32 accumulate, epilogue fused per tile
+//
+// Operands arrive in either of two global layouts and are staged to LDS images the MFMA
+// fragments read directly:
+//   "row" image  [R][BK]  (K contiguous)  <- A stored [M][K] / B stored [N][K]
+//                fragment = ds_read_b128                         (f16/bf16: 8 k per lane)
+//   "col" image  [BK][R]  (R contiguous)  <- A stored [K][M] / B stored [K][N]
+//                fragment = 2 x ds_read_b64_tr_b16 (CDNA4 transposing LDS read)
+// so no operand is ever transposed in HBM or in registers.  Source element type may differ from
+// the compute type (fp32 master weights are converted to f16/bf16 while staging).
+//
+// Tile 128x128, 256 threads = 4 waves in 2x2, each wave 64x64 = 2x2 blocks of
+// v_mfma_f32_32x32x16_{f16,bf16} (BK = 64) or v_mfma_f32_32x32x2_f32 (BK = 32, exact-f32 mode).
+// Register-prefetch double buffering: one barrier per K-step (cdna_hip_programming.md T14).
+#pragma once
+#include "ocf_common.h"
+
+namespace ocf {
+
+constexpr int GT_BM = 128;
+constexpr int GT_BN = 128;
+constexpr int GT_THREADS = 256;
+
+template <typename CT> struct KInfo { static constexpr int BK = 64; };
+template <> struct KInfo<float> { static constexpr int BK = 32; };
+
+// byte strides of the two LDS image kinds (see bank analysis in DESIGN.md):
+//   row image: BK*s + 16  -> 144 B = 9 x 16-B slots (odd): ds_read_b128 conflict-free
+//   col image: R*s + 64   -> rows 16 banks apart: ds_read_b64_tr_b16 conflict-free (f16/bf16)
+template <typename CT, int R, bool COL> struct Img {
+  static constexpr int BK = KInfo<CT>::BK;
+  static constexpr int ES = (int)sizeof(CT);
+  static constexpr int STRIDE = COL ? (R * ES + (ES == 2 ? 64 : 16)) : (BK * ES + 16);
+  static constexpr int BYTES = COL ? BK * STRIDE : R * STRIDE;
+};
+
+// ---------------------------------------------------------------------------------------
+// global -> register -> LDS staging of one operand tile (R rows of the M/N dim x BK)
+template <typename GT, typename CT, int R, bool COL> struct Stager {
+  static constexpr int BK = KInfo<CT>::BK;
+  static constexpr int CHUNKS = R * BK / 8;  // 8 elements per chunk
+  static constexpr int NCH = CHUNKS / GT_THREADS;
+  static_assert(NCH * GT_THREADS == CHUNKS, "tile/threads mismatch");
+  GT v[NCH][8];
+
+  // src points at element (rdim=0, k=0) of this tile; ld in elements
+  __device__ __forceinline__ void load(const GT* __restrict__ src, int64_t ld, int tid) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = tid + i * GT_THREADS;
+      const GT* p;
+      if (!COL) {  // [R][K] k-contiguous; chunk = 8 consecutive k of one row
+        int r = c / (BK / 8), kc = c % (BK / 8);
+        p = src + (int64_t)r * ld + kc * 8;
+      } else {  // [K][R] r-contiguous; chunk = 8 consecutive r of one k
+        int k = c / (R / 8), rc = c % (R / 8);
+        p = src + (int64_t)k * ld + rc * 8;
+      }
+      if constexpr (sizeof(GT) == 4) {
+        float4 a = *reinterpret_cast<const float4*>(p);
+        float4 b = *reinterpret_cast<const float4*>(p + 4);
+        v[i][0] = a.x; v[i][1] = a.y; v[i][2] = a.z; v[i][3] = a.w;
+        v[i][4] = b.x; v[i][5] = b.y; v[i][6] = b.z; v[i][7] = b.w;
+      } else {
+        uint4 a = *reinterpret_cast<const uint4*>(p);
+        __builtin_memcpy(&v[i][0], &a, 16);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(char* img, int tid) const {
+    using I = Img<CT, R, COL>;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = tid + i * GT_THREADS;
+      char* dst;
+      if (!COL) {
+        int r = c / (BK / 8), kc = c % (BK / 8);
+        dst = img + r * I::STRIDE + kc * 8 * (int)sizeof(CT);
+      } else {
+        int k = c / (R / 8), rc = c % (R / 8);
+        dst = img + k * I::STRIDE + rc * 8 * (int)sizeof(CT);
+      }
+      CT o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = CvtT<CT>::to((float)v[i][j]);
+      if constexpr (sizeof(CT) == 2) {
+        uint4 w;
+        __builtin_memcpy(&w, o, 16);
+        *reinterpret_cast<uint4*>(dst) = w;
+      } else {
+        float4 a = make_float4(o[0], o[1], o[2], o[3]);
+        float4 b = make_float4(o[4], o[5], o[6], o[7]);
+        reinterpret_cast<float4*>(dst)[0] = a;
+        reinterpret_cast<float4*>(dst)[1] = b;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// MFMA fragment readers
+template <typename CT> struct Frag;
+template <> struct Frag<_Float16> { using T = ocf_h8; };
+template <> struct Frag<__bf16> { using T = ocf_b8; };
+
+// f16/bf16: k-substep ks (16 k), block of 32 rows starting at rb within the image
+template <typename CT, int R, bool COL>
+__device__ __forceinline__ typename Frag<CT>::T read_frag16(const char* img, int rb, int ks, int lane) {
+  using I = Img<CT, R, COL>;
+  typename Frag<CT>::T f;
+  if constexpr (!COL) {
+    const char* p = img + (rb + (lane & 31)) * I::STRIDE + (16 * ks + 8 * (lane >> 5)) * 2;
+    uint4 w = *reinterpret_cast<const uint4*>(p);
+    __builtin_memcpy(&f, &w, 16);
+  } else {
+    // 16-lane group g reads a 4(k) x 16(r) block; lane 4q+p addresses row q, cols 4p..4p+3
+    int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    int r0 = rb + 16 * (g & 1);
+    int k0 = 16 * ks + 8 * (g >> 1);
+    const char* p = img + (k0 + q) * I::STRIDE + (r0 + 4 * pp) * 2;
+    ocf_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) ocf_s4*)(size_t)(p));
+    ocf_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) ocf_s4*)(size_t)(p + 4 * I::STRIDE));
+    short s8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    __builtin_memcpy(&f, s8, 16);
+  }
+  return f;
+}
+
+// f32: the whole BK=32 slice for one lane: 16 values, substep s uses element s
+// (k index of (lane half h, substep s) is 16h + s -- same map for A and B)
+template <int R, bool COL>
+__device__ __forceinline__ void read_frag32(const char* img, int rb, int lane, float (&out)[16]) {
+  using I = Img<float, R, COL>;
+  int r = lane & 31, h = lane >> 5;
+  if constexpr (!COL) {
+    const char* p = img + (rb + r) * I::STRIDE + 16 * h * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 w = reinterpret_cast<const float4*>(p)[q];
+      out[4 * q + 0] = w.x; out[4 * q + 1] = w.y; out[4 * q + 2] = w.z; out[4 * q + 3] = w.w;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+      out[s] = *reinterpret_cast<const float*>(img + (16 * h + s) * I::STRIDE + (rb + r) * 4);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// accumulator element -> (row, col) within the wave's 64x64 sub-tile
+__device__ __forceinline__ int acc_row(int bi, int reg, int lane) {
+  return 32 * bi + (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+__device__ __forceinline__ int acc_col(int bj, int lane) { return 32 * bj + (lane & 31); }
+
+struct TileCtx {
+  int m0, n0;    // tile origin (global)
+  int wm, wn;    // wave origin within the tile (0 or 64)
+  int lane, tid;
+  int split;     // split-K index
+  int tile_m, tile_n;
+  char* lds;     // LDS scratch (operand buffers are free at epilogue time)
+};
+
+struct GemmShape {
+  const void* A;
+  const void* B;
+  int64_t lda, ldb;
+  int M, N, K;
+  int kchunk;    // K elements per split (multiple of BK)
+  int order;     // 0: n-fastest tile order, 1: m-fastest (XCD-local neighbours)
+};
+
+template <typename CT, bool ACOL, bool BCOL, typename AGT, typename BGT> struct GemmCfg {
+  using ImgA = Img<CT, GT_BM, ACOL>;
+  using ImgB = Img<CT, GT_BN, BCOL>;
+  static constexpr int BK = KInfo<CT>::BK;
+  static constexpr int BUF = ImgA::BYTES + ImgB::BYTES;
+  static constexpr int OPER_LDS = 2 * BUF;
+};
+
+// bijective XCD-aware remap (cdna_hip_programming.md T1): blocks with the same id % 8 run on
+// one XCD; give each such class a contiguous range of logical tiles.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+template <typename CT, bool ACOL, bool BCOL, typename AGT, typename BGT, class Epi, int LDS_BYTES>
+__global__ void __launch_bounds__(GT_THREADS)
+gemm_kernel(GemmShape sh, typename Epi::Params ep) {
+  using Cfg = GemmCfg<CT, ACOL, BCOL, AGT, BGT>;
+  constexpr int BK = Cfg::BK;
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int gm = sh.M / GT_BM, gn = sh.N / GT_BN;
+  const int ntile = gm * gn;
+  const int nwg = ntile * gridDim.y;
+  const int lin = xcd_remap(blockIdx.x + gridDim.x * blockIdx.y, nwg);
+  const int split = lin / ntile;
+  const int t = lin % ntile;
+  const int tile_m = sh.order ? (t % gm) : (t / gn);
+  const int tile_n = sh.order ? (t / gm) : (t % gn);
+  const int m0 = tile_m * GT_BM, n0 = tile_n * GT_BN;
+  const int k_begin = split * sh.kchunk;
+  int k_end = k_begin + sh.kchunk;
+  if (k_end > sh.K) k_end = sh.K;
+  const int nk = (k_end - k_begin) / BK;
+
+  const AGT* Ag = reinterpret_cast<const AGT*>(sh.A);
+  const BGT* Bg = reinterpret_cast<const BGT*>(sh.B);
+  // tile origin pointers; advance per K-step
+  auto a_ptr = [&](int k) -> const AGT* {
+    return ACOL ? Ag + (int64_t)k * sh.lda + m0 : Ag + (int64_t)m0 * sh.lda + k;
+  };
+  auto b_ptr = [&](int k) -> const BGT* {
+    return BCOL ? Bg + (int64_t)k * sh.ldb + n0 : Bg + (int64_t)n0 * sh.ldb + k;
+  };
+
+  Stager<AGT, CT, GT_BM, ACOL> sa;
+  Stager<BGT, CT, GT_BN, BCOL> sb;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  ocf_f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    sa.load(a_ptr(k_begin), sh.lda, tid);
+    sb.load(b_ptr(k_begin), sh.ldb, tid);
+    sa.store(lds, tid);
+    sb.store(lds + Cfg::ImgA::BYTES, tid);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* bufA = lds + (kt & 1) * Cfg::BUF;
+    const char* bufB = bufA + Cfg::ImgA::BYTES;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(a_ptr(k_begin + (kt + 1) * BK), sh.lda, tid);
+      sb.load(b_ptr(k_begin + (kt + 1) * BK), sh.ldb, tid);
+    }
+    if constexpr (sizeof(CT) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        typename Frag<CT>::T fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = read_frag16<CT, GT_BM, ACOL>(bufA, wm + 32 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = read_frag16<CT, GT_BN, BCOL>(bufB, wn + 32 * j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if constexpr (std::is_same<CT, _Float16>::value)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          }
+      }
+    } else {
+      float fa[2][16], fb[2][16];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) read_frag32<GT_BM, ACOL>(bufA, wm + 32 * i, lane, fa[i]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) read_frag32<GT_BN, BCOL>(bufB, wn + 32 * j, lane, fb[j]);
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* nb = lds + ((kt + 1) & 1) * Cfg::BUF;
+      sa.store(nb, tid);
+      sb.store(nb + Cfg::ImgA::BYTES, tid);
+    }
+    __syncthreads();
+  }
+
+  TileCtx c;
+  c.m0 = m0; c.n0 = n0; c.wm = wm; c.wn = wn; c.lane = lane; c.tid = tid;
+  c.split = split; c.tile_m = tile_m; c.tile_n = tile_n; c.lds = lds;
+  Epi::apply(ep, acc, c, sh);
+}
+
+}  // namespace ocf

@@ -1,0 +1,124 @@
+// ocf_gemm: dispatch of the MFMA GEMM template to the layout / dtype / epilogue combinations the
+// autoencoder step uses ("GEMM inventory").
+#include <algorithm>
+
+#include "ocf_epilogues.h"
+#include "ocf_internal.h"
+
+using namespace ocf;
+
+namespace {
+
+template <typename CT, bool ACOL, bool BCOL, typename BGT, class Epi>
+void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s) {
+  using Cfg = GemmCfg<CT, ACOL, BCOL, CT, BGT>;
+  constexpr int LDS = std::max(Cfg::OPER_LDS, Epi::LDS_NEED);
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  GemmShape sh;
+  sh.A = g.A; sh.B = g.B; sh.lda = g.lda; sh.ldb = g.ldb;
+  sh.M = g.M; sh.N = g.N; sh.K = g.K; sh.order = g.order;
+  const int splits = std::max(1, g.splits);
+  const int ksteps = g.K / Cfg::BK;
+  const int per = (ksteps + splits - 1) / splits;
+  sh.kchunk = per * Cfg::BK;
+  const int ntile = (g.M / GT_BM) * (g.N / GT_BN);
+  hipLaunchKernelGGL((gemm_kernel<CT, ACOL, BCOL, CT, BGT, Epi, LDS>), dim3(ntile, splits), dim3(GT_THREADS), 0, s, sh, ep);
+  OCF_HIP(hipGetLastError());
+}
+
+BiasActParams bias_act_params(const OcfGemmArgs& g) {
+  BiasActParams p;
+  p.bias = g.bias; p.act = g.act; p.keep = g.keep; p.seed = g.seed; p.stream = g.stream;
+  p.mask_in = g.mask_in; p.mask_out = g.mask_out; p.a_out = g.a_out; p.h_out = g.h_out; p.h_dtype = g.h_dtype;
+  p.ld = g.ld_out; p.m_real = g.m_real; p.n_real = g.n_real;
+  return p;
+}
+
+template <typename CT>
+void dispatch(const OcfGemmArgs& g, hipStream_t s) {
+  const bool b_f32 = g.b_dtype == OCF_F32;
+  if (!g.a_col && g.b_col) {
+    OCF_CHECK(b_f32, "ocf_gemm: [M][K] x [K][N] requires fp32 B (master weights)");
+    switch (g.epi) {
+      case OCF_EPI_SLAB: {
+        EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
+        launch<CT, false, true, float, EpiSlab>(g, p, s);
+      } break;
+      case OCF_EPI_BIAS_ACT:
+        launch<CT, false, true, float, EpiBiasAct>(g, bias_act_params(g), s);
+        break;
+      case OCF_EPI_PREDICT: {
+        EpiPredict::Params p{g.bias, g.pmask, g.ld_pmask, g.out, g.ld_out, g.m_real, g.n_real};
+        launch<CT, false, true, float, EpiPredict>(g, p, s);
+      } break;
+      case OCF_EPI_MASKED_MSE: {
+        EpiMaskedMSE::Params p;
+        p.bias = g.bias; p.bk_ptr = g.bk_ptr; p.bk_rc = g.bk_rc; p.bk_t = g.bk_t; p.bk_m = g.bk_m;
+        p.d_out = g.h_out; p.d_dtype = g.h_dtype; p.ld_d = g.ld_out; p.db_part = g.db_part; p.ld_db = g.ld_db;
+        p.gscale = g.opt.gscale; p.stats_part = g.stats_part; p.row_sse_part = g.row_sse_part;
+        OCF_CHECK(g.stats_part && g.bk_ptr, "ocf_gemm MASKED_MSE: stats_part / buckets required");
+        launch<CT, false, true, float, EpiMaskedMSE>(g, p, s);
+      } break;
+      default:
+        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[M][K] x B[K][N]");
+    }
+  } else if (!g.a_col && !g.b_col) {
+    OCF_CHECK(b_f32, "ocf_gemm: [M][K] x [N][K] requires fp32 B (master weights)");
+    switch (g.epi) {
+      case OCF_EPI_SLAB: {
+        EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
+        launch<CT, false, false, float, EpiSlab>(g, p, s);
+      } break;
+      case OCF_EPI_GRAD_ACT: {
+        GradActParams p;
+        p.a = g.a_in; p.mask = g.mask_in; p.keep = g.keep; p.act = g.act; p.d_out = g.h_out; p.d_dtype = g.h_dtype;
+        p.ld = g.ld_out; p.db_part = g.db_part; p.gscale = g.opt.gscale; p.m_real = g.m_real; p.n_real = g.n_real;
+        OCF_CHECK(g.a_in && g.h_out, "ocf_gemm GRAD_ACT: a_in / h_out required");
+        launch<CT, false, false, float, EpiGradAct>(g, p, s);
+      } break;
+      default:
+        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[M][K] x B[N][K]");
+    }
+  } else if (g.a_col && g.b_col) {
+    OCF_CHECK(g.b_dtype == g.compute_dtype, "ocf_gemm: [K][M] x [K][N] requires B in the compute dtype");
+    switch (g.epi) {
+      case OCF_EPI_OPTIM: {
+        EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt};
+        OCF_CHECK(g.p != nullptr, "ocf_gemm OPTIM: p required");
+        launch<CT, true, true, CT, EpiOptim>(g, p, s);
+      } break;
+      case OCF_EPI_GRAD: {
+        EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale};
+        launch<CT, true, true, CT, EpiGradStore>(g, p, s);
+      } break;
+      default:
+        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[K][M] x B[K][N]");
+    }
+  } else {
+    throw std::runtime_error("ocf_gemm: layout A[K][M] x B[N][K] not instantiated");
+  }
+}
+
+}  // namespace
+
+extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfGemmArgs& g = *args;
+  OCF_CHECK(g.A && g.B, "ocf_gemm: null operand");
+  OCF_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "ocf_gemm: empty shape");
+  OCF_CHECK(g.M % GT_BM == 0 && g.N % GT_BN == 0, "ocf_gemm: M and N must be multiples of 128");
+  const int bk = g.compute_dtype == OCF_F32 ? 32 : 64;
+  OCF_CHECK(g.K % bk == 0, "ocf_gemm: K must be a multiple of 64 (f16/bf16) or 32 (f32)");
+  OCF_CHECK(g.a_dtype == g.compute_dtype, "ocf_gemm: A must be in the compute dtype");
+  OCF_CHECK(g.lda % 8 == 0 && g.ldb % 8 == 0, "ocf_gemm: leading dimensions must be multiples of 8");
+  OCF_CHECK(g.splits >= 1, "ocf_gemm: splits >= 1");
+  OCF_CHECK(g.splits == 1 || g.epi == OCF_EPI_SLAB, "ocf_gemm: split-K only with the SLAB epilogue");
+  hipStream_t s = (hipStream_t)stream;
+  switch (g.compute_dtype) {
+    case OCF_F16: dispatch<_Float16>(g, s); break;
+    case OCF_BF16: dispatch<__bf16>(g, s); break;
+    case OCF_F32: dispatch<float>(g, s); break;
+    default: throw std::runtime_error("ocf_gemm: bad compute dtype");
+  }
+  OCF_TRY_END
+}

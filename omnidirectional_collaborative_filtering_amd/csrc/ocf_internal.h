@@ -1,0 +1,35 @@
+// Internal glue: public ABI structs, error handling.
+#pragma once
+#include <exception>
+#include <stdexcept>
+#include <string>
+
+#include "../../include/ocf.h"
+#include "ocf_common.h"
+
+namespace ocf {
+using ScatterArgs = OcfScatterArgs;
+void set_error(const std::string& msg);
+}  // namespace ocf
+
+#define OCF_TRY_BEGIN try {
+#define OCF_TRY_END                                       \
+  return 0;                                               \
+  }                                                       \
+  catch (const std::exception& e) {                       \
+    ocf::set_error(e.what());                             \
+    return 1;                                             \
+  }
+
+#define OCF_CHECK(cond, msg)                              \
+  do {                                                    \
+    if (!(cond)) throw std::runtime_error(msg);           \
+  } while (0)
+
+#define OCF_HIP(expr)                                                               \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));     \
+  } while (0)

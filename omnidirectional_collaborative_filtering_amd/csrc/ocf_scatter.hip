@@ -1,0 +1,301 @@
+// K1: sparse-rating -> dense-batch assembly (replaces data_reader.py:95-298).
+//
+// One workgroup per batch row.  The dataset lives in HBM as row-CSR in the reference's list
+// order (row_ptr int64, col int32 = dense column index, val f32) plus an optional duplicate
+// chain dup[e] = next entry of the same row with the same column (or -1), so that the
+// reference's last-write-wins per array (data_reader.py:158-166, 250-266) is reproduced by a
+// parallel scatter: an entry writes a *value* array only if no later entry of its chain
+// writes that array.  Mask arrays all receive the same constant (aux) so they need no check.
+//
+// Entry roles:
+//   train  (mode 0): input  = keep (reciprocal split, data_reader.py:130,158)
+//                    target = !keep || pass_through (:161-166)
+//   eval   (mode 1): source-1 entries are inputs only (:234-252),
+//                    source-2 entries are targets only (:256-268)
+// Outputs (all optional): dense f32 X / M_in / M_out / T / M_miss (the data_gen API arrays),
+// the concatenated layer-0 input in the compute dtype, and the target entries bucketed by
+// 128-column tile for the fused masked-MSE epilogue.
+#include "ocf_internal.h"
+
+namespace ocf {
+
+struct EntryCtx {
+  const ScatterArgs* a;
+  int b;          // batch row
+  int64_t rs1;    // CSR row start in source 1 (or -1)
+  int64_t bo1;    // batch-local offset of this row's first source-1 entry
+};
+
+__device__ __forceinline__ float reciprocal_cut(float s) { return (1.0f - s) / ((1.0f - s) + s); }
+
+__device__ __forceinline__ bool keep_of(const ScatterArgs& a, int b, int64_t local_j, int64_t bo1, float cut) {
+  if (a.keep1) return a.keep1[bo1 + local_j] != 0;
+  if (a.s0 >= 1.0f) return true;
+  float u = philox_uniform(a.seed, a.stream + 1, (uint64_t)(bo1 + local_j));
+  return u >= cut;
+}
+
+__device__ __forceinline__ float row_cut(const ScatterArgs& a, int b) {
+  if (a.keep1 || a.s0 >= 1.0f) return 0.f;
+  float s = a.s0 + (a.s1 - a.s0) * philox_uniform(a.seed, a.stream, (uint64_t)b);
+  return reciprocal_cut(s);
+}
+
+// role bits: 1 = input, 2 = target
+__device__ __forceinline__ int role1(const ScatterArgs& a, int b, int64_t local_j, int64_t bo1, float cut) {
+  if (a.mode == 1) return 1;
+  bool k = keep_of(a, b, local_j, bo1, cut);
+  return (k ? 1 : 0) | ((!k || a.pass_through) ? 2 : 0);
+}
+
+__device__ __forceinline__ void store_val(void* base, int dtype, int64_t idx, float v) {
+  if (dtype == OCF_F32) reinterpret_cast<float*>(base)[idx] = v;
+  else if (dtype == OCF_F16) reinterpret_cast<_Float16*>(base)[idx] = (_Float16)v;
+  else reinterpret_cast<__bf16*>(base)[idx] = (__bf16)v;
+}
+
+__device__ __forceinline__ void zero_row(void* base, int esize, int64_t ld, int b, int tid) {
+  if (!base) return;
+  char* row = reinterpret_cast<char*>(base) + (int64_t)b * ld * esize;
+  int64_t bytes = ld * esize;             // callers guarantee 16-B multiple rows
+  uint4 z = make_uint4(0, 0, 0, 0);
+  for (int64_t o = (int64_t)tid * 16; o < bytes; o += (int64_t)blockDim.x * 16)
+    *reinterpret_cast<uint4*>(row + o) = z;
+}
+
+__global__ void __launch_bounds__(256) scatter_rows_kernel(ScatterArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  // 1. zero this row of every requested output
+  zero_row(a.X, 4, a.ld, b, tid);
+  zero_row(a.Min, 4, a.ld, b, tid);
+  zero_row(a.Mout, 4, a.ld, b, tid);
+  zero_row(a.T, 4, a.ld, b, tid);
+  zero_row(a.Mmiss, 4, a.ld, b, tid);
+  zero_row(a.xin, a.xin_dtype == OCF_F32 ? 4 : 2, a.xin_ld, b, tid);
+  __syncthreads();   // s_waitcnt vmcnt(0) + s_barrier: zero stores complete before scatter stores
+  if (b >= a.B) return;
+  const float aux = a.aux;
+  const int64_t xb = a.xin_block;
+
+  // 2. source 1
+  int r1 = a.rows1 ? a.rows1[b] : -1;
+  if (r1 >= 0) {
+    const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
+    const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
+    const float cut = row_cut(a, b);
+    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+      const int c = a.col1[i];
+      const float v = a.val1[i];
+      const int role = role1(a, b, i - s, bo1, cut);
+      // later duplicates of the same column that also write the value arrays
+      bool later_in = false, later_tg = false;
+      if (a.dup1) {
+        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) {
+          int rf = role1(a, b, f - s, bo1, cut);
+          later_in |= (rf & 1) != 0;
+          later_tg |= (rf & 2) != 0;
+        }
+      }
+      const int64_t o = (int64_t)b * a.ld + c;
+      const int64_t ox = (int64_t)b * a.xin_ld + c;
+      if (role & 1) {
+        if (a.Min) a.Min[o] = aux;
+        if (!later_in) {
+          if (a.X) a.X[o] = v;
+          if (a.xin) store_val(a.xin, a.xin_dtype, ox, v);
+        }
+        if (a.xin && a.feed == 1) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+      }
+      if (role & 2) {
+        if (a.Mout) a.Mout[o] = aux;
+        if (!later_tg && a.T) a.T[o] = v;
+        if (!later_tg && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
+      }
+      if (a.Mmiss) a.Mmiss[o] = aux;
+      if (a.xin) {
+        if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+        if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
+      }
+    }
+  }
+  // 3. source 2 (eval targets)
+  int r2 = a.rows2 ? a.rows2[b] : -1;
+  if (r2 >= 0) {
+    const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
+    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+      const int c = a.col2[i];
+      const float v = a.val2[i];
+      const bool dead = a.dup2 && a.dup2[i] >= 0;   // every source-2 entry is a target
+      const int64_t o = (int64_t)b * a.ld + c;
+      const int64_t ox = (int64_t)b * a.xin_ld + c;
+      if (a.Mout) a.Mout[o] = aux;
+      if (!dead && a.T) a.T[o] = v;
+      if (!dead && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
+      if (a.Mmiss) a.Mmiss[o] = aux;
+      if (a.xin) {
+        if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+        if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
+      }
+    }
+  }
+}
+
+// exclusive scan of per-tile target counts -> bucket pointers; resets counts for next batch
+__global__ void __launch_bounds__(1024) bucket_scan_kernel(int* tile_cnt, int* bk_ptr, int* bk_cur, int n_tiles) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  const int per = (n_tiles + 1023) / 1024;
+  const int lo = tid * per;
+  int hi = lo + per;
+  if (hi > n_tiles) hi = n_tiles;
+  int s = 0;
+  for (int i = lo; i < hi; ++i) s += tile_cnt[i];
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan
+    int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int run = tid ? part[tid - 1] : 0;
+  for (int i = lo; i < hi; ++i) {
+    bk_ptr[i] = run;
+    bk_cur[i] = run;
+    run += tile_cnt[i];
+    tile_cnt[i] = 0;
+  }
+  if (tid == 1023) bk_ptr[n_tiles] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) bucket_fill_kernel(ScatterArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b >= a.B) return;
+  int r1 = a.rows1 ? a.rows1[b] : -1;
+  if (r1 >= 0 && a.mode == 0) {
+    const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
+    const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
+    const float cut = row_cut(a, b);
+    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+      const int role = role1(a, b, i - s, bo1, cut);
+      if (!(role & 2)) continue;
+      bool later_tg = false;
+      if (a.dup1)
+        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) later_tg |= (role1(a, b, f - s, bo1, cut) & 2) != 0;
+      if (later_tg) continue;
+      const int c = a.col1[i];
+      int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
+      a.bk_rc[slot] = (b << 7) | (c & 127);
+      a.bk_t[slot] = a.val1[i];
+      a.bk_m[slot] = a.aux;
+    }
+  }
+  int r2 = a.rows2 ? a.rows2[b] : -1;
+  if (r2 >= 0) {
+    const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
+    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+      if (a.dup2 && a.dup2[i] >= 0) continue;
+      const int c = a.col2[i];
+      int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
+      a.bk_rc[slot] = (b << 7) | (c & 127);
+      a.bk_t[slot] = a.val2[i];
+      a.bk_m[slot] = a.aux;
+    }
+  }
+}
+
+// ---- targets given as dense arrays (Model.train_on_batch / evaluate on user arrays) -----
+// entry wherever T != 0 or M != 0, with its own (t, m)
+__global__ void dense_targets_count_kernel(const float* T, const float* M, int64_t ld, int B, int N, int* tile_cnt) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t tot = (int64_t)B * N;
+  if (i >= tot) return;
+  int b = (int)(i / N), n = (int)(i % N);
+  int64_t o = (int64_t)b * ld + n;
+  if (T[o] != 0.f || M[o] != 0.f) atomicAdd(&tile_cnt[n >> 7], 1);
+}
+__global__ void dense_targets_fill_kernel(const float* T, const float* M, int64_t ld, int B, int N, int* bk_cur,
+                                          int* bk_rc, float* bk_t, float* bk_m) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t tot = (int64_t)B * N;
+  if (i >= tot) return;
+  int b = (int)(i / N), n = (int)(i % N);
+  int64_t o = (int64_t)b * ld + n;
+  float t = T[o], m = M[o];
+  if (t != 0.f || m != 0.f) {
+    int slot = atomicAdd(&bk_cur[n >> 7], 1);
+    bk_rc[slot] = (b << 7) | (n & 127);
+    bk_t[slot] = t;
+    bk_m[slot] = m;
+  }
+}
+
+// pack dense f32 inputs [B][ld_src] (k blocks) into the compute-dtype layer-0 input
+__global__ void pack_input_kernel(const float* s0, const float* s1, const float* s2, int64_t ld_src, int B, int N,
+                                  void* xin, int dtype, int64_t xin_ld, int64_t xin_block, int B_pad) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t tot = (int64_t)B_pad * xin_ld;
+  if (i >= tot) return;
+  int b = (int)(i / xin_ld);
+  int64_t j = i % xin_ld;
+  int blk = (int)(j / xin_block);
+  int64_t n = j % xin_block;
+  float v = 0.f;
+  const float* src = blk == 0 ? s0 : (blk == 1 ? s1 : s2);
+  if (b < B && n < N && src) v = src[(int64_t)b * ld_src + n];
+  store_val(xin, dtype, i, v);
+}
+
+}  // namespace ocf
+
+using namespace ocf;
+
+extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const ScatterArgs& a = *args;
+  hipStream_t s = (hipStream_t)stream;
+  OCF_CHECK(a.B >= 0 && a.B <= a.B_pad, "ocf_scatter_batch: need 0 <= B <= B_pad");
+  OCF_CHECK(a.mode == 0 || a.mode == 1, "ocf_scatter_batch: mode must be 0 (train) or 1 (eval)");
+  OCF_CHECK((a.ld * 4) % 16 == 0, "ocf_scatter_batch: dense ld must be a multiple of 4 floats");
+  if (a.xin) OCF_CHECK((a.xin_ld * (a.xin_dtype == OCF_F32 ? 4 : 2)) % 16 == 0, "ocf_scatter_batch: xin ld alignment");
+  if (a.tile_cnt) OCF_CHECK(a.bk_ptr && a.bk_cur && a.bk_rc && a.bk_t && a.bk_m && a.n_tiles > 0,
+                            "ocf_scatter_batch: bucket outputs incomplete");
+  if (a.B_pad == 0) return 0;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(a.B_pad), dim3(256), 0, s, a);
+  OCF_HIP(hipGetLastError());
+  if (a.tile_cnt) {
+    hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, a.tile_cnt, a.bk_ptr, a.bk_cur, a.n_tiles);
+    OCF_HIP(hipGetLastError());
+    if (a.B > 0) hipLaunchKernelGGL(bucket_fill_kernel, dim3(a.B), dim3(256), 0, s, a);
+    OCF_HIP(hipGetLastError());
+  }
+  OCF_TRY_END
+}
+
+extern "C" int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,
+                                 int* bk_ptr, int* bk_cur, int* bk_rc, float* bk_t, float* bk_m, void* stream) {
+  OCF_TRY_BEGIN
+  hipStream_t s = (hipStream_t)stream;
+  OCF_CHECK(T && M && tile_cnt && bk_ptr && bk_cur && bk_rc && bk_t && bk_m, "ocf_dense_targets: null pointer");
+  OCF_CHECK(n_tiles * 128 >= N, "ocf_dense_targets: n_tiles too small");
+  int64_t tot = (int64_t)B * N;
+  int grid = (int)((tot + 255) / 256);
+  if (tot > 0) hipLaunchKernelGGL(dense_targets_count_kernel, dim3(grid), dim3(256), 0, s, T, M, ld, B, N, tile_cnt);
+  hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, tile_cnt, bk_ptr, bk_cur, n_tiles);
+  if (tot > 0)
+    hipLaunchKernelGGL(dense_targets_fill_kernel, dim3(grid), dim3(256), 0, s, T, M, ld, B, N, bk_cur, bk_rc, bk_t, bk_m);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+extern "C" int ocf_pack_input(const float* s0, const float* s1, const float* s2, int64_t ld_src, int B, int N, void* xin,
+                              int dtype, int64_t xin_ld, int64_t xin_block, int B_pad, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(xin && s0, "ocf_pack_input: null pointer");
+  int64_t tot = (int64_t)B_pad * xin_ld;
+  if (tot == 0) return 0;
+  hipLaunchKernelGGL(pack_input_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, (hipStream_t)stream, s0, s1, s2,
+                     ld_src, B, N, xin, dtype, xin_ld, xin_block, B_pad);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}

@@ -1,0 +1,236 @@
+"""Drop-in for the reference's ``data_reader`` (data_reader.py:11-419).
+
+Same constructor and ``data_gen`` signature; batches come out of the GPU scatter kernel (K1,
+``ocf_scatter_batch``) instead of a Python double loop over dicts.  Differences that are
+deliberate:
+
+* arrays are float32 CUDA tensors of shape [B, num_items] (the reference yields float64 NumPy
+  arrays that Keras immediately casts to float32);
+* the dataset is uploaded to HBM once as row-CSR (dataset.py); a batch never leaves the GPU;
+* the NumPy global RNG is consumed exactly as the reference consumes it (same permutation,
+  same ``uniform`` / ``choice`` draws -> bit-identical reciprocal masks).  The draws of a whole
+  training epoch are taken when the generator is first pulled: Keras 2.0.4's GeneratorEnqueuer
+  drains the generator ahead of ``fit_generator`` (queue of 10 > the one batch train.py leaves
+  unused), so every train draw precedes the validation permutation in the reference as well.
+  ``rng="device"`` instead draws reciprocal masks with Philox on the GPU (same distribution,
+  no host work) and skips the NumPy draws; with data_sparsity [1, 1] (train.py:28) both modes
+  give identical masks.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .dataset import FixedSplit, load_reference_json
+from .engine import TILE, cur_stream, ptr, ru
+
+AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
+
+
+class _DeviceCSR:
+    def __init__(self, csr, dev):
+        self.host = csr
+        self.rp = torch.as_tensor(csr.row_ptr, device=dev)
+        self.col = torch.as_tensor(csr.col, device=dev)
+        self.val = torch.as_tensor(csr.val, device=dev)
+        self.dup = None if csr.dup is None else torch.as_tensor(csr.dup, device=dev)
+        self.lens = csr.row_lengths()
+
+
+class data_reader(object):
+    """``data_reader(num_items, num_users, filepath, nonsequentialusers, use_json, eval_mode,
+    useTimestamps, reverse_user_item_data)`` (data_reader.py:12).  ``dataset=`` accepts a prebuilt
+    ``FixedSplit`` (or a path to its .npz) instead of the JSON files; ``rng`` selects the
+    reciprocal-mask RNG ('numpy' exact, or 'device')."""
+
+    def __init__(self, num_items, num_users, filepath=None, nonsequentialusers=False, use_json=True,
+                 eval_mode="ablation", useTimestamps=False, reverse_user_item_data=False, dataset=None,
+                 rng="numpy", device=None):
+        if useTimestamps:
+            raise NotImplementedError("useTimestamps: broken in the reference (data_reader.py:358-359 feeds the "
+                                      "whole dict); not supported")
+        if eval_mode != "fixed_split":
+            raise NotImplementedError("eval_mode='ablation' (split_for_validation) is out of scope; use fixed_split")
+        self.num_items = int(num_items)
+        self.num_users = int(num_users)
+        self.filepath = filepath
+        self.nonsequentialusers = nonsequentialusers
+        self.eval_mode = eval_mode
+        self.useTimestamps = False
+        self.rng = rng
+        if dataset is None:
+            dataset = load_reference_json(filepath, reverse_user_item_data, use_json)
+        elif isinstance(dataset, str):
+            dataset = FixedSplit.load(dataset)
+        self.data = dataset
+        if dataset.num_cols != self.num_items:
+            raise ValueError("num_items=%d but the data has %d columns" % (self.num_items, dataset.num_cols))
+        self.items_to_densevec = {c: i for i, c in enumerate(dataset.col_ids)}
+        self.densevec_to_items = {i: c for i, c in enumerate(dataset.col_ids)}
+        # data_reader.py:73-80
+        self.train_set = list(dataset.train.keys)
+        self.val_set = list(dataset.valid_tgt.keys)
+        self.test_set = list(dataset.test_tgt.keys)
+        self.train_set_size = len(self.train_set)
+        self.val_set_size = len(self.val_set)
+        self.test_set_size = len(self.test_set)
+        self.device = torch.device(device if device is not None else "cuda")
+        self._dev = None
+        print("Finished loading data")
+
+    def _on_device(self):
+        if self._dev is None:
+            d = self.device
+            self._dev = {k: _DeviceCSR(getattr(self.data, k), d)
+                         for k in ("train", "valid_in", "valid_tgt", "test_in", "test_tgt")}
+        return self._dev
+
+    def split_for_validation(self, val_split, seed=None):
+        raise NotImplementedError("ablation eval mode is out of scope")
+
+    def data_gen(self, batch_size, data_sparsity, train_val_test="train", shuffle=True,
+                 auxilliary_mask_type="dropout", aux_var_value=-1, return_target_count=False,
+                 sparse_representation=False, pass_through_input_training=False):
+        """data_reader.py:314-419 -- returns a generator object (also usable by Model's fast path)."""
+        if sparse_representation:
+            raise NotImplementedError("sparse_representation needs a patched Keras backend in the reference "
+                                      "(train.py:53); dense only")
+        if auxilliary_mask_type not in AUX_FEED:
+            raise ValueError("Auxilliary mask type %r doesn't exist" % (auxilliary_mask_type,))
+        return BatchGenerator(self, int(batch_size), data_sparsity, train_val_test, shuffle, auxilliary_mask_type,
+                              float(aux_var_value), return_target_count, bool(pass_through_input_training))
+
+
+class BatchGenerator(object):
+    """Lazy like the reference generator: nothing is drawn before the first pull."""
+
+    def __init__(self, reader, B, sparsity, split, shuffle, aux_type, aux, return_count, pass_through):
+        self.r = reader
+        self.B = B
+        self.sparsity = sparsity
+        self.split = split
+        self.shuffle = shuffle
+        self.aux_type = aux_type
+        self.aux = aux
+        self.return_count = return_count
+        self.pass_through = pass_through
+        self.keys = {"train": reader.train_set, "valid": reader.val_set, "test": reader.test_set}[split]
+        self.n = len(self.keys)
+        self.num_batches = self.n // B                                   # data_reader.py:329
+        self.i = 0
+        self.started = False
+        self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if reader.rng == "device" else 0
+
+    # ------------------------------------------------------------ epoch plan
+    def _start(self):
+        self.started = True
+        r = self.r
+        dev = r._on_device()
+        order = np.random.permutation(self.n) if self.shuffle else np.arange(self.n)   # :326-327
+        nb, B = self.num_batches, self.B
+        rows = order[: nb * B].reshape(nb, B).astype(np.int64)
+        self.rows_host = rows
+        if self.split == "train":
+            self.src1, self.src2 = dev["train"], None
+        elif self.split == "valid":
+            self.src1, self.src2 = dev["valid_in"], dev["valid_tgt"]
+        else:
+            self.src1, self.src2 = dev["test_in"], dev["test_tgt"]
+        lens1 = self.src1.lens[rows]                      # [nb, B]
+        boff = np.zeros((nb, B + 1), dtype=np.int64)
+        np.cumsum(lens1, axis=1, out=boff[:, 1:])
+        self.nnz1 = boff[:, -1].copy()
+        self.tcount = self.src2.lens[rows].sum(axis=1) if self.src2 is not None else None
+        self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
+        self.boff_dev = torch.as_tensor(boff, device=r.device)
+        self.keep_dev = None
+        self.keep_off = None
+        if self.split == "train" and r.rng == "numpy":
+            s0, s1 = float(self.sparsity[0]), float(self.sparsity[1])
+            keeps = []
+            for bi in range(nb):
+                s_rows = np.random.uniform(low=s0, high=s1, size=B)                    # :120
+                u = np.random.random_sample(int(self.nnz1[bi]))                         # :130, one call/batch
+                cut = (1.0 - s_rows) / ((1.0 - s_rows) + s_rows)
+                keeps.append(u >= np.repeat(cut, lens1[bi]))
+            if not (s0 >= 1.0 and s1 >= 1.0):
+                flat = np.concatenate(keeps) if keeps else np.zeros(0, bool)
+                self.keep_dev = torch.as_tensor(flat.astype(np.uint8), device=r.device)
+                self.keep_off = np.concatenate([[0], np.cumsum(self.nnz1)])
+        self.max_targets = int(max(self.nnz1.max() if nb else 0, self.tcount.max() if (self.tcount is not None and nb) else 0))
+
+    def scatter_args(self, bi, engine_args=None, dense=None, B_pad=None):
+        """OcfScatterArgs for batch bi (onto an engine's xin/buckets and/or dense outputs)."""
+        a = engine_args if engine_args is not None else _lib.OcfScatterArgs()
+        B = self.B
+        s1 = self.src1
+        a.rp1, a.col1, a.val1, a.dup1 = ptr(s1.rp), ptr(s1.col), ptr(s1.val), ptr(s1.dup)
+        a.rows1 = self.rows_dev.data_ptr() + 4 * bi * B
+        a.boff1 = self.boff_dev.data_ptr() + 8 * bi * (B + 1)
+        a.keep1 = None if self.keep_dev is None else self.keep_dev.data_ptr() + int(self.keep_off[bi])
+        if self.split == "train":
+            a.mode = 0
+            a.pass_through = int(self.pass_through)
+            if self.r.rng == "device":
+                a.s0, a.s1 = float(self.sparsity[0]), float(self.sparsity[1])
+                a.seed, a.stream = self.seed, 2 * (bi + 1)
+            else:
+                a.s0 = a.s1 = 1.0
+        else:
+            a.mode = 1
+            s2 = self.src2
+            a.rp2, a.col2, a.val2, a.dup2 = ptr(s2.rp), ptr(s2.col), ptr(s2.val), ptr(s2.dup)
+            a.rows2 = a.rows1
+        a.B = B
+        a.aux = self.aux
+        a.feed = AUX_FEED[self.aux_type]
+        a.both = int(self.aux_type == "both")
+        if dense is not None:
+            a.X, a.Min, a.Mout, a.T, a.Mmiss = [ptr(t) for t in dense]
+            a.ld = dense[0].stride(0)
+            a.B_pad = B_pad if B_pad is not None else B
+        return a
+
+    # ------------------------------------------------------------ fast path (Model.fit_generator)
+    def next_batch_index(self):
+        if not self.started:
+            self._start()
+        if self.i >= self.num_batches:
+            return None
+        bi = self.i
+        self.i += 1
+        return bi
+
+    def target_count(self, bi):
+        return int(self.tcount[bi]) if self.tcount is not None else None
+
+    # ------------------------------------------------------------ reference-compatible iteration
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        bi = self.next_batch_index()
+        if bi is None:
+            return None                                                                 # :418-419
+        B, N = self.B, self.r.num_items
+        ld = ru(N, 4)
+        buf = torch.empty(5, B, ld, device=self.r.device, dtype=torch.float32)
+        X, Min, Mout, T, Mmiss = buf[0], buf[1], buf[2], buf[3], buf[4]
+        a = self.scatter_args(bi, dense=(X, Min, Mout, T, Mmiss))
+        _lib.call("ocf_scatter_batch", a, cur_stream())
+        v = lambda t: t[:, :N]
+        x, m_in, m_out, t, m_miss = v(X), v(Min), v(Mout), v(T), v(Mmiss)
+        if self.aux_type is None:
+            inputs = [x, m_out]
+        else:
+            feed = {"causal": m_miss, "dropout": m_in, "both": m_in,
+                    "zeros": torch.zeros_like(m_in)}[self.aux_type]
+            inputs = [x, feed, m_out]
+            if self.aux_type == "both":
+                inputs.append(m_miss)
+        if self.split != "train" and self.return_count:
+            return inputs, t, self.target_count(bi)
+        return inputs, t
+
+    next = __next__   # py2-style gen.next() as used at train.py:233

@@ -1,0 +1,254 @@
+"""Host-side rating storage: row-CSR in the reference's list order.
+
+The reference keeps ratings as JSON dicts ``row_key -> [[col_raw_id, rating], ...]`` and maps
+column ids through ``items_to_densevec`` (data_reader.py:20-28, 85-92).  Here every split is
+converted once, at load time, into a row-CSR
+
+    row_ptr int64 [rows+1]   col int32 [nnz] (dense column index)   val float32 [nnz]
+
+whose per-row entry order is the dict's list order (so the j-th NumPy draw of
+``choice(..., size=len(list))`` still belongs to the j-th rating, data_reader.py:130-135), plus an
+optional duplicate chain (next entry of the same row with the same column) that lets the GPU
+scatter reproduce last-write-wins (data_reader.py:158-166).  Fixed-split data (eval_mode
+'fixed_split', data_reader.py:57-80) is a train CSR plus (input CSR, target CSR) pairs for valid
+and test, rows in target-dict key order.
+
+Also here: the rating-level 80/10/10 split of TrainValidTestSplit.py:74-103 (``split_ratings``), a
+synthetic generator shaped like the BASELINE configs, and a binary .npz cache format.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+
+def dup_chain(row_ptr: np.ndarray, col: np.ndarray) -> Optional[np.ndarray]:
+    """next[e] = next entry (CSR index) in the same row with the same column, else -1.
+    Returns None when the matrix has no duplicate (row, col) pairs."""
+    nnz = len(col)
+    if nnz == 0:
+        return None
+    rows = np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int64), np.diff(row_ptr))
+    key = rows * (int(col.max()) + 1) + col.astype(np.int64)
+    order = np.argsort(key, kind="stable")
+    ks = key[order]
+    same = ks[1:] == ks[:-1]
+    if not same.any():
+        return None
+    nxt = np.full(nnz, -1, dtype=np.int32)
+    nxt[order[:-1][same]] = order[1:][same].astype(np.int32)
+    return nxt
+
+
+@dataclass
+class RatingsCSR:
+    row_ptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+    keys: List = field(default_factory=list)
+    dup: Optional[np.ndarray] = None
+
+    @property
+    def n_rows(self):
+        return len(self.row_ptr) - 1
+
+    @property
+    def nnz(self):
+        return int(self.row_ptr[-1])
+
+    def row_lengths(self):
+        return np.diff(self.row_ptr)
+
+    @classmethod
+    def from_lists(cls, keys, lists, col_index):
+        """lists[i] = [[col_raw_id, rating], ...] or None (empty row)."""
+        lens = np.fromiter((0 if l is None else len(l) for l in lists), dtype=np.int64, count=len(lists))
+        rp = np.zeros(len(lists) + 1, dtype=np.int64)
+        np.cumsum(lens, out=rp[1:])
+        col = np.empty(int(rp[-1]), dtype=np.int32)
+        val = np.empty(int(rp[-1]), dtype=np.float32)
+        pos = 0
+        for l in lists:
+            if l is None:
+                continue
+            for cid, r in l:
+                col[pos] = lookup_col(col_index, cid)
+                val[pos] = r
+                pos += 1
+        c = cls(rp, col, val, list(keys))
+        c.dup = dup_chain(rp, col)
+        return c
+
+    @classmethod
+    def from_coo(cls, rows, cols, vals, n_rows, keys=None):
+        """rows need not be sorted; within a row the given order is kept (stable)."""
+        rows = np.asarray(rows, dtype=np.int64)
+        order = np.argsort(rows, kind="stable")
+        counts = np.bincount(rows, minlength=n_rows)
+        rp = np.zeros(n_rows + 1, dtype=np.int64)
+        np.cumsum(counts, out=rp[1:])
+        c = cls(rp, np.asarray(cols, dtype=np.int32)[order], np.asarray(vals, dtype=np.float32)[order],
+                list(range(n_rows)) if keys is None else list(keys))
+        c.dup = dup_chain(rp, c.col)
+        return c
+
+    def subset_rows(self, idx):
+        """Rows idx (negative = empty row) as a new CSR."""
+        idx = np.asarray(idx, dtype=np.int64)
+        lens = np.where(idx >= 0, self.row_ptr[np.maximum(idx, 0) + 1] - self.row_ptr[np.maximum(idx, 0)], 0)
+        rp = np.zeros(len(idx) + 1, dtype=np.int64)
+        np.cumsum(lens, out=rp[1:])
+        take = np.concatenate([np.arange(self.row_ptr[i], self.row_ptr[i + 1]) for i in idx if i >= 0]) \
+            if len(idx) else np.zeros(0, np.int64)
+        c = RatingsCSR(rp, self.col[take] if len(take) else np.zeros(0, np.int32),
+                       self.val[take] if len(take) else np.zeros(0, np.float32), [])
+        c.dup = dup_chain(rp, c.col)
+        return c
+
+
+def lookup_col(col_index, cid):
+    try:
+        return col_index[cid]
+    except KeyError:
+        return col_index[str(cid)]
+
+
+@dataclass
+class FixedSplit:
+    """eval_mode='fixed_split' data (data_reader.py:57-80)."""
+    num_cols: int
+    train: RatingsCSR
+    valid_in: RatingsCSR
+    valid_tgt: RatingsCSR
+    test_in: RatingsCSR
+    test_tgt: RatingsCSR
+    col_ids: List = field(default_factory=list)
+
+    def save(self, path):
+        arrs = {"num_cols": np.array(self.num_cols)}
+        for name in ("train", "valid_in", "valid_tgt", "test_in", "test_tgt"):
+            c = getattr(self, name)
+            arrs[name + "/row_ptr"] = c.row_ptr
+            arrs[name + "/col"] = c.col
+            arrs[name + "/val"] = c.val
+            arrs[name + "/keys"] = np.asarray([str(k) for k in c.keys])
+        np.savez(path, **arrs)
+
+    @classmethod
+    def load(cls, path):
+        z = np.load(path, allow_pickle=False)
+        parts = {}
+        for name in ("train", "valid_in", "valid_tgt", "test_in", "test_tgt"):
+            c = RatingsCSR(z[name + "/row_ptr"], z[name + "/col"], z[name + "/val"], list(z[name + "/keys"]))
+            c.dup = dup_chain(c.row_ptr, c.col)
+            parts[name] = c
+        return cls(int(z["num_cols"]), **parts)
+
+
+def load_reference_json(filepath, reverse_user_item_data=True, use_json=True):
+    """Read the reference's fixed-split files (data_reader.py:20-28, 46-49, 66-80)."""
+    if not use_json:
+        raise ValueError("pickle inputs are not loaded (unsafe deserialisation); convert to JSON or .npz")
+
+    def rd(name):
+        with open(os.path.join(filepath, name + ".json"), "r") as f:
+            return json.load(f)
+
+    uniq = rd("unique_users_list" if reverse_user_item_data else "unique_items_list")
+    col_index = {c: i for i, c in enumerate(uniq)}
+    base = "ratingsByItem" if reverse_user_item_data else "ratingsByUser"
+    tr = rd(base + "_dicts_train")
+    va_in, va_t = rd(base + "_dicts_valid")
+    te_in, te_t = rd(base + "_dicts_test")
+    train = RatingsCSR.from_lists(list(tr.keys()), list(tr.values()), col_index)
+    vk = list(va_t.keys())
+    tk = list(te_t.keys())
+    return FixedSplit(
+        num_cols=len(uniq),
+        train=train,
+        valid_in=RatingsCSR.from_lists(vk, [va_in.get(k) for k in vk], col_index),
+        valid_tgt=RatingsCSR.from_lists(vk, [va_t[k] for k in vk], col_index),
+        test_in=RatingsCSR.from_lists(tk, [te_in.get(k) for k in tk], col_index),
+        test_tgt=RatingsCSR.from_lists(tk, [te_t[k] for k in tk], col_index),
+        col_ids=list(uniq),
+    )
+
+
+def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=None):
+    """Rating-level permutation split of TrainValidTestSplit.py:74-103.
+
+    valid inputs = the row's train ratings (:101, map_inputs_to_targets :183-195),
+    test inputs = the row's train+valid ratings (:83, :103); rows keyed by their index.
+    """
+    rng = np.random if rng is None else rng
+    n = len(rows)
+    perm = rng.permutation(n)
+    ntr, nva = int(n * split[0]), int(n * split[1])
+    tr, va, te = perm[:ntr], perm[ntr:ntr + nva], perm[ntr + nva:]
+    rows = np.asarray(rows, np.int64)
+    cols = np.asarray(cols, np.int32)
+    vals = np.asarray(vals, np.float32)
+
+    def csr_of(idx):
+        return RatingsCSR.from_coo(rows[idx], cols[idx], vals[idx], n_rows)
+
+    full_tr = csr_of(tr)
+    full_va = csr_of(va)
+    full_te = csr_of(te)
+    full_te_in = csr_of(np.concatenate([tr, va]))
+    tr_rows = np.nonzero(full_tr.row_lengths())[0]
+    va_rows = np.nonzero(full_va.row_lengths())[0]
+    te_rows = np.nonzero(full_te.row_lengths())[0]
+    train = full_tr.subset_rows(tr_rows)
+    train.keys = [int(r) for r in tr_rows]
+    has_tr = full_tr.row_lengths() > 0
+    has_te_in = full_te_in.row_lengths() > 0
+
+    def pair(target_full, rows_sel, input_full, has_input):
+        tgt = target_full.subset_rows(rows_sel)
+        tgt.keys = [int(r) for r in rows_sel]
+        inp = input_full.subset_rows(np.where(has_input[rows_sel], rows_sel, -1))
+        inp.keys = list(tgt.keys)
+        return inp, tgt
+
+    va_in, va_t = pair(full_va, va_rows, full_tr, has_tr)
+    te_in, te_t = pair(full_te, te_rows, full_te_in, has_te_in)
+    return FixedSplit(n_cols, train, va_in, va_t, te_in, te_t, list(range(n_cols)))
+
+
+# density / shape table for synthetic inputs (rows x N in I-AutoRec orientation)
+SYNTH_SHAPES = {
+    "ml100k": dict(rows=1682, cols=943, nnz=100_000, half_stars=False),
+    "ml1m": dict(rows=3706, cols=6040, nnz=1_000_209, half_stars=False),
+    "ml20m": dict(rows=26_744, cols=138_493, nnz=20_000_263, half_stars=True),
+    "netflix": dict(rows=17_770, cols=480_189, nnz=100_480_507, half_stars=False),
+}
+
+
+def synthetic_ratings(rows, cols, nnz, half_stars=False, seed=0):
+    """Uniform-column synthetic ratings, multinomial row counts, duplicates removed."""
+    g = np.random.default_rng(seed)
+    counts = g.multinomial(nnz, np.full(rows, 1.0 / rows))
+    r = np.repeat(np.arange(rows, dtype=np.int64), counts)
+    c = g.integers(0, cols, size=len(r), dtype=np.int64)
+    key = np.unique(r * cols + c)
+    r = (key // cols).astype(np.int64)
+    c = (key % cols).astype(np.int32)
+    if half_stars:
+        v = g.integers(1, 11, size=len(r)).astype(np.float32) / 2.0
+    else:
+        v = g.integers(1, 6, size=len(r)).astype(np.float32)
+    return r, c, v
+
+
+def synthetic_fixed_split(name_or_shape, seed=0, scale_rows=None):
+    shp = dict(SYNTH_SHAPES[name_or_shape]) if isinstance(name_or_shape, str) else dict(name_or_shape)
+    if scale_rows:
+        shp["nnz"] = int(shp["nnz"] * scale_rows / shp["rows"])
+        shp["rows"] = scale_rows
+    r, c, v = synthetic_ratings(shp["rows"], shp["cols"], shp["nnz"], shp.get("half_stars", False), seed)
+    return split_ratings(r, c, v, shp["rows"], shp["cols"], rng=np.random.RandomState(seed))

@@ -1,0 +1,405 @@
+"""GPU engine: parameters, workspaces and the per-step kernel sequence of the autoencoder.
+
+Replaces what Keras/TF do for model.py:43-99 + train.py:49-51,131-133 (graph build, MatMul,
+BiasAdd, activation, Dropout, Mul, MSE, gradients, optimizer Assign ops) with calls into
+libocf.so.  Tensors are PyTorch-ROCm device tensors (memory + streams only); every byte of
+arithmetic runs in the hand-written HIP kernels.
+
+Padded HBM layout (DESIGN.md "Data layout"):
+  * batch rows       B  -> Bp = roundup(B, 128)
+  * output width     N  -> Np = roundup(N, 128); layer-0 input = k blocks of Np (concat order of
+                            model.py:47-56: data | observed mask | second mask)
+  * hidden widths    H  -> Hp = roundup(H, 128)
+  * W_i  fp32 [in_p][out_p] (Keras (in, out) layout), b_i fp32 [out_p]; pads are zero and stay
+    zero (their gradients are exactly zero, the optimizers map g = 0, state = 0 to no change)
+Per step the loss gradient is carried unscaled (err * mask) in the compute dtype and the
+constant 2/(B*N) of Keras' MSE is folded into the weight/bias-gradient epilogues (gscale), which
+keeps f16 operands far from underflow.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import OcfGemmArgs, OcfScatterArgs, call
+
+TILE = 128
+DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
+          "bfloat16": (_lib.DT_BF16, torch.bfloat16)}
+DTYPE_ALIASES = {"f32": "float32", "fp32": "float32", "f16": "float16", "fp16": "float16", "half": "float16",
+                 "bf16": "bfloat16"}
+
+
+def ru(x, m):
+    return ((int(x) + m - 1) // m) * m
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def cur_stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def glorot_uniform(rng, fan_in, fan_out):
+    lim = math.sqrt(6.0 / (fan_in + fan_out))
+    return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
+
+
+class Engine:
+    def __init__(self, N, hidden, batch_size, k_blocks=1, activation="tanh", dropout=None, l2=None,
+                 compute_dtype="float32", device=None, seed=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("omnidirectional_collaborative_filtering_amd needs a ROCm GPU (MI355X); none visible")
+        _lib.load()
+        cd = DTYPE_ALIASES.get(compute_dtype, compute_dtype)
+        if cd not in DTYPES:
+            raise ValueError("compute_dtype must be float32, float16 or bfloat16")
+        self.cdtype = cd
+        self.cdt, self.tdt = DTYPES[cd]
+        self.dev = torch.device(device if device is not None else "cuda")
+        self.N = int(N)
+        self.Np = ru(N, TILE)
+        self.k = int(k_blocks)
+        self.H = [int(h) for h in hidden]
+        self.Hp = [ru(h, TILE) for h in self.H]
+        self.B = int(batch_size)
+        self.Bp = ru(self.B, TILE)
+        self.act = _lib.ACT[activation]
+        self.activation = activation
+        self.dropout = dropout
+        self.keep = 1.0 - float(dropout) if dropout else 1.0
+        self.l2 = float(l2) if l2 else 0.0
+        self.seed = int(seed if seed is not None else np.random.randint(0, 2 ** 31 - 1))
+        self.real_dims = [self.k * self.N] + self.H + [self.N]
+        self.pad_dims = [self.k * self.Np] + self.Hp + [self.Np]
+        self.n_tiles = self.Np // TILE
+        self.step_count = 0
+        self.opt = None
+        self.slots = []
+        self._alloc_params()
+        self._alloc_workspace()
+        self.init_weights(np.random.RandomState(self.seed))
+
+    # ---------------------------------------------------------------- parameters
+    def _alloc_params(self):
+        f = dict(device=self.dev, dtype=torch.float32)
+        self.W = [torch.zeros(i, o, **f) for i, o in zip(self.pad_dims[:-1], self.pad_dims[1:])]
+        self.b = [torch.zeros(o, **f) for o in self.pad_dims[1:]]
+
+    def _row_map(self, layer):
+        """padded row index of each real input row of layer `layer`."""
+        if layer == 0:
+            blk = np.arange(self.k * self.N) // self.N
+            return blk * self.Np + np.arange(self.k * self.N) % self.N
+        return np.arange(self.real_dims[layer])
+
+    def init_weights(self, rng):
+        """Keras glorot_uniform kernels, zero biases (fan in/out of the real, unpadded layer)."""
+        ws = [glorot_uniform(rng, i, o) for i, o in zip(self.real_dims[:-1], self.real_dims[1:])]
+        self.set_weights([x for w in ws for x in (w, np.zeros(w.shape[1], np.float32))])
+
+    def get_weights(self):
+        """Keras-layout numpy list [W0, b0, W1, b1, ...] (padding stripped)."""
+        out = []
+        for i, (w, b) in enumerate(zip(self.W, self.b)):
+            rows = torch.as_tensor(self._row_map(i), device=self.dev)
+            out.append(w.index_select(0, rows)[:, : self.real_dims[i + 1]].cpu().numpy())
+            out.append(b[: self.real_dims[i + 1]].cpu().numpy())
+        return out
+
+    def set_weights(self, weights):
+        for i in range(len(self.W)):
+            w = torch.as_tensor(np.asarray(weights[2 * i], np.float32), device=self.dev)
+            bb = torch.as_tensor(np.asarray(weights[2 * i + 1], np.float32), device=self.dev)
+            if tuple(w.shape) != (self.real_dims[i], self.real_dims[i + 1]):
+                raise ValueError("weight %d has shape %s, expected %s" % (i, tuple(w.shape),
+                                                                         (self.real_dims[i], self.real_dims[i + 1])))
+            self.W[i].zero_()
+            rows = torch.as_tensor(self._row_map(i), device=self.dev)
+            self.W[i][:, : self.real_dims[i + 1]].index_copy_(0, rows, w)
+            self.b[i].zero_()
+            self.b[i][: self.real_dims[i + 1]] = bb
+
+    def set_optimizer(self, opt):
+        self.opt = opt
+        self.slots = []
+        for w, b in zip(self.W, self.b):
+            sw = [torch.zeros_like(w) for _ in range(opt.n_slots)] + [None] * (2 - opt.n_slots)
+            sb = [torch.zeros_like(b) for _ in range(opt.n_slots)] + [None] * (2 - opt.n_slots)
+            self.slots.append((sw, sb))
+
+    # ---------------------------------------------------------------- workspace
+    def _alloc_workspace(self):
+        d = self.dev
+        Bp = self.Bp
+        self.xin = torch.zeros(Bp, self.pad_dims[0], device=d, dtype=self.tdt)
+        self.a = [torch.zeros(Bp, h, device=d, dtype=torch.float32) for h in self.Hp]
+        self.h = [torch.zeros(Bp, h, device=d, dtype=self.tdt) for h in self.Hp]
+        self.dh = [torch.zeros(Bp, h, device=d, dtype=self.tdt) for h in self.Hp]
+        self.mask = [torch.zeros(Bp, h, device=d, dtype=torch.uint8) for h in self.Hp] if self.keep < 1 else \
+            [None] * len(self.Hp)
+        self.d_out = torch.zeros(Bp, self.Np, device=d, dtype=self.tdt)
+        self.db_out_part = torch.zeros(Bp // TILE, self.Np, device=d, dtype=torch.float32)
+        self.db_h = [torch.zeros(Bp // TILE, h, device=d, dtype=torch.float32) for h in self.Hp]
+        self.splits0 = self._pick_splits(self.pad_dims[0], self.Hp[0])
+        self.splitsL = self._pick_splits(self.Np, self.Hp[-1])
+        smax = max(self.splits0 * self.Hp[0], self.splitsL * self.Hp[-1])
+        self.slabs = torch.zeros(smax * Bp, device=d, dtype=torch.float32)
+        self.tile_cnt = torch.zeros(self.n_tiles, device=d, dtype=torch.int32)
+        self.bk_ptr = torch.zeros(self.n_tiles + 1, device=d, dtype=torch.int32)
+        self.bk_cur = torch.zeros(self.n_tiles, device=d, dtype=torch.int32)
+        self.bk_cap = 0
+        self._grow_buckets(1 << 16)
+        gm = Bp // TILE
+        self.stats_part = torch.zeros(self.n_tiles * gm * 4, device=d, dtype=torch.float32)
+        self.row_sse_part = torch.zeros(self.n_tiles * Bp, device=d, dtype=torch.float32)
+        self.stats_cap = 0
+        self.stats_hist = None
+        self._grow_stats(64)
+        self.n_stats = 0
+        self.dense_in = None
+
+    def _pick_splits(self, K, Hp):
+        bk = 32 if self.cdt == _lib.DT_F32 else 64
+        ksteps = K // bk
+        tiles = (self.Bp // TILE) * (Hp // TILE)
+        s = max(1, min(ksteps // 8, max(1, 512 // tiles)))
+        return s
+
+    def _grow_buckets(self, n):
+        if n <= self.bk_cap:
+            return
+        cap = max(n, 2 * self.bk_cap)
+        self.bk_rc = torch.zeros(cap, device=self.dev, dtype=torch.int32)
+        self.bk_t = torch.zeros(cap, device=self.dev, dtype=torch.float32)
+        self.bk_m = torch.zeros(cap, device=self.dev, dtype=torch.float32)
+        self.bk_cap = cap
+
+    def _grow_stats(self, n):
+        if n <= self.stats_cap:
+            return
+        cap = max(n, 2 * self.stats_cap)
+        new = torch.zeros(cap, 4 + self.Bp, device=self.dev, dtype=torch.float32)
+        if self.stats_hist is not None and self.n_stats:
+            new[: self.n_stats] = self.stats_hist[: self.n_stats]
+        self.stats_hist = new
+        self.stats_cap = cap
+
+    # ---------------------------------------------------------------- batch assembly
+    def scatter_args(self):
+        a = OcfScatterArgs()
+        a.B = self.B
+        a.B_pad = self.Bp
+        a.N = self.N
+        a.xin = ptr(self.xin)
+        a.xin_dtype = self.cdt
+        a.xin_ld = self.pad_dims[0]
+        a.xin_block = self.Np
+        a.tile_cnt = ptr(self.tile_cnt)
+        a.bk_ptr = ptr(self.bk_ptr)
+        a.bk_cur = ptr(self.bk_cur)
+        a.bk_rc = ptr(self.bk_rc)
+        a.bk_t = ptr(self.bk_t)
+        a.bk_m = ptr(self.bk_m)
+        a.n_tiles = self.n_tiles
+        a.s0 = a.s1 = 1.0
+        return a
+
+    def load_batch(self, a, max_targets):
+        """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller)."""
+        self._grow_buckets(max_targets)
+        a.bk_rc, a.bk_t, a.bk_m = ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m)
+        call("ocf_scatter_batch", a, cur_stream())
+
+    def load_dense(self, inputs, out_mask, targets):
+        """API path: dense arrays (torch/numpy) in the model.py input order."""
+        B, N = self.B, self.N
+        if self.dense_in is None:
+            self.dense_in = torch.zeros(5, self.B, self.Np, device=self.dev, dtype=torch.float32)
+        buf = self.dense_in
+        buf.zero_()
+        srcs = list(inputs) + [out_mask, targets]
+        for i, s in enumerate(srcs):
+            t = torch.as_tensor(np.asarray(s) if not torch.is_tensor(s) else s)
+            if tuple(t.shape) != (B, N):
+                raise ValueError("input %d has shape %s, expected (%d, %d)" % (i, tuple(t.shape), B, N))
+            slot = i if i < len(inputs) else (3 if s is out_mask else 4)
+            buf[slot, :, :N] = t.to(self.dev, torch.float32)
+        p0 = ptr(buf[0])
+        p1 = ptr(buf[1]) if len(inputs) > 1 else None
+        p2 = ptr(buf[2]) if len(inputs) > 2 else None
+        s = cur_stream()
+        call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
+             self.Bp, s)
+        self._grow_buckets(B * N)
+        call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
+             ptr(self.bk_ptr), ptr(self.bk_cur), ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m), s)
+
+    # ---------------------------------------------------------------- GEMM helper
+    def _gemm(self, A, a_col, lda, Bm, b_dtype, b_col, ldb, M, N, K, epi, **kw):
+        g = OcfGemmArgs()
+        g.compute_dtype = self.cdt
+        g.A = ptr(A)
+        g.a_dtype = self.cdt
+        g.a_col = a_col
+        g.lda = lda
+        g.B = ptr(Bm)
+        g.b_dtype = b_dtype
+        g.b_col = b_col
+        g.ldb = ldb
+        g.M, g.N, g.K = M, N, K
+        g.splits = kw.pop("splits", 1)
+        g.order = kw.pop("order", 0)
+        g.epi = epi
+        g.keep = 1.0
+        for k, v in kw.items():
+            if torch.is_tensor(v):
+                v = ptr(v)
+            setattr(g, k, v)
+        call("ocf_gemm", g, cur_stream())
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, training):
+        """Encoder stack; leaves h[-1] (compute dtype) for the output layer."""
+        s = cur_stream()
+        Bp, L = self.Bp, len(self.H)
+        keep = self.keep if training else 1.0
+        stream_id = (self.step_count * 16) if training else 0
+        # layer 0: split-K over the (k x Np)-wide input
+        Hp0 = self.Hp[0]
+        sstride = Bp * Hp0
+        self._gemm(self.xin, 0, self.pad_dims[0], self.W[0], _lib.DT_F32, 1, Hp0, Bp, Hp0, self.pad_dims[0],
+                   _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
+        call("ocf_splitk_bias_act", ptr(self.slabs), self.splits0, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
+             keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
+             ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
+        for i in range(1, L):
+            self._gemm(self.h[i - 1], 0, self.Hp[i - 1], self.W[i], _lib.DT_F32, 1, self.Hp[i], Bp, self.Hp[i],
+                       self.Hp[i - 1], _lib.EPI_BIAS_ACT, bias=self.b[i], act=self.act, keep=keep, seed=self.seed,
+                       stream=stream_id + i, mask_out=self.mask[i] if keep < 1 else None, a_out=self.a[i],
+                       h_out=self.h[i], h_dtype=self.cdt, ld_out=self.Hp[i], m_real=self.B, n_real=self.H[i])
+
+    def output_loss(self, with_grad):
+        """Decoder GEMM with the fused masked-MSE epilogue; stats -> stats_hist[n_stats]."""
+        L = len(self.H)
+        gscale = 2.0 / (self.B * self.N)
+        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 1, self.Np, self.Bp, self.Np,
+                   self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], bk_ptr=self.bk_ptr,
+                   bk_rc=self.bk_rc, bk_t=self.bk_t, bk_m=self.bk_m,
+                   h_out=self.d_out if with_grad else None, h_dtype=self.cdt, ld_out=self.Np,
+                   db_part=self.db_out_part if with_grad else None, ld_db=self.Np,
+                   opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
+                   stats_part=self.stats_part, row_sse_part=self.row_sse_part)
+        self._grow_stats(self.n_stats + 1)
+        call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
+             self.n_tiles, self.Bp, ptr(self.stats_hist[self.n_stats]), cur_stream())
+        self.n_stats += 1
+
+    def predict_dense(self, out_mask, out):
+        """PREDICT epilogue: out[B][N] = out_mask * (h W + b)."""
+        L = len(self.H)
+        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 1, self.Np, self.Bp, self.Np,
+                   self.Hp[L - 1], _lib.EPI_PREDICT, bias=self.b[L], pmask=out_mask,
+                   ld_pmask=out_mask.stride(0) if out_mask is not None else 0, out=out, ld_out=out.stride(0),
+                   m_real=self.B, n_real=self.N)
+
+    # ---------------------------------------------------------------- backward + update
+    def backward_update(self, grads_out=None):
+        """Backward pass; with grads_out=None the optimizer is fused into the weight-gradient GEMMs
+        (single GPU).  Otherwise raw gradients are written to grads_out (list matching params) and
+        the caller all-reduces and calls apply_grads()."""
+        s = cur_stream()
+        L, Bp = len(self.H), self.Bp
+        gscale = 2.0 / (self.B * self.N)
+        fused = grads_out is None
+        op = self.opt.step_params(1.0, self.l2) if fused else None
+        self._bias_op = self.opt.step_params(1.0, 0.0) if fused else None   # l2 regularises kernels only
+        # delta of the last hidden layer: split-K over Np
+        HpL = self.Hp[L - 1]
+        sstride = Bp * HpL
+        self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 0, self.Np, Bp, HpL, self.Np, _lib.EPI_SLAB,
+                   splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
+        db_last = self.db_h[L - 1]
+        call("ocf_splitk_grad_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.a[L - 1]),
+             ptr(self.mask[L - 1]), self.keep, self.act, ptr(self.dh[L - 1]), self.cdt, ptr(db_last[0]), gscale,
+             self.B, self.H[L - 1], s)
+        # output layer bias + weights
+        self._bias_update(L, self.db_out_part, Bp // TILE, self.Np, self.Np, grads_out, op)
+        self._weight_update(L, self.h[L - 1], HpL, self.d_out, self.Np, HpL, self.Np, gscale, grads_out, op)
+        parts_last = 1
+        for i in range(L - 1, 0, -1):
+            # delta of hidden layer i-1 through W_i (before W_i changes)
+            self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
+                       self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
+                       act=self.act, h_out=self.dh[i - 1], h_dtype=self.cdt, ld_out=self.Hp[i - 1],
+                       db_part=self.db_h[i - 1], opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
+                       m_real=self.B, n_real=self.H[i - 1])
+            self._bias_update(i, self.db_h[i], parts_last, self.Hp[i], self.Hp[i], grads_out, op)
+            self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
+                                self.Hp[i], gscale, grads_out, op)
+            parts_last = Bp // TILE
+        self._bias_update(0, self.db_h[0], parts_last, self.Hp[0], self.Hp[0], grads_out, op)
+        self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0], self.Hp[0],
+                            gscale, grads_out, op)
+        if fused:
+            self.opt.iterations += 1
+
+    def _bias_update(self, i, part, parts, ld, n, grads_out, op):
+        s = cur_stream()
+        sw, sb = self.slots[i] if self.slots else ([None, None], [None, None])
+        if grads_out is None:
+            call("ocf_bias_opt_from_partials", ptr(self.b[i]), ptr(part), parts, ld, n, ptr(sb[0]), ptr(sb[1]),
+                 None, self._bias_op, s)
+        else:
+            call("ocf_bias_opt_from_partials", ptr(self.b[i]), ptr(part), parts, ld, n, None, None,
+                 ptr(grads_out[2 * i + 1]), _lib.OcfOptParams(), s)
+
+    def _weight_update(self, i, A, lda, Bm, ldb, M, N, gscale, grads_out, op):
+        K = self.Bp
+        if grads_out is None:
+            sw, _ = self.slots[i]
+            o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
+            self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
+                       ld_out=N, opt=o)
+        else:
+            self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
+                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale))
+
+    def apply_grads(self, grads, scale=1.0):
+        """Elementwise optimizer over all parameters (after a data-parallel all-reduce)."""
+        s = cur_stream()
+        op = self.opt.step_params(scale, self.l2)
+        for i in range(len(self.W)):
+            sw, sb = self.slots[i]
+            call("ocf_opt_step", ptr(self.W[i]), ptr(grads[2 * i]), ptr(sw[0]), ptr(sw[1]), self.W[i].numel(), op, s)
+            ob = self.opt.step_params(scale, 0.0)
+            call("ocf_opt_step", ptr(self.b[i]), ptr(grads[2 * i + 1]), ptr(sb[0]), ptr(sb[1]), self.b[i].numel(), ob, s)
+        self.opt.iterations += 1
+
+    def grad_buffers(self):
+        out = []
+        for w, b in zip(self.W, self.b):
+            out += [torch.zeros_like(w), torch.zeros_like(b)]
+        return out
+
+    # ---------------------------------------------------------------- steps
+    def train_step(self, grads_out=None):
+        self.forward(training=True)
+        self.output_loss(with_grad=True)
+        self.backward_update(grads_out)
+        self.step_count += 1
+
+    def eval_step(self):
+        self.forward(training=False)
+        self.output_loss(with_grad=False)
+
+    def take_stats(self):
+        """host copy of the per-step stats recorded since the last call: [steps, 4 + Bp]."""
+        out = self.stats_hist[: self.n_stats].cpu().numpy().astype(np.float64)
+        self.n_stats = 0
+        return out

@@ -1,0 +1,322 @@
+"""Drop-in for the reference's ``omni_model`` (model.py:33-99) and the Keras ``Model`` subset that
+train.py / train_jester.py use: compile, fit_generator, evaluate_generator, predict, fit,
+train_on_batch, test_on_batch, save, metrics_names, get_weights / set_weights.
+
+Graph (model.py:43-99):  x = concat([data, observed_mask?, second_mask?]);
+L x [Dense(H, act) -> Dropout(p, noise_shape=[B, H])] ; y = output_mask * Dense(N, linear)(x)
+Loss: Keras 'mean_squared_error' (train.py:49).  Everything runs through engine.Engine on the GPU.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from . import metrics as M
+from . import optimizers
+from .data_reader import BatchGenerator
+from .engine import Engine
+
+
+class History(object):
+    def __init__(self):
+        self.history = {}
+        self.epoch = []
+
+
+class EarlyStopping(object):
+    """keras.callbacks.EarlyStopping(monitor, min_delta, patience, mode='auto') as train_jester.py:65 uses it."""
+
+    def __init__(self, monitor="val_loss", min_delta=0, patience=0, verbose=0, mode="auto"):
+        self.monitor, self.min_delta, self.patience = monitor, min_delta, patience
+        self.best = np.inf
+        self.wait = 0
+        self.stop = False
+
+    def on_epoch_end(self, logs):
+        v = logs.get(self.monitor)
+        if v is None:
+            return
+        if v < self.best - self.min_delta:
+            self.best, self.wait = v, 0
+        else:
+            self.wait += 1
+            if self.wait > self.patience:
+                self.stop = True
+
+
+class Model(object):
+    def __init__(self, engine, use_causal_info, use_both_masks, rating_range=1.0):
+        self.engine = engine
+        self.use_causal_info = use_causal_info
+        self.use_both_masks = use_both_masks
+        self.optimizer = None
+        self.metric_names = []
+        self.rating_range = float(rating_range)
+        self.stop_training = False
+
+    # ------------------------------------------------------------------ compile
+    def compile(self, optimizer, loss="mean_squared_error", metrics=None, rating_range=None):
+        if loss not in ("mean_squared_error", "mse"):
+            raise NotImplementedError("only the masked 'mean_squared_error' loss of train.py:49 is implemented")
+        self.optimizer = optimizers.get(optimizer)
+        self.engine.set_optimizer(self.optimizer)
+        self.metric_names = [M.metric_name(m) for m in (metrics or [])]
+        if rating_range is not None:
+            self.rating_range = float(rating_range)
+
+    @property
+    def metrics_names(self):
+        return ["loss"] + list(self.metric_names)
+
+    def _logs_from_stats(self, st, rows=None):
+        """st: [steps, 4 + Bp] device stats -> epoch-mean logs (Keras weights batches by size)."""
+        e = self.engine
+        B = e.B
+        out = {k: [] for k in self.metrics_names}
+        for row in st:
+            sse, sae, cnt = row[0], row[1], row[2]
+            out["loss"].append(sse / (B * e.N))
+            for name in self.metric_names:
+                out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N, self.rating_range))
+        return {k: float(np.mean(v)) if v else float("nan") for k, v in out.items()}
+
+    # ------------------------------------------------------------------ batch plumbing
+    def _split_inputs(self, x):
+        """model.py:89-97 input order -> (layer-0 blocks, output mask)."""
+        x = list(x)
+        if self.use_causal_info:
+            blocks = [x[0], x[1]]
+            out_mask = x[2]
+            rest = x[3:]
+        else:
+            blocks = [x[0]]
+            out_mask = x[1]
+            rest = x[2:]
+        if self.use_both_masks:
+            blocks.append(rest[0])
+        return blocks, out_mask
+
+    def _load(self, item, gen=None, bi=None):
+        e = self.engine
+        if gen is not None:
+            args = gen.scatter_args(bi, engine_args=e.scatter_args())
+            e.load_batch(args, gen.max_targets)
+            return gen.target_count(bi)
+        x, y = item[0], item[1]
+        blocks, out_mask = self._split_inputs(x)
+        e.load_dense(blocks, out_mask, y)
+        return item[2] if len(item) > 2 else None
+
+    def _pull(self, gen):
+        if isinstance(gen, BatchGenerator):
+            self._check_gen(gen)
+            bi = gen.next_batch_index()
+            if bi is None:
+                raise StopIteration("generator exhausted (data_reader.py:418 yields None)")
+            return self._load(None, gen, bi)
+        item = next(gen)
+        if item is None:
+            raise StopIteration("generator yielded None")
+        return self._load(item)
+
+    def _check_gen(self, gen):
+        e = self.engine
+        if gen.B != e.B:
+            raise ValueError("generator batch_size %d != model batch_size %d (Dropout noise_shape, model.py:73)"
+                             % (gen.B, e.B))
+        want_k = 1 + int(self.use_causal_info) + int(self.use_both_masks)
+        have_k = 1 + int(gen.aux_type is not None) + int(gen.aux_type == "both")
+        if want_k != have_k:
+            raise ValueError("auxilliary_mask_type=%r does not match the model inputs" % (gen.aux_type,))
+
+    # ------------------------------------------------------------------ training
+    def train_on_batch(self, x, y):
+        self._load((x, y))
+        self.engine.train_step()
+        return self._finish(self.engine.take_stats())
+
+    def test_on_batch(self, x, y):
+        self._load((x, y))
+        self.engine.eval_step()
+        return self._finish(self.engine.take_stats())
+
+    def _finish(self, st):
+        logs = self._logs_from_stats(st)
+        vals = [logs[k] for k in self.metrics_names]
+        return vals[0] if len(vals) == 1 else vals
+
+    def fit_generator(self, generator, steps_per_epoch, epochs=1, verbose=1, callbacks=None, validation_data=None,
+                      validation_steps=None, initial_epoch=0, **kw):
+        hist = History()
+        callbacks = callbacks or []
+        steps = int(steps_per_epoch)
+        for epoch in range(initial_epoch, epochs):
+            t0 = time.time()
+            for _ in range(steps):
+                self._pull(generator)
+                self.engine.train_step()
+            logs = self._logs_from_stats(self.engine.take_stats())
+            if validation_data is not None:
+                vals = self.evaluate_generator(validation_data, validation_steps)
+                vals = vals if isinstance(vals, list) else [vals]
+                for k, v in zip(self.metrics_names, vals):
+                    logs["val_" + k] = v
+            for k, v in logs.items():
+                hist.history.setdefault(k, []).append(v)
+            hist.epoch.append(epoch)
+            if verbose:
+                print("Epoch %d - %.1fs - " % (epoch + 1, time.time() - t0) +
+                      " - ".join("%s: %.4f" % kv for kv in logs.items()))
+            for cb in callbacks:
+                cb.on_epoch_end(logs)
+                self.stop_training |= getattr(cb, "stop", False)
+            if self.stop_training:
+                break
+        return hist
+
+    def evaluate_generator(self, generator, steps, **kw):
+        steps = int(steps)
+        self.engine.take_stats()
+        for _ in range(steps):
+            self._pull(generator)
+            self.engine.eval_step()
+        return self._finish(self.engine.take_stats())
+
+    def evaluate_sse(self, generator, steps):
+        """Fused form of train.py:225-255: (sum of squared errors, sum of target_count)."""
+        self.engine.take_stats()
+        count = 0
+        for _ in range(int(steps)):
+            c = self._pull(generator)
+            self.engine.eval_step()
+            count += int(c) if c is not None else 0
+        st = self.engine.take_stats()
+        return float(st[:, 0].sum()), count
+
+    def predict(self, x, batch_size=None, verbose=0):
+        """Returns y = output_mask * (h W_out + b_out) as a float32 CUDA tensor [B, N]."""
+        e = self.engine
+        blocks, out_mask = self._split_inputs(x)
+        dummy_t = torch.zeros(e.B, e.N, device=e.dev)
+        e.load_dense(blocks, out_mask, dummy_t)
+        e.forward(training=False)
+        out = torch.empty(e.B, e.N, device=e.dev, dtype=torch.float32)
+        om = out_mask if torch.is_tensor(out_mask) else torch.as_tensor(np.asarray(out_mask, np.float32))
+        om = om.to(e.dev, torch.float32).contiguous()
+        e.predict_dense(om, out)
+        return out
+
+    def fit(self, x, y, batch_size=None, epochs=1, verbose=1, callbacks=None, validation_split=0.0, shuffle=True,
+            **kw):
+        """Keras Model.fit on dense arrays (train_jester.py:78-79): last validation_split fraction held out,
+        np.random.shuffle of the training indices each epoch; full batches only (fixed noise_shape)."""
+        e = self.engine
+        bs = int(batch_size or e.B)
+        if bs != e.B:
+            raise ValueError("batch_size must equal the model batch_size (Dropout noise_shape, model.py:73)")
+        x = [np.asarray(a) if not torch.is_tensor(a) else a for a in x]
+        n = len(x[0])
+        split_at = int(n * (1.0 - validation_split)) if validation_split else n
+        hist = History()
+        callbacks = callbacks or []
+        for epoch in range(epochs):
+            idx = np.arange(split_at)
+            if shuffle:
+                np.random.shuffle(idx)
+            for s in range(split_at // bs):
+                sel = idx[s * bs:(s + 1) * bs]
+                self._load(([a[sel] for a in x], y[sel]))
+                e.train_step()
+            logs = self._logs_from_stats(e.take_stats())
+            if split_at < n and (n - split_at) >= bs:
+                vals = []
+                for s in range((n - split_at) // bs):
+                    sel = np.arange(split_at + s * bs, split_at + (s + 1) * bs)
+                    self._load(([a[sel] for a in x], y[sel]))
+                    e.eval_step()
+                vl = self._logs_from_stats(e.take_stats())
+                for k, v in vl.items():
+                    logs["val_" + k] = v
+            for k, v in logs.items():
+                hist.history.setdefault(k, []).append(v)
+            hist.epoch.append(epoch)
+            for cb in callbacks:
+                cb.on_epoch_end(logs)
+                self.stop_training |= getattr(cb, "stop", False)
+            if self.stop_training:
+                break
+        return hist
+
+    # ------------------------------------------------------------------ weights / checkpoints
+    def get_weights(self):
+        return self.engine.get_weights()
+
+    def set_weights(self, weights):
+        self.engine.set_weights(weights)
+
+    def save(self, path):
+        """Weights (Keras layout) + optimizer state in a safetensors file (replaces the h5 of train.py:169)."""
+        from safetensors.numpy import save_file
+        e = self.engine
+        tensors = {}
+        for i, w in enumerate(e.get_weights()):
+            tensors["param/%d" % i] = np.ascontiguousarray(w)
+        if self.optimizer is not None and e.slots:
+            for i, (sw, sb) in enumerate(e.slots):
+                for j, t in enumerate(sw):
+                    if t is not None:
+                        tensors["opt/W%d/%d" % (i, j)] = t.cpu().numpy()
+                for j, t in enumerate(sb):
+                    if t is not None:
+                        tensors["opt/b%d/%d" % (i, j)] = t.cpu().numpy()
+            tensors["opt/iterations"] = np.array([self.optimizer.iterations], np.int64)
+        save_file(tensors, path)
+
+    def load(self, path, with_optimizer=True):
+        from safetensors.numpy import load_file
+        t = load_file(path)
+        n = len([k for k in t if k.startswith("param/")])
+        self.set_weights([t["param/%d" % i] for i in range(n)])
+        e = self.engine
+        if with_optimizer and self.optimizer is not None and "opt/iterations" in t:
+            for i, (sw, sb) in enumerate(e.slots):
+                for j, s in enumerate(sw):
+                    if s is not None:
+                        s.copy_(torch.as_tensor(t["opt/W%d/%d" % (i, j)]))
+                for j, s in enumerate(sb):
+                    if s is not None:
+                        s.copy_(torch.as_tensor(t["opt/b%d/%d" % (i, j)]))
+            self.optimizer.iterations = int(t["opt/iterations"][0])
+
+
+class omni_model(object):
+    """model.py:34-35 signature; extra keyword ``compute_dtype`` ('float32' = exact-fp32 MFMA, the
+    parity mode; 'float16' / 'bfloat16' MFMA with fp32 accumulation) and ``seed``."""
+
+    def __init__(self, numlayers, num_hidden_units, input_shape, batch_size, dense_activation="tanh",
+                 use_causal_info=True, use_timestamps=False, use_both_masks=False, l2_weight_regulatization=None,
+                 sparse_representation=False, dropout_probability=None, use_sparse_masking_layer=False,
+                 compute_dtype="float32", seed=None, device=None, rating_range=1.0):
+        if use_timestamps:
+            raise NotImplementedError("use_timestamps: broken in the reference; not supported")
+        if sparse_representation:
+            raise NotImplementedError("sparse_representation: needs a patched Keras in the reference; dense only")
+        if use_sparse_masking_layer:
+            raise NotImplementedError("Dynamic_Masking_Layer is broken in the reference (model.py:186)")
+        self.numlayers = numlayers
+        self.num_hidden_units = num_hidden_units
+        self.input_shape = input_shape
+        self.batch_size = batch_size
+        k = 1 + int(bool(use_causal_info)) + int(bool(use_both_masks))
+        self.engine = Engine(input_shape, [num_hidden_units] * numlayers, batch_size, k_blocks=k,
+                             activation=dense_activation, dropout=dropout_probability, l2=l2_weight_regulatization,
+                             compute_dtype=compute_dtype, device=device, seed=seed)
+        self.model = Model(self.engine, bool(use_causal_info), bool(use_both_masks), rating_range)
+
+    def save_weights(self, filename):
+        self.model.save(filename)
+
+    def load_weights(self, weights):
+        self.model.set_weights(weights)
