@@ -1,0 +1,233 @@
+"""Headline benchmark: ML-20M-shaped I-AutoRec training steps on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One step = one pass of the hot path over one batch resident in HBM: K1 scatter of B item-rows of
+the rating CSR -> encoder GEMM (split-K) + bias/sigmoid/dropout -> decoder GEMM with the fused
+masked-MSE epilogue -> backward GEMMs -> Adagrad (fused into the weight-gradient GEMMs at N=1;
+all-reduce of the gradients + elementwise Adagrad at N>1).  Configuration = train.py's
+(sigmoid, dropout 0.2, Adagrad lr 0.005, pass-through training, data_sparsity [1,1]) at
+BASELINE.json configs[2]: ML-20M I-AutoRec (26,744 item rows x 138,493 users), 500 hidden units,
+batch 256, fp16 MFMA with fp32 accumulation.  Data: synthetic, ML-20M density, seeded.
+
+Prints ONE JSON line (rank 0).  value = ratings/s summed over ranks = sum of input ratings
+processed / max-over-ranks wall time of the K timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "ratings/sec + masked-RMSE, ML-20M I-AutoRec at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+MFMA_F16_PEAK_TFS = 2500.0     # dense f16/bf16 MFMA (spec)
+OPT_STATE_BYTES = {"adagrad": 16, "rmsprop": 16, "adam": 24, "sgd": 8}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="ml20m")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--hidden", type=int, default=500)
+    ap.add_argument("--dtype", default="float16")
+    ap.add_argument("--optimizer", default="adagrad")
+    ap.add_argument("--dropout", type=float, default=0.2)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--phase-timers", type=int, default=1)
+    ap.add_argument("--rmse", type=int, default=1)
+    return ap.parse_args()
+
+
+def optim(name, lr):
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    return {"adagrad": lambda: O.Adagrad(lr=lr, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=lr),
+            "adam": lambda: O.Adam(lr=lr), "sgd": lambda: O.SGD(lr=lr)}[name]()
+
+
+def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps):
+    """The oracle restatement on the host cores (bounded sample): per-rating Python assembler
+    (data_reader.py:95-200, one core) + NumPy fp32 model step (Keras math, BLAS threads)."""
+    from threadpoolctl import threadpool_info
+    from oracle.batch_oracle import train_batch_loop_csr
+    from oracle.model_oracle import AdagradOracle, OmniOracle
+    tr = data.train
+    t_asm = t_mod = 0.0
+    nnz = 0
+    ora = OmniOracle([N, H, N], activation="sigmoid", dtype=np.float32).set_params(w0[0::2], w0[1::2])
+    opt = AdagradOracle(lr=lr)
+    for rows in rows_batches[:n_steps]:
+        t0 = time.perf_counter()
+        m_in, m_out, x, t, m_miss = train_batch_loop_csr(tr.row_ptr, tr.col, tr.val, rows, N)
+        t1 = time.perf_counter()
+        loss, _, gW, gb = ora.loss_and_grads(x, m_out, t)
+        ora.set_flat(opt.step(ora.params(), [g for pair in zip(gW, gb) for g in pair]))
+        t2 = time.perf_counter()
+        t_asm += t1 - t0
+        t_mod += t2 - t1
+        nnz += int(tr.row_lengths()[rows].sum())
+    threads = max([d.get("num_threads", 1) for d in threadpool_info()] + [1])
+    return {"value": nnz / (t_asm + t_mod), "unit": "ratings/s", "cores": int(threads), "kind": "port",
+            "sample": "%d ML-20M-shaped train steps (B=%d): per-rating Python assembler %.2fs/step on 1 core + "
+                      "NumPy fp32 dense model step (Adagrad) %.2fs/step on %d BLAS threads"
+                      % (n_steps, len(rows_batches[0]), t_asm / n_steps, t_mod / n_steps, threads)}
+
+
+def main():
+    args = parse()
+    from omnidirectional_collaborative_filtering_amd.parallel import (GradBucket, dp_train_step, init_from_env,
+                                                                      shard_batches)
+    rank, world, local = init_from_env()
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+
+    t0 = time.time()
+    data = synthetic_fixed_split(args.config, seed=0)
+    N = data.num_cols
+    n_rows = data.train.n_rows
+    np.random.seed(1234)
+    rd = data_reader(N, n_rows, dataset=data, eval_mode="fixed_split", rng="device", device=dev)
+    B, H = args.batch, args.hidden
+    om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False,
+                    dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev)
+    m = om.model
+    lr = 0.005 if args.optimizer == "adagrad" else 0.001
+    m.compile(optim(args.optimizer, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
+    w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
+    eng = om.engine
+    gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    gen._start()
+    batches = shard_batches(gen.num_batches, rank, world)
+    bucket = GradBucket(eng) if world > 1 else None
+    nnz_of = gen.nnz1
+    setup_s = time.time() - t0
+
+    def step(i):
+        bi = batches[i % len(batches)]
+        m._load(None, gen, bi)
+        dp_train_step(eng, bucket, world)
+        return int(nnz_of[bi])
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    eng.enable_timers(bool(args.phase_timers))
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    nnz = 0
+    for i in range(args.steps):
+        nnz += step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    phases = eng.phase_times_ms()
+    eng.timers = None
+    tot = torch.tensor([elapsed, float(nnz)], device=dev, dtype=torch.float64)
+    if world > 1:
+        tmax = tot[:1].clone()
+        torch.distributed.all_reduce(tmax, op=torch.distributed.ReduceOp.MAX)
+        nsum = tot[1:].clone()
+        torch.distributed.all_reduce(nsum, op=torch.distributed.ReduceOp.SUM)
+        elapsed, nnz = float(tmax.item()), float(nsum.item())
+    eng.take_stats()
+
+    # masked RMSE on the test split (train.py:225-255, fused form)
+    rmse = None
+    if args.rmse:
+        tgen = rd.data_gen(B, None, "test", True, None, -1, return_target_count=True)
+        sse, cnt = m.evaluate_sse(tgen, rd.test_set_size // B)
+        rmse = float(np.sqrt(sse / cnt)) if cnt else None
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    # roofline of the dominant kernel: fused weight-gradient GEMM + optimizer update
+    P = N * H
+    opt_b = OPT_STATE_BYTES[args.optimizer]
+    dom = None
+    if phases:
+        cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
+        dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
+    alg = {
+        # bytes per launch, algorithmic (real, unpadded sizes): optimizer state r/w + streamed operand
+        "dW_in": P * opt_b + B * N * 2 + B * H * 2,
+        "dW_out": P * opt_b + B * N * 2 + B * H * 2,
+        "enc_gemm": P * 4 + B * N * 2,
+        "dec_gemm_mse": P * 4 + B * H * 2 + B * N * 2,
+        "dec_bwd_gemm": P * 4 + B * N * 2,
+    }
+    roof = None
+    if dom is not None:
+        if world > 1 and dom in ("dW_in", "dW_out"):
+            alg[dom] = P * 4 + B * N * 2 + B * H * 2     # gradient store instead of the fused update
+        ms = phases[dom]["mean_ms"]
+        ach = alg[dom] / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                "kernel_mean_us": round(ms * 1e3, 1), "alg_bytes_per_launch": int(alg[dom])}
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                tr = json.load(f).get(dom)
+            if tr:
+                roof["traffic"] = tr
+    ms_step = elapsed / args.steps * 1e3
+    step_flops = 10.0 * B * N * H
+    step_bytes = P * 2 * (opt_b + 4) + 2 * (3 * N * H) + 8 * (nnz / args.steps / max(world, 1))
+    line = {
+        "metric": METRIC, "value": round(nnz / elapsed, 1), "unit": "ratings/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": {"float16": "f16", "bfloat16": "bf16",
+                                                          "float32": "f32"}[args.dtype],
+        "data": "synthetic ML-20M-shaped fixed split (26,744 x 138,493, 20.0M ratings, seed 0); random-init weights",
+        "config": {"workload": "ml20m I-AutoRec train step (BASELINE configs[2])", "rows": n_rows, "N": N,
+                   "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
+                   "activation": "sigmoid", "dropout": args.dropout, "compute": args.dtype + " MFMA, fp32 accumulate",
+                   "parallelism": "dp%d" % world},
+        "masked_rmse": rmse,
+        "roofline": roof,
+        "step_roofline": {"alg_bytes": int(step_bytes), "alg_flops": int(step_flops),
+                          "hbm_bound_ms": round(step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 4),
+                          "mfma_bound_ms": round(step_flops / (MFMA_F16_PEAK_TFS * 1e12) * 1e3, 4),
+                          "frac_of_binding_roof": round(max(step_bytes / (HBM_PEAK_GBS * 1e9),
+                                                            step_flops / (MFMA_F16_PEAK_TFS * 1e12))
+                                                        / (ms_step * 1e-3), 4)},
+        "phases_ms": {k: round(v["mean_ms"], 4) for k, v in phases.items()},
+        "setup_s": round(setup_s, 1),
+    }
+    if world == 1 and args.cpu_baseline:
+        rows_b = [gen.rows_host[bi] for bi in batches[: args.cpu_steps]]
+        try:
+            line["cpu_baseline"] = cpu_baseline(data, rows_b, N, H, w0, lr, args.cpu_steps)
+        except Exception as e:  # the baseline is reported, never the measured value
+            line["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

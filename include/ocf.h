@@ -127,7 +127,9 @@ typedef struct OcfGemmArgs {
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
 
-/* split-K reductions fused with the layer epilogue (see OCF_EPI_BIAS_ACT / OCF_EPI_GRAD_ACT). */
+/* split-K reductions fused with the layer epilogue (see OCF_EPI_BIAS_ACT / OCF_EPI_GRAD_ACT).
+ * ocf_splitk_grad_act writes bias-gradient partials db[M/4][ld] (one row per 4 batch rows,
+ * already * gscale) for ocf_bias_opt_from_partials. */
 int ocf_splitk_bias_act(const float* slabs, int splits, int64_t split_stride, int M, int N, int64_t ld,
                         const float* bias, int act, float keep, uint64_t seed, uint64_t stream,
                         const uint8_t* mask_in, uint8_t* mask_out, float* a_out, void* h_out, int h_dtype,

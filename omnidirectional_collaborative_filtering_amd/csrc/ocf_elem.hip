@@ -10,40 +10,45 @@ namespace ocf {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
-// grid: N/64 column blocks; 256 threads = 64 columns x 4 row groups
+// Split-K reductions: grid (N/64, M/4); 256 threads = 64 columns x 4 rows, one output element per
+// thread, slabs summed in a fixed order (4 independent partial sums for memory-level parallelism).
+__device__ __forceinline__ float sum_slabs(const float* s, int splits, int64_t sstride) {
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= splits; k += 4) {
+    v0 += s[(int64_t)(k + 0) * sstride];
+    v1 += s[(int64_t)(k + 1) * sstride];
+    v2 += s[(int64_t)(k + 2) * sstride];
+    v3 += s[(int64_t)(k + 3) * sstride];
+  }
+  for (; k < splits; ++k) v0 += s[(int64_t)k * sstride];
+  return (v0 + v1) + (v2 + v3);
+}
+
 __global__ void __launch_bounds__(256) splitk_bias_act_kernel(const float* slabs, int splits, int64_t sstride, int M,
                                                               int N, BiasActParams p) {
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rg = threadIdx.x >> 6;
-  if (col >= N) return;
-  for (int m = rg; m < M; m += 4) {
-    const float* s = slabs + (int64_t)m * p.ld + col;
-    float v = 0.f;
-    for (int k = 0; k < splits; ++k) v += s[(int64_t)k * sstride];
-    bias_act_store(p, m, col, v);
-  }
+  const int m = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (col >= N || m >= M) return;
+  bias_act_store(p, m, col, sum_slabs(slabs + (int64_t)m * p.ld + col, splits, sstride));
 }
 
+// db_part[blockIdx.y][col] = gscale * sum of the block's 4 rows (fixed order)
 __global__ void __launch_bounds__(256) splitk_grad_act_kernel(const float* slabs, int splits, int64_t sstride, int M,
-                                                              int N, GradActParams p, float* db) {
+                                                              int N, GradActParams p, float* db_part) {
   __shared__ float part[4][64];
-  const int cl = threadIdx.x & 63;
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
-  const int rg = threadIdx.x >> 6;
-  float cs = 0.f;
-  if (col < N) {
-    for (int m = rg; m < M; m += 4) {
-      const float* s = slabs + (int64_t)m * p.ld + col;
-      float v = 0.f;
-      for (int k = 0; k < splits; ++k) v += s[(int64_t)k * sstride];
-      float d = grad_act_value(p, m, col, v);
-      store_ct(p.d_out, p.d_dtype, (int64_t)m * p.ld + col, d);
-      cs += d;
-    }
+  const int m = blockIdx.y * 4 + rg;
+  float d = 0.f;
+  if (col < N && m < M) {
+    d = grad_act_value(p, m, col, sum_slabs(slabs + (int64_t)m * p.ld + col, splits, sstride));
+    store_ct(p.d_out, p.d_dtype, (int64_t)m * p.ld + col, d);
   }
-  part[rg][cl] = cs;
+  part[rg][cl] = d;
   __syncthreads();
-  if (rg == 0 && col < N && db) db[col] = ((part[0][cl] + part[1][cl]) + (part[2][cl] + part[3][cl])) * p.gscale;
+  if (rg == 0 && col < N && db_part)
+    db_part[(int64_t)blockIdx.y * p.ld + col] = ((part[0][cl] + part[1][cl]) + (part[2][cl] + part[3][cl])) * p.gscale;
 }
 
 __global__ void opt_kernel(float* p, const float* g, float* s1, float* s2, int64_t n, OcfOptParams o) {
@@ -80,31 +85,37 @@ __global__ void bias_opt_partials_kernel(float* bvec, const float* db_part, int 
   if (s2) s2[i] = b;
 }
 
-// one block: out[0..2] = fixed-order sums of the per-tile stats; out[4+m] = row SSE
+// grid 1 + M/4: block 0 = fixed-order totals of the per-tile stats; block b>0 = row SSE of rows
+// 4(b-1)..4(b-1)+3, one wave per row (lane-strided over tiles, then a fixed butterfly).
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const float* sp, int n_parts, const float* rsp,
                                                              int n_tiles, int M, float* out) {
-  __shared__ float red[3][256];
   const int tid = threadIdx.x;
-  float a = 0.f, b = 0.f, c = 0.f;
-  for (int i = tid; i < n_parts; i += 256) {
-    a += sp[(int64_t)i * 4 + 0];
-    b += sp[(int64_t)i * 4 + 1];
-    c += sp[(int64_t)i * 4 + 2];
-  }
-  red[0][tid] = a; red[1][tid] = b; red[2][tid] = c;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s)
-      for (int k = 0; k < 3; ++k) red[k][tid] += red[k][tid + s];
-    __syncthreads();
-  }
-  if (tid == 0) { out[0] = red[0][0]; out[1] = red[1][0]; out[2] = red[2][0]; out[3] = 0.f; }
-  if (rsp)
-    for (int m = tid; m < M; m += 256) {
-      float r = 0.f;
-      for (int t = 0; t < n_tiles; ++t) r += rsp[(int64_t)t * M + m];
-      out[4 + m] = r;
+  if (blockIdx.x == 0) {
+    __shared__ float red[3][256];
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int i = tid; i < n_parts; i += 256) {
+      a += sp[(int64_t)i * 4 + 0];
+      b += sp[(int64_t)i * 4 + 1];
+      c += sp[(int64_t)i * 4 + 2];
     }
+    red[0][tid] = a; red[1][tid] = b; red[2][tid] = c;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+      if (tid < s)
+        for (int k = 0; k < 3; ++k) red[k][tid] += red[k][tid + s];
+      __syncthreads();
+    }
+    if (tid == 0) { out[0] = red[0][0]; out[1] = red[1][0]; out[2] = red[2][0]; out[3] = 0.f; }
+    return;
+  }
+  if (!rsp) return;
+  const int m = (blockIdx.x - 1) * 4 + (tid >> 6);
+  const int lane = tid & 63;
+  if (m >= M) return;
+  float r = 0.f;
+  for (int t = lane; t < n_tiles; t += 64) r += rsp[(int64_t)t * M + m];
+  for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+  if (lane == 0) out[4 + m] = r;
 }
 
 }  // namespace ocf
@@ -124,8 +135,8 @@ extern "C" int ocf_splitk_bias_act(const float* slabs, int splits, int64_t split
   p.bias = bias; p.act = act; p.keep = keep; p.seed = seed; p.stream = stream; p.mask_in = mask_in;
   p.mask_out = mask_out; p.a_out = a_out; p.h_out = h_out; p.h_dtype = h_dtype; p.ld = ld;
   p.m_real = m_real; p.n_real = n_real;
-  hipLaunchKernelGGL(splitk_bias_act_kernel, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)hstream, slabs, splits,
-                     split_stride, M, N, p);
+  hipLaunchKernelGGL(splitk_bias_act_kernel, dim3((N + 63) / 64, (M + 3) / 4), dim3(256), 0, (hipStream_t)hstream,
+                     slabs, splits, split_stride, M, N, p);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }
@@ -138,8 +149,8 @@ extern "C" int ocf_splitk_grad_act(const float* slabs, int splits, int64_t split
   GradActParams p;
   p.a = a_in; p.mask = mask; p.keep = keep; p.act = act; p.d_out = d_out; p.d_dtype = d_dtype; p.ld = ld;
   p.db_part = nullptr; p.gscale = gscale; p.m_real = m_real; p.n_real = n_real;
-  hipLaunchKernelGGL(splitk_grad_act_kernel, dim3((N + 63) / 64), dim3(256), 0, (hipStream_t)hstream, slabs, splits,
-                     split_stride, M, N, p, db);
+  hipLaunchKernelGGL(splitk_grad_act_kernel, dim3((N + 63) / 64, (M + 3) / 4), dim3(256), 0, (hipStream_t)hstream,
+                     slabs, splits, split_stride, M, N, p, db);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }
@@ -171,8 +182,8 @@ extern "C" int ocf_stats_finalize(const float* stats_part, int n_parts, const fl
                                   float* out, void* stream) {
   OCF_TRY_BEGIN
   OCF_CHECK(stats_part && out, "ocf_stats_finalize: null pointer");
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats_part, n_parts,
-                     row_sse_part, n_tiles, M, out);
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3(1 + (M + 3) / 4), dim3(256), 0, (hipStream_t)stream, stats_part,
+                     n_parts, row_sse_part, n_tiles, M, out);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

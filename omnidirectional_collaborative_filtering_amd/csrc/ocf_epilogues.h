@@ -178,9 +178,14 @@ struct EpiGradStore {
   }
 };
 
-// ---- fused optimizer: weight-gradient tile never leaves registers -----------------------
+// ---- fused optimizer: the weight-gradient tile never reaches HBM ------------------------
+// The 128x128 fp32 gradient tile is staged in LDS (operand buffers are free by now), then each
+// thread streams 16 float4 chunks of the parameter / optimizer-state rows (512 contiguous bytes
+// per tile row, 4 chunks = 8-12 16-B loads in flight per lane), applies the Keras update and
+// writes them back.  This is the HBM-bound part of the step (16 B/param for Adagrad).
 struct EpiOptim {
-  static constexpr int LDS_NEED = 0;
+  static constexpr int YS = GT_BN + 4;
+  static constexpr int LDS_NEED = GT_BM * YS * 4;
   struct Params {
     float* p;
     float* s1;
@@ -189,17 +194,43 @@ struct EpiOptim {
     OcfOptParams op;
   };
   __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
-    OcfOptParams o = p.op;
-    for_each_acc(acc, c, [&](int m, int n, float v) {
-      int64_t idx = (int64_t)m * p.ld + n;
-      float w = p.p[idx];
-      float a = p.s1 ? p.s1[idx] : 0.f;
-      float b = p.s2 ? p.s2[idx] : 0.f;
-      opt_update(o, v * o.gscale, w, a, b);
-      p.p[idx] = w;
-      if (p.s1) p.s1[idx] = a;
-      if (p.s2) p.s2[idx] = b;
-    });
+    float* Y = reinterpret_cast<float*>(c.lds);
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Y[(c.wm + acc_row(bi, r, c.lane)) * YS + c.wn + acc_col(bj, c.lane)] = acc[bi][bj][r];
+    __syncthreads();
+    const OcfOptParams o = p.op;
+    constexpr int CH = GT_BM * (GT_BN / 4) / GT_THREADS;   // 16 chunks of 4 per thread
+    constexpr int U = 4;
+#pragma unroll 1
+    for (int g = 0; g < CH; g += U) {
+      float4 pv[U], av[U], bv[U], gv[U];
+      int64_t off[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int ch = c.tid + (g + u) * GT_THREADS;
+        const int ml = ch >> 5, c4 = (ch & 31) * 4;
+        off[u] = (int64_t)(c.m0 + ml) * p.ld + c.n0 + c4;
+        gv[u] = *reinterpret_cast<const float4*>(Y + ml * YS + c4);
+        pv[u] = *reinterpret_cast<const float4*>(p.p + off[u]);
+        av[u] = p.s1 ? *reinterpret_cast<const float4*>(p.s1 + off[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[u] = p.s2 ? *reinterpret_cast<const float4*>(p.s2 + off[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        opt_update(o, gv[u].x * o.gscale, pv[u].x, av[u].x, bv[u].x);
+        opt_update(o, gv[u].y * o.gscale, pv[u].y, av[u].y, bv[u].y);
+        opt_update(o, gv[u].z * o.gscale, pv[u].z, av[u].z, bv[u].z);
+        opt_update(o, gv[u].w * o.gscale, pv[u].w, av[u].w, bv[u].w);
+        *reinterpret_cast<float4*>(p.p + off[u]) = pv[u];
+        if (p.s1) *reinterpret_cast<float4*>(p.s1 + off[u]) = av[u];
+        if (p.s2) *reinterpret_cast<float4*>(p.s2 + off[u]) = bv[u];
+      }
+    }
   }
 };
 

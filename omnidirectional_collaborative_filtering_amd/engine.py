@@ -145,7 +145,8 @@ class Engine:
             [None] * len(self.Hp)
         self.d_out = torch.zeros(Bp, self.Np, device=d, dtype=self.tdt)
         self.db_out_part = torch.zeros(Bp // TILE, self.Np, device=d, dtype=torch.float32)
-        self.db_h = [torch.zeros(Bp // TILE, h, device=d, dtype=torch.float32) for h in self.Hp]
+        # bias-gradient partials: Bp/4 rows from the split-K reduction, Bp/128 from GRAD_ACT tiles
+        self.db_h = [torch.zeros(Bp // 4, h, device=d, dtype=torch.float32) for h in self.Hp]
         self.splits0 = self._pick_splits(self.pad_dims[0], self.Hp[0])
         self.splitsL = self._pick_splits(self.Np, self.Hp[-1])
         smax = max(self.splits0 * self.Hp[0], self.splitsL * self.Hp[-1])
@@ -163,6 +164,39 @@ class Engine:
         self._grow_stats(64)
         self.n_stats = 0
         self.dense_in = None
+        self.timers = None          # {phase: [(start_event, end_event), ...]} when profiling
+
+    # ---------------------------------------------------------------- phase timing (bench.py)
+    def enable_timers(self, on=True):
+        self.timers = {} if on else None
+
+    class _Phase:
+        def __init__(self, eng, name):
+            self.eng, self.name = eng, name
+
+        def __enter__(self):
+            if self.eng.timers is not None:
+                self.s = torch.cuda.Event(enable_timing=True)
+                self.s.record()
+            return self
+
+        def __exit__(self, *exc):
+            if self.eng.timers is not None:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                self.eng.timers.setdefault(self.name, []).append((self.s, e))
+            return False
+
+    def phase(self, name):
+        return Engine._Phase(self, name)
+
+    def phase_times_ms(self):
+        """mean / total milliseconds per phase (call after synchronize)."""
+        out = {}
+        for k, v in (self.timers or {}).items():
+            ts = [a.elapsed_time(b) for a, b in v]
+            out[k] = {"mean_ms": float(np.mean(ts)), "total_ms": float(np.sum(ts)), "n": len(ts)}
+        return out
 
     def _pick_splits(self, K, Hp):
         bk = 32 if self.cdt == _lib.DT_F32 else 64
@@ -214,7 +248,8 @@ class Engine:
         """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller)."""
         self._grow_buckets(max_targets)
         a.bk_rc, a.bk_t, a.bk_m = ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m)
-        call("ocf_scatter_batch", a, cur_stream())
+        with self.phase("scatter"):
+            call("ocf_scatter_batch", a, cur_stream())
 
     def load_dense(self, inputs, out_mask, targets):
         """API path: dense arrays (torch/numpy) in the model.py input order."""
@@ -273,8 +308,9 @@ class Engine:
         # layer 0: split-K over the (k x Np)-wide input
         Hp0 = self.Hp[0]
         sstride = Bp * Hp0
-        self._gemm(self.xin, 0, self.pad_dims[0], self.W[0], _lib.DT_F32, 1, Hp0, Bp, Hp0, self.pad_dims[0],
-                   _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
+        with self.phase("enc_gemm"):
+            self._gemm(self.xin, 0, self.pad_dims[0], self.W[0], _lib.DT_F32, 1, Hp0, Bp, Hp0, self.pad_dims[0],
+                       _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
         call("ocf_splitk_bias_act", ptr(self.slabs), self.splits0, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
              keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
              ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
@@ -288,6 +324,14 @@ class Engine:
         """Decoder GEMM with the fused masked-MSE epilogue; stats -> stats_hist[n_stats]."""
         L = len(self.H)
         gscale = 2.0 / (self.B * self.N)
+        with self.phase("dec_gemm_mse"):
+            self._gemm_mse(L, gscale, with_grad)
+        self._grow_stats(self.n_stats + 1)
+        call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
+             self.n_tiles, self.Bp, ptr(self.stats_hist[self.n_stats]), cur_stream())
+        self.n_stats += 1
+
+    def _gemm_mse(self, L, gscale, with_grad):
         self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 1, self.Np, self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], bk_ptr=self.bk_ptr,
                    bk_rc=self.bk_rc, bk_t=self.bk_t, bk_m=self.bk_m,
@@ -295,10 +339,6 @@ class Engine:
                    db_part=self.db_out_part if with_grad else None, ld_db=self.Np,
                    opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
                    stats_part=self.stats_part, row_sse_part=self.row_sse_part)
-        self._grow_stats(self.n_stats + 1)
-        call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
-             self.n_tiles, self.Bp, ptr(self.stats_hist[self.n_stats]), cur_stream())
-        self.n_stats += 1
 
     def predict_dense(self, out_mask, out):
         """PREDICT epilogue: out[B][N] = out_mask * (h W + b)."""
@@ -322,16 +362,18 @@ class Engine:
         # delta of the last hidden layer: split-K over Np
         HpL = self.Hp[L - 1]
         sstride = Bp * HpL
-        self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 0, self.Np, Bp, HpL, self.Np, _lib.EPI_SLAB,
-                   splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
+        with self.phase("dec_bwd_gemm"):
+            self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 0, self.Np, Bp, HpL, self.Np, _lib.EPI_SLAB,
+                       splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
         db_last = self.db_h[L - 1]
         call("ocf_splitk_grad_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.a[L - 1]),
              ptr(self.mask[L - 1]), self.keep, self.act, ptr(self.dh[L - 1]), self.cdt, ptr(db_last[0]), gscale,
              self.B, self.H[L - 1], s)
         # output layer bias + weights
         self._bias_update(L, self.db_out_part, Bp // TILE, self.Np, self.Np, grads_out, op)
-        self._weight_update(L, self.h[L - 1], HpL, self.d_out, self.Np, HpL, self.Np, gscale, grads_out, op)
-        parts_last = 1
+        with self.phase("dW_out"):
+            self._weight_update(L, self.h[L - 1], HpL, self.d_out, self.Np, HpL, self.Np, gscale, grads_out, op)
+        parts_last = Bp // 4
         for i in range(L - 1, 0, -1):
             # delta of hidden layer i-1 through W_i (before W_i changes)
             self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
@@ -344,8 +386,9 @@ class Engine:
                                 self.Hp[i], gscale, grads_out, op)
             parts_last = Bp // TILE
         self._bias_update(0, self.db_h[0], parts_last, self.Hp[0], self.Hp[0], grads_out, op)
-        self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0], self.Hp[0],
-                            gscale, grads_out, op)
+        with self.phase("dW_in"):
+            self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0],
+                                self.Hp[0], gscale, grads_out, op)
         if fused:
             self.opt.iterations += 1
 

@@ -195,3 +195,33 @@ def scatter_rows_numpy(row_ptr, col, val, rows, N, keep=None, aux=-1.0, pass_thr
     t[r[tgt], c[tgt]] = v[tgt]
     m_miss[r, c] = aux
     return m_in, m_out, x, t, m_miss
+
+
+def train_batch_loop_csr(row_ptr, col, val, rows, N, s_range=(1.0, 1.0), aux=-1.0, pass_through=True):
+    """build_sparse_batch (data_reader.py:95-200) over a CSR instead of dicts: same float64 zeros,
+    same per-batch uniform and per-row choice draws, same per-rating scalar stores.  This is the
+    scalar CPU baseline bench.py times (one core)."""
+    B = len(rows)
+    m_in = np.zeros([B, N])
+    x = np.zeros([B, N])
+    m_miss = np.zeros([B, N])
+    t = np.zeros([B, N])
+    m_out = np.zeros([B, N])
+    s_rows = np.random.uniform(low=s_range[0], high=s_range[1], size=B)
+    for r in range(B):
+        lo, hi = int(row_ptr[rows[r]]), int(row_ptr[rows[r] + 1])
+        split = np.random.choice([0, 1], size=hi - lo, p=[1 - s_rows[r], s_rows[r]])
+        for j in range(lo, hi):
+            c = col[j]
+            v = val[j]
+            if split[j - lo] == 1:
+                m_in[r, c] = aux
+                x[r, c] = v
+                if pass_through:
+                    m_out[r, c] = aux
+                    t[r, c] = v
+            else:
+                m_out[r, c] = aux
+                t[r, c] = v
+            m_miss[r, c] = aux
+    return m_in, m_out, x, t, m_miss
