@@ -123,42 +123,53 @@ class BatchGenerator(object):
         self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if reader.rng == "device" else 0
 
     # ------------------------------------------------------------ epoch plan
+    def plan(self, row_lengths1, row_lengths2=None):
+        """Host half of the epoch plan (no GPU): permutation, batch rows, batch-local entry offsets
+        and -- for train batches with rng='numpy' -- the reciprocal keep flags, drawing from the
+        NumPy global RNG exactly as data_reader.py:120,130,326-327 do."""
+        order = np.random.permutation(self.n) if self.shuffle else np.arange(self.n)   # :326-327
+        nb, B = self.num_batches, self.B
+        rows = order[: nb * B].reshape(nb, B).astype(np.int64)
+        lens1 = row_lengths1[rows]                       # [nb, B]
+        boff = np.zeros((nb, B + 1), dtype=np.int64)
+        np.cumsum(lens1, axis=1, out=boff[:, 1:])
+        tcount = row_lengths2[rows].sum(axis=1) if row_lengths2 is not None else None
+        keep = None
+        if self.split == "train" and self.r.rng == "numpy":
+            s0, s1 = float(self.sparsity[0]), float(self.sparsity[1])
+            keeps = []
+            for bi in range(nb):
+                s_rows = np.random.uniform(low=s0, high=s1, size=B)                    # :120
+                u = np.random.random_sample(int(boff[bi, -1]))                          # :130, one call/batch
+                cut = (1.0 - s_rows) / ((1.0 - s_rows) + s_rows)
+                keeps.append(u >= np.repeat(cut, lens1[bi]))
+            if not (s0 >= 1.0 and s1 >= 1.0):
+                keep = np.concatenate(keeps) if keeps else np.zeros(0, bool)
+        return rows, boff, tcount, keep
+
     def _start(self):
         self.started = True
         r = self.r
         dev = r._on_device()
-        order = np.random.permutation(self.n) if self.shuffle else np.arange(self.n)   # :326-327
-        nb, B = self.num_batches, self.B
-        rows = order[: nb * B].reshape(nb, B).astype(np.int64)
-        self.rows_host = rows
         if self.split == "train":
             self.src1, self.src2 = dev["train"], None
         elif self.split == "valid":
             self.src1, self.src2 = dev["valid_in"], dev["valid_tgt"]
         else:
             self.src1, self.src2 = dev["test_in"], dev["test_tgt"]
-        lens1 = self.src1.lens[rows]                      # [nb, B]
-        boff = np.zeros((nb, B + 1), dtype=np.int64)
-        np.cumsum(lens1, axis=1, out=boff[:, 1:])
+        rows, boff, self.tcount, keep = self.plan(self.src1.lens, None if self.src2 is None else self.src2.lens)
+        nb = self.num_batches
+        self.rows_host = rows
         self.nnz1 = boff[:, -1].copy()
-        self.tcount = self.src2.lens[rows].sum(axis=1) if self.src2 is not None else None
         self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
         self.boff_dev = torch.as_tensor(boff, device=r.device)
         self.keep_dev = None
         self.keep_off = None
-        if self.split == "train" and r.rng == "numpy":
-            s0, s1 = float(self.sparsity[0]), float(self.sparsity[1])
-            keeps = []
-            for bi in range(nb):
-                s_rows = np.random.uniform(low=s0, high=s1, size=B)                    # :120
-                u = np.random.random_sample(int(self.nnz1[bi]))                         # :130, one call/batch
-                cut = (1.0 - s_rows) / ((1.0 - s_rows) + s_rows)
-                keeps.append(u >= np.repeat(cut, lens1[bi]))
-            if not (s0 >= 1.0 and s1 >= 1.0):
-                flat = np.concatenate(keeps) if keeps else np.zeros(0, bool)
-                self.keep_dev = torch.as_tensor(flat.astype(np.uint8), device=r.device)
-                self.keep_off = np.concatenate([[0], np.cumsum(self.nnz1)])
-        self.max_targets = int(max(self.nnz1.max() if nb else 0, self.tcount.max() if (self.tcount is not None and nb) else 0))
+        if keep is not None:
+            self.keep_dev = torch.as_tensor(keep.astype(np.uint8), device=r.device)
+            self.keep_off = np.concatenate([[0], np.cumsum(self.nnz1)])
+        self.max_targets = int(max(self.nnz1.max() if nb else 0,
+                                   self.tcount.max() if (self.tcount is not None and nb) else 0))
 
     def scatter_args(self, bi, engine_args=None, dense=None, B_pad=None):
         """OcfScatterArgs for batch bi (onto an engine's xin/buckets and/or dense outputs)."""

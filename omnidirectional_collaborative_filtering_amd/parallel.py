@@ -32,11 +32,11 @@ def init_from_env(backend=None):
 class GradBucket:
     """All parameter gradients of an Engine as views into ONE flat fp32 buffer (one collective)."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, dtype=torch.float32):
         sizes = []
         for w, b in zip(engine.W, engine.b):
             sizes += [w.numel(), b.numel()]
-        self.flat = torch.zeros(sum(sizes), device=engine.dev, dtype=torch.float32)
+        self.flat = torch.zeros(sum(sizes), device=engine.dev, dtype=dtype)
         self.views = []
         off = 0
         shapes = []

@@ -1,0 +1,81 @@
+"""CPU: libocf.so loads, exports every function include/ocf.h declares, and the ctypes mirrors of the
+ABI structs have exactly the C layout (sizes and offsets from gcc on the same header).  No compute
+calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from omnidirectional_collaborative_filtering_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "ocf.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ocf_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_expected_entry_points():
+    fns = declared_functions()
+    for must in ("ocf_scatter_batch", "ocf_gemm", "ocf_opt_step", "ocf_splitk_bias_act", "ocf_splitk_grad_act",
+                 "ocf_stats_finalize", "ocf_last_error", "ocf_version"):
+        assert must in fns
+    assert set(fns) == set(_lib.SIGNATURES), set(fns) ^ set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    lib = _lib.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.ocf_version() >= 1
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for name in declared_functions():
+        assert re.search(r"\bT %s\b" % name, out), name
+
+
+STRUCTS = {
+    "OcfOptParams": (_lib.OcfOptParams, ["kind", "lr", "gscale"]),
+    "OcfScatterArgs": (_lib.OcfScatterArgs, ["keep1", "s0", "seed", "mode", "rows2", "aux", "ld", "xin_dtype",
+                                             "feed", "tile_cnt", "n_tiles"]),
+    "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
+                                       "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part"]),
+}
+
+
+def test_struct_layout_matches_c():
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "%s"' % HDR, "int main(void) {"]
+    for s, (_, fields) in STRUCTS.items():
+        lines.append('printf("%s size %%zu\\n", sizeof(%s));' % (s, s))
+        for f in fields:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (s, f, s, f))
+    lines.append("return 0; }")
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "layout.c")
+        with open(c, "w") as fh:
+            fh.write("\n".join(lines))
+        exe = os.path.join(d, "layout")
+        subprocess.run(["gcc", "-std=c99", "-o", exe, c], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    got = {}
+    for line in out.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for s, (cls, fields) in STRUCTS.items():
+        assert ctypes.sizeof(cls) == got[(s, "size")], s
+        for f in fields:
+            assert getattr(cls, f).offset == got[(s, f)], (s, f)
+
+
+def test_errors_are_reported_not_silent():
+    """A bad call fails loudly with a message (no compute happens: argument validation only)."""
+    a = _lib.OcfGemmArgs()
+    a.M, a.N, a.K = 100, 128, 64       # M not a multiple of 128
+    a.A = a.B = 1
+    with pytest.raises(_lib.OcfError, match="multiples of 128"):
+        _lib.call("ocf_gemm", a, None)

@@ -1,0 +1,93 @@
+"""CPU: the oracle restatement of data_reader.py is pinned to the reference's own outputs
+(tests/golden/batches.npz, produced by importing /root/reference/data_reader.py), and the host half
+of the product's epoch plan (permutation + NumPy-exact reciprocal draws) reproduces them too."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.batch_oracle import ReaderOracle, reciprocal_cut, scatter_rows_numpy
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOY = os.path.join(GOLD, "toy")
+
+
+def _cfg():
+    with open(os.path.join(GOLD, "batches_config.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(os.path.join(GOLD, "batches.npz"))
+
+
+def _drain(gen, n):
+    out = [next(gen) for _ in range(n)]
+    assert next(gen) is None
+    return out
+
+
+@pytest.mark.parametrize("ci", range(5))
+def test_oracle_reproduces_reference(gold, ci):
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    B = cfg["B"]
+    np.random.seed(cfg["seed_base"] + ci)
+    rd = ReaderOracle.from_dir(TOY)
+    seq = [("train1", rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through=pt), len(rd.train_keys)),
+           ("valid", rd.data_gen(B, sp, "valid", True, aux_type, auxv, return_target_count=True), len(rd.valid_keys)),
+           ("test", rd.data_gen(B, sp, "test", True, aux_type, auxv, return_target_count=True), len(rd.test_keys)),
+           ("train2", rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through=pt), len(rd.train_keys))]
+    for tag, gen, n in seq:
+        for bi, item in enumerate(_drain(gen, n // B)):
+            for k, a in enumerate(item[0]):
+                np.testing.assert_array_equal(a, gold["%s/%s/%d/in%d" % (name, tag, bi, k)])
+            np.testing.assert_array_equal(item[1], gold["%s/%s/%d/targets" % (name, tag, bi)])
+            if len(item) == 3:
+                assert item[2] == int(gold["%s/%s/%d/count" % (name, tag, bi)])
+
+
+@pytest.mark.parametrize("s", [0.0, 0.123456, 0.3, 0.5, 0.7, 0.9999, 1.0])
+def test_choice_restatement(s):
+    np.random.seed(7)
+    a = np.random.choice([0, 1], size=5000, p=[1 - s, s])
+    np.random.seed(7)
+    u = np.random.random_sample(5000)
+    np.testing.assert_array_equal(a, (u >= reciprocal_cut(s)).astype(int))
+
+
+def test_uniform_and_stream_concatenation():
+    np.random.seed(3)
+    x = np.random.uniform(0.2, 0.9, 5)
+    y = np.concatenate([np.random.random_sample(4), np.random.random_sample(6)])
+    np.random.seed(3)
+    assert np.array_equal(x, 0.2 + (0.9 - 0.2) * np.random.random_sample(5))
+    assert np.array_equal(y, np.random.random_sample(10))
+
+
+@pytest.mark.parametrize("ci", range(5))
+def test_product_epoch_plan_matches_reference(gold, ci):
+    """BatchGenerator.plan (host) + the vectorised scatter reproduce the reference train batches."""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    B = cfg["B"]
+    meta = cfg["meta"]
+    np.random.seed(cfg["seed_base"] + ci)
+    rd = data_reader(meta["num_users"], meta["num_items"], TOY, eval_mode="fixed_split", reverse_user_item_data=True)
+    gen = rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through_input_training=pt)
+    tr = rd.data.train
+    rows, boff, _, keep = gen.plan(tr.row_lengths())
+    for bi in range(len(rows)):
+        kb = None
+        if keep is not None:
+            start = int(sum(boff[j, -1] for j in range(bi)))
+            kb = keep[start: start + int(boff[bi, -1])]
+        m_in, m_out, x, t, m_miss = scatter_rows_numpy(tr.row_ptr, tr.col, tr.val, rows[bi], rd.num_items, keep=kb,
+                                                       aux=auxv, pass_through=pt)
+        np.testing.assert_array_equal(x, gold["%s/train1/%d/in0" % (name, bi)])
+        np.testing.assert_array_equal(t, gold["%s/train1/%d/targets" % (name, bi)])
+        out_mask = gold["%s/train1/%d/in%d" % (name, bi, 1 if aux_type is None else 2)]
+        np.testing.assert_array_equal(m_out, out_mask)
