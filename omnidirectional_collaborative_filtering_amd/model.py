@@ -55,6 +55,26 @@ class Model(object):
         self.metric_names = []
         self.rating_range = float(rating_range)
         self.stop_training = False
+        self.rank, self.world, self.bucket = 0, 1, None
+
+    def enable_data_parallel(self, rank, world):
+        """Row data parallelism (parallel.py): call after torch.distributed is initialised."""
+        from .parallel import GradBucket
+        self.rank, self.world = int(rank), int(world)
+        self.bucket = GradBucket(self.engine) if world > 1 else None
+
+    def _train_one(self, gen):
+        """One optimizer step; under data parallelism rank r takes the r-th of the next `world` batches."""
+        from .parallel import dp_train_step
+        if self.world > 1 and isinstance(gen, BatchGenerator):
+            idx = [gen.next_batch_index() for _ in range(self.world)]
+            if idx[-1] is None:
+                raise StopIteration("generator exhausted")
+            self._check_gen(gen)
+            self._load(None, gen, idx[self.rank])
+        else:
+            self._pull(gen)
+        dp_train_step(self.engine, self.bucket, self.world)
 
     # ------------------------------------------------------------------ compile
     def compile(self, optimizer, loss="mean_squared_error", metrics=None, rating_range=None):
@@ -154,10 +174,11 @@ class Model(object):
         steps = int(steps_per_epoch)
         for epoch in range(initial_epoch, epochs):
             t0 = time.time()
-            for _ in range(steps):
-                self._pull(generator)
-                self.engine.train_step()
+            for _ in range(steps // self.world if self.world > 1 else steps):
+                self._train_one(generator)
             logs = self._logs_from_stats(self.engine.take_stats())
+            if self.world > 1:
+                logs = self._mean_over_ranks(logs)
             if validation_data is not None:
                 vals = self.evaluate_generator(validation_data, validation_steps)
                 vals = vals if isinstance(vals, list) else [vals]
@@ -175,6 +196,13 @@ class Model(object):
             if self.stop_training:
                 break
         return hist
+
+    def _mean_over_ranks(self, logs):
+        import torch.distributed as dist
+        keys = sorted(logs)
+        t = torch.tensor([logs[k] for k in keys], dtype=torch.float64, device=self.engine.dev)
+        dist.all_reduce(t)
+        return {k: float(v) / self.world for k, v in zip(keys, t.tolist())}
 
     def evaluate_generator(self, generator, steps, **kw):
         steps = int(steps)

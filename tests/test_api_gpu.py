@@ -1,0 +1,96 @@
+"""GPU: the drop-in surfaces end to end -- train.py driver, Keras-style fit on dense arrays
+(train_jester.py:78-79), predict, train_on_batch on user arrays vs the generator fast path,
+checkpoint save/load."""
+import numpy as np
+import pytest
+
+from oracle.batch_oracle import scatter_rows_numpy
+from oracle.model_oracle import OmniOracle
+
+
+def _data(rows=600, cols=200, nnz=9000, seed=2):
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=seed)
+    return split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(seed))
+
+
+@pytest.mark.gpu
+def test_trainer_end_to_end(gpu, tmp_path):
+    from omnidirectional_collaborative_filtering_amd import train
+    cfg = dict(train.DEFAULTS)
+    cfg.update(synthetic="ml100k", max_epochs=3, batch_size=128, num_hidden_units=64, patience=5,
+               model_save_path=str(tmp_path), compute_dtype="float16", seed=4)
+    out = train.run(cfg)
+    assert np.isfinite(out["manual_test_RMSE"]) and 0.3 < out["manual_test_RMSE"] < 5.0
+    assert out["epochs_run"] == 3
+
+
+@pytest.mark.gpu
+def test_predict_matches_oracle(gpu):
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rng = np.random.RandomState(0)
+    B, N, H = 128, 150, 40
+    om = omni_model(2, H, N, B, dense_activation="tanh", use_causal_info=True, compute_dtype="float32", seed=2)
+    x = rng.rand(B, N) * (rng.rand(B, N) < 0.1)
+    obs = -1.0 * (x != 0)
+    mask = -1.0 * (rng.rand(B, N) < 0.2)
+    y = om.model.predict([x, obs, mask]).cpu().numpy()
+    w = om.model.get_weights()
+    ora = OmniOracle([2 * N, H, H, N], activation="tanh").set_params(w[0::2], w[1::2])
+    ref, _ = ora.forward(np.concatenate([x, obs], 1), mask)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_dense_train_on_batch_equals_generator_path(gpu):
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    from omnidirectional_collaborative_filtering_amd.optimizers import Adagrad
+    data = _data()
+    N = data.num_cols
+    np.random.seed(9)
+    rd = data_reader(N, 600, dataset=data, eval_mode="fixed_split")
+    a = omni_model(1, 32, N, 128, "sigmoid", use_causal_info=False, compute_dtype="float32", seed=5).model
+    b = omni_model(1, 32, N, 128, "sigmoid", use_causal_info=False, compute_dtype="float32", seed=5).model
+    a.compile(Adagrad(lr=0.01), "mean_squared_error")
+    b.compile(Adagrad(lr=0.01), "mean_squared_error")
+    gen = rd.data_gen(128, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    la = a.fit_generator(gen, 2, verbose=0).history["loss"][0]
+    lbs = []
+    for bi in range(2):
+        _, m_out, x, t, _ = scatter_rows_numpy(data.train.row_ptr, data.train.col, data.train.val, gen.rows_host[bi],
+                                               N, aux=-1.0)
+        lbs.append(b.train_on_batch([x, m_out], t))
+    assert abs(la - np.mean(lbs)) <= 1e-6 * abs(la)
+    for wa, wb in zip(a.get_weights(), b.get_weights()):
+        np.testing.assert_array_equal(wa, wb)
+
+
+@pytest.mark.gpu
+def test_jester_style_fit_and_checkpoint(gpu, tmp_path):
+    """train_jester.py params: 2x256 hidden, causal concat, rmsprop, reciprocal 0.5 split sampled once."""
+    from omnidirectional_collaborative_filtering_amd.model import EarlyStopping, omni_model
+    rng = np.random.RandomState(1)
+    n, N = 1280, 100
+    data = np.where(rng.rand(n, N) < 0.56, rng.uniform(-10, 10, (n, N)), 99.0)
+    observed = (data != 99).astype(np.float64)
+    drop = rng.choice([0, 1], size=data.shape, p=[0.5, 0.5])
+    in_m, out_m = drop * observed, (1 - drop) * observed
+    inputs, targets = np.where(in_m > 0, data, 0.0), np.where(out_m > 0, data, 0.0)
+    om = omni_model(2, 256, N, 128, dense_activation="tanh", use_causal_info=True, compute_dtype="bfloat16", seed=3,
+                    rating_range=20)
+    m = om.model
+    m.compile("rmsprop", "mean_squared_error", metrics=["mae", "accurate_MAE", "nMAE"])
+    h = m.fit([inputs, observed, out_m], targets, batch_size=128, validation_split=0.1, epochs=4, shuffle=True,
+              callbacks=[EarlyStopping(monitor="val_loss", patience=3)])
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    assert "val_loss" in h.history and "val_nMAE" in h.history
+    p = str(tmp_path / "ck.safetensors")
+    m.save(p)
+    w = m.get_weights()
+    om2 = omni_model(2, 256, N, 128, dense_activation="tanh", use_causal_info=True, compute_dtype="bfloat16", seed=99)
+    om2.model.compile("rmsprop", "mean_squared_error")
+    om2.model.load(p)
+    for a, b in zip(w, om2.model.get_weights()):
+        np.testing.assert_array_equal(a, b)
+    assert om2.model.optimizer.iterations == m.optimizer.iterations
