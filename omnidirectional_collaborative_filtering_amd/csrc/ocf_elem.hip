@@ -65,12 +65,20 @@ __global__ void opt_kernel(float* p, const float* g, float* s1, float* s2, int64
   }
 }
 
-__global__ void bias_opt_partials_kernel(float* bvec, const float* db_part, int parts, int64_t ld, int n, float* s1,
-                                         float* s2, float* g_out, OcfOptParams o) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float g = 0.f;
-  for (int k = 0; k < parts; ++k) g += db_part[(int64_t)k * ld + i];
+// grid n/64; 256 threads = 64 columns x 4 partial groups; fixed summation order
+__global__ void __launch_bounds__(256) bias_opt_partials_kernel(float* bvec, const float* db_part, int parts,
+                                                                int64_t ld, int n, float* s1, float* s2, float* g_out,
+                                                                OcfOptParams o) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + cl;
+  float part = 0.f;
+  if (i < n)
+    for (int k = grp; k < parts; k += 4) part += db_part[(int64_t)k * ld + i];
+  red[grp][cl] = part;
+  __syncthreads();
+  if (grp != 0 || i >= n) return;
+  const float g = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
   if (g_out) {           // data-parallel: hand the gradient to the all-reduce instead
     g_out[i] = g;
     return;
@@ -172,7 +180,7 @@ extern "C" int ocf_bias_opt_from_partials(float* b, const float* db_part, int pa
   OCF_TRY_BEGIN
   OCF_CHECK(b && db_part && opt, "ocf_bias_opt_from_partials: null pointer");
   if (n == 0) return 0;
-  hipLaunchKernelGGL(bias_opt_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, b, db_part,
+  hipLaunchKernelGGL(bias_opt_partials_kernel, dim3((n + 63) / 64), dim3(256), 0, (hipStream_t)stream, b, db_part,
                      parts, ld, n, s1, s2, g_out, *opt);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END

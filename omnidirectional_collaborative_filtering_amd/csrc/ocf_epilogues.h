@@ -5,6 +5,12 @@
 
 namespace ocf {
 
+struct NoPre {};
+#define OCF_NO_PROLOGUE                                                                            \
+  using Pre = NoPre;                                                                             \
+  template <class P>                                                                             \
+  __device__ static Pre prologue(const P&, int, int, int, int, int, const GemmShape&) { return {}; }
+
 template <class F>
 __device__ __forceinline__ void for_each_acc(ocf_f16v (&acc)[2][2], const TileCtx& c, F&& f) {
 #pragma unroll
@@ -47,13 +53,14 @@ __device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float
 
 // ---- split-K partial slab: out[split][m][n] --------------------------------------------
 struct EpiSlab {
+  OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
     float* out;
     int64_t ld;
     int64_t split_stride;
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     float* o = p.out + (int64_t)c.split * p.split_stride;
     for_each_acc(acc, c, [&](int m, int n, float v) { o[(int64_t)m * p.ld + n] = v; });
   }
@@ -95,9 +102,10 @@ __device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, in
 }
 
 struct EpiBiasAct {
+  OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   using Params = BiasActParams;
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     for_each_acc(acc, c, [&](int m, int n, float v) { bias_act_store(p, m, n, v); });
   }
 };
@@ -131,9 +139,10 @@ __device__ __forceinline__ void store_ct(void* out, int dtype, int64_t idx, floa
 }
 
 struct EpiGradAct {
+  OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 2 * GT_BN * 4;
   using Params = GradActParams;
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     float colsum[2] = {0.f, 0.f};
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
@@ -167,13 +176,14 @@ struct EpiGradAct {
 
 // ---- raw gradient store (data-parallel path: all-reduce before the optimizer) ------------
 struct EpiGradStore {
+  OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
     float* g;
     int64_t ld;
     float gscale;
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     for_each_acc(acc, c, [&](int m, int n, float v) { p.g[(int64_t)m * p.ld + n] = v * p.gscale; });
   }
 };
@@ -184,6 +194,7 @@ struct EpiGradStore {
 // per tile row, 4 chunks = 8-12 16-B loads in flight per lane), applies the Keras update and
 // writes them back.  This is the HBM-bound part of the step (16 B/param for Adagrad).
 struct EpiOptim {
+  OCF_NO_PROLOGUE
   static constexpr int YS = GT_BN + 4;
   static constexpr int LDS_NEED = GT_BM * YS * 4;
   struct Params {
@@ -193,7 +204,7 @@ struct EpiOptim {
     int64_t ld;
     OcfOptParams op;
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     float* Y = reinterpret_cast<float*>(c.lds);
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
@@ -236,6 +247,7 @@ struct EpiOptim {
 
 // ---- predict: y = mask * (acc + b) (model.py:82-86) -------------------------------------
 struct EpiPredict {
+  OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
     const float* bias;
@@ -245,7 +257,7 @@ struct EpiPredict {
     int64_t ld_out;
     int m_real, n_real;
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&) {
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
     for_each_acc(acc, c, [&](int m, int n, float v) {
       if (m < p.m_real && n < p.n_real) {
         float y = v + p.bias[n];
@@ -266,7 +278,8 @@ struct EpiPredict {
 // / per-row SSE feed the loss and the train.py metrics.
 struct EpiMaskedMSE {
   static constexpr int YS = GT_BN + 4;   // LDS row stride (floats) of the staged tile
-  static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 4 * GT_THREADS * 4;
+  static constexpr int NPRE = 2;         // bucket entries per thread loaded in the prologue
+  static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 2 * GT_BN * 4 + 3 * 4 * 4;
   struct Params {
     const float* bias;        // output bias [N]
     const int* bk_ptr;        // [n_tiles+1]
@@ -282,52 +295,77 @@ struct EpiMaskedMSE {
     float* stats_part;        // [n_tiles * gm][4]: sse, sae, nnz(T+yhat), unused
     float* row_sse_part;      // [n_tiles][M] (nullable)
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape& sh) {
+  struct Pre {
+    int b0, b1;
+    int rc[NPRE];
+    float t[NPRE], m[NPRE];
+  };
+  __device__ static Pre prologue(const Params& p, int, int tile_n, int, int, int tid, const GemmShape&) {
+    Pre q;
+    q.b0 = p.bk_ptr[tile_n];
+    q.b1 = p.bk_ptr[tile_n + 1];
+#pragma unroll
+    for (int k = 0; k < NPRE; ++k) {
+      int e = q.b0 + tid + k * GT_THREADS;
+      bool ok = e < q.b1;
+      q.rc[k] = ok ? p.bk_rc[e] : -1;
+      q.t[k] = ok ? p.bk_t[e] : 0.f;
+      q.m[k] = ok ? p.bk_m[e] : 0.f;
+    }
+    return q;
+  }
+  __device__ static void entry(float* Y, uint32_t* bits, float* rsse, int m0, int rc, float t, float m, float& sse,
+                               float& sae, float& cnt) {
+    int row = rc >> 7, nl = rc & 127;
+    int ml = row - m0;
+    if (rc < 0 || ml < 0 || ml >= GT_BM) return;
+    float yhat = m * Y[ml * YS + nl];
+    float err = yhat - t;
+    Y[ml * YS + nl] = err * m;
+    atomicOr(&bits[ml * 4 + (nl >> 5)], 1u << (nl & 31));
+    sse += err * err;
+    sae += fabsf(err);
+    cnt += (t + yhat != 0.f) ? 1.f : 0.f;
+    atomicAdd(&rsse[ml], err * err);
+  }
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape& sh,
+                               const Pre& q) {
     float* Y = reinterpret_cast<float*>(c.lds);
     uint32_t* bits = reinterpret_cast<uint32_t*>(c.lds + GT_BM * YS * 4);
     float* rsse = reinterpret_cast<float*>(c.lds + GT_BM * YS * 4 + GT_BM * 16);
-    float* red = rsse + GT_BM;
+    float* colp = rsse + GT_BM;          // [2][GT_BN]
+    float* red = colp + 2 * GT_BN;       // [3][4]
     // 1. stage y = acc + b
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+    for (int bj = 0; bj < 2; ++bj) {
+      const float bias = p.bias[c.n0 + c.wn + acc_col(bj, c.lane)];
 #pragma unroll
-      for (int bj = 0; bj < 2; ++bj)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          int ml = c.wm + acc_row(bi, r, c.lane);
-          int nl = c.wn + acc_col(bj, c.lane);
-          Y[ml * YS + nl] = acc[bi][bj][r] + p.bias[c.n0 + nl];
-        }
+        for (int r = 0; r < 16; ++r)
+          Y[(c.wm + acc_row(bi, r, c.lane)) * YS + c.wn + acc_col(bj, c.lane)] = acc[bi][bj][r] + bias;
+    }
     for (int i = c.tid; i < GT_BM * 4; i += GT_THREADS) bits[i] = 0u;
     if (c.tid < GT_BM) rsse[c.tid] = 0.f;
     __syncthreads();
-    // 2. target entries of this column tile falling in this row tile
+    // 2. target entries of this column tile falling in this row tile (first NPRE per thread prefetched)
     float sse = 0.f, sae = 0.f, cnt = 0.f;
-    const int b0 = p.bk_ptr[c.tile_n], b1 = p.bk_ptr[c.tile_n + 1];
-    for (int e = b0 + c.tid; e < b1; e += GT_THREADS) {
-      int rc = p.bk_rc[e];
-      int row = rc >> 7, nl = rc & 127;
-      int ml = row - c.m0;
-      if (ml < 0 || ml >= GT_BM) continue;
-      float m = p.bk_m[e], t = p.bk_t[e];
-      float yhat = m * Y[ml * YS + nl];
-      float err = yhat - t;
-      Y[ml * YS + nl] = err * m;
-      atomicOr(&bits[ml * 4 + (nl >> 5)], 1u << (nl & 31));
-      sse += err * err;
-      sae += fabsf(err);
-      cnt += (t + yhat != 0.f) ? 1.f : 0.f;
-      atomicAdd(&rsse[ml], err * err);
-    }
+#pragma unroll
+    for (int k = 0; k < NPRE; ++k) entry(Y, bits, rsse, c.m0, q.rc[k], q.t[k], q.m[k], sse, sae, cnt);
+    for (int e = q.b0 + c.tid + NPRE * GT_THREADS; e < q.b1; e += GT_THREADS)
+      entry(Y, bits, rsse, c.m0, p.bk_rc[e], p.bk_t[e], p.bk_m[e], sse, sae, cnt);
     __syncthreads();
     // 3. dense delta tile (zeros where no target) -> compute dtype, 8 columns per chunk
     if (p.d_out) {
+#pragma unroll 2
       for (int ch = c.tid; ch < GT_BM * (GT_BN / 8); ch += GT_THREADS) {
         int ml = ch / (GT_BN / 8), c8 = (ch % (GT_BN / 8)) * 8;
         uint32_t w = bits[ml * 4 + (c8 >> 5)] >> (c8 & 31);
-        float v[8];
+        const float4 y0 = *reinterpret_cast<const float4*>(Y + ml * YS + c8);
+        const float4 y1 = *reinterpret_cast<const float4*>(Y + ml * YS + c8 + 4);
+        float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ((w >> j) & 1u) ? Y[ml * YS + c8 + j] : 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = ((w >> j) & 1u) ? v[j] : 0.f;
         int64_t off = (int64_t)(c.m0 + ml) * p.ld_d + c.n0 + c8;
         if (p.d_dtype == OCF_F32) {
           float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.d_out) + off);
@@ -348,33 +386,36 @@ struct EpiMaskedMSE {
         }
       }
     }
-    // 4. output-bias gradient column partials (fixed order over rows)
-    if (p.db_part && c.tid < GT_BN) {
-      float s = 0.f;
-      const int nl = c.tid;
-      for (int ml = 0; ml < GT_BM; ++ml)
-        if ((bits[ml * 4 + (nl >> 5)] >> (nl & 31)) & 1u) s += Y[ml * YS + nl];
-      p.db_part[(int64_t)c.tile_m * p.ld_db + c.n0 + nl] = s * p.gscale;
-    }
-    // 5. loss / metric partials
-    red[c.tid] = sse;
-    red[GT_THREADS + c.tid] = sae;
-    red[2 * GT_THREADS + c.tid] = cnt;
-    __syncthreads();
-    for (int s = GT_THREADS / 2; s > 0; s >>= 1) {
-      if (c.tid < s) {
-        red[c.tid] += red[c.tid + s];
-        red[GT_THREADS + c.tid] += red[GT_THREADS + c.tid + s];
-        red[2 * GT_THREADS + c.tid] += red[2 * GT_THREADS + c.tid + s];
+    // 4. output-bias gradient column partials: 2 threads per column, 64 rows each, fixed order
+    if (p.db_part) {
+      const int nl = c.tid & (GT_BN - 1), half = c.tid >> 7;
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll 8
+      for (int ml = half * 64; ml < half * 64 + 64; ml += 2) {
+        uint32_t w0 = bits[ml * 4 + (nl >> 5)], w1 = bits[(ml + 1) * 4 + (nl >> 5)];
+        s0 += ((w0 >> (nl & 31)) & 1u) ? Y[ml * YS + nl] : 0.f;
+        s1 += ((w1 >> (nl & 31)) & 1u) ? Y[(ml + 1) * YS + nl] : 0.f;
       }
-      __syncthreads();
+      colp[half * GT_BN + nl] = s0 + s1;
     }
+    // 5. loss / metric partials: wave butterflies, then 4 wave partials in fixed order
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      sse += __shfl_xor(sse, off);
+      sae += __shfl_xor(sae, off);
+      cnt += __shfl_xor(cnt, off);
+    }
+    const int wave = c.tid >> 6;
+    if (c.lane == 0) { red[wave] = sse; red[4 + wave] = sae; red[8 + wave] = cnt; }
+    __syncthreads();
+    if (p.db_part && c.tid < GT_BN)
+      p.db_part[(int64_t)c.tile_m * p.ld_db + c.n0 + c.tid] = (colp[c.tid] + colp[GT_BN + c.tid]) * p.gscale;
     const int gm = sh.M / GT_BM;
     if (c.tid == 0) {
       float* sp = p.stats_part + ((int64_t)c.tile_n * gm + c.tile_m) * 4;
-      sp[0] = red[0];
-      sp[1] = red[GT_THREADS];
-      sp[2] = red[2 * GT_THREADS];
+      sp[0] = (red[0] + red[1]) + (red[2] + red[3]);
+      sp[1] = (red[4] + red[5]) + (red[6] + red[7]);
+      sp[2] = (red[8] + red[9]) + (red[10] + red[11]);
       sp[3] = 0.f;
     }
     if (p.row_sse_part && c.tid < GT_BM)

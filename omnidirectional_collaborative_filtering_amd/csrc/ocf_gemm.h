@@ -227,6 +227,9 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   Stager<AGT, CT, GT_BM, ACOL> sa;
   Stager<BGT, CT, GT_BN, BCOL> sb;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  // epilogue inputs that do not depend on the product (e.g. target buckets) are loaded here, so
+  // their latency hides under the K-loop
+  const typename Epi::Pre pre = Epi::prologue(ep, tile_m, tile_n, m0, n0, tid, sh);
 
   ocf_f16v acc[2][2];
 #pragma unroll
@@ -294,7 +297,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   TileCtx c;
   c.m0 = m0; c.n0 = n0; c.wm = wm; c.wn = wn; c.lane = lane; c.tid = tid;
   c.split = split; c.tile_m = tile_m; c.tile_n = tile_n; c.lds = lds;
-  Epi::apply(ep, acc, c, sh);
+  Epi::apply(ep, acc, c, sh, pre);
 }
 
 }  // namespace ocf

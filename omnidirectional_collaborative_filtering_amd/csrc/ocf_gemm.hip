@@ -69,6 +69,18 @@ void dispatch(const OcfGemmArgs& g, hipStream_t s) {
         EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
         launch<CT, false, false, float, EpiSlab>(g, p, s);
       } break;
+      case OCF_EPI_PREDICT: {
+        EpiPredict::Params p{g.bias, g.pmask, g.ld_pmask, g.out, g.ld_out, g.m_real, g.n_real};
+        launch<CT, false, false, float, EpiPredict>(g, p, s);
+      } break;
+      case OCF_EPI_MASKED_MSE: {
+        EpiMaskedMSE::Params p;
+        p.bias = g.bias; p.bk_ptr = g.bk_ptr; p.bk_rc = g.bk_rc; p.bk_t = g.bk_t; p.bk_m = g.bk_m;
+        p.d_out = g.h_out; p.d_dtype = g.h_dtype; p.ld_d = g.ld_out; p.db_part = g.db_part; p.ld_db = g.ld_db;
+        p.gscale = g.opt.gscale; p.stats_part = g.stats_part; p.row_sse_part = g.row_sse_part;
+        OCF_CHECK(g.stats_part && g.bk_ptr, "ocf_gemm MASKED_MSE: stats_part / buckets required");
+        launch<CT, false, false, float, EpiMaskedMSE>(g, p, s);
+      } break;
       case OCF_EPI_GRAD_ACT: {
         GradActParams p;
         p.a = g.a_in; p.mask = g.mask_in; p.keep = g.keep; p.act = g.act; p.d_out = g.h_out; p.d_dtype = g.h_dtype;

@@ -1,6 +1,6 @@
 // K1: sparse-rating -> dense-batch assembly (replaces data_reader.py:95-298).
 //
-// One workgroup per batch row.  The dataset lives in HBM as row-CSR in the reference's list
+// Grid (B, 4): four workgroups per batch row.  The dataset lives in HBM as row-CSR in the reference's list
 // order (row_ptr int64, col int32 = dense column index, val f32) plus an optional duplicate
 // chain dup[e] = next entry of the same row with the same column (or -1), so that the
 // reference's last-write-wins per array (data_reader.py:158-166, 250-266) is reproduced by a
@@ -18,13 +18,6 @@
 #include "ocf_internal.h"
 
 namespace ocf {
-
-struct EntryCtx {
-  const ScatterArgs* a;
-  int b;          // batch row
-  int64_t rs1;    // CSR row start in source 1 (or -1)
-  int64_t bo1;    // batch-local offset of this row's first source-1 entry
-};
 
 __device__ __forceinline__ float reciprocal_cut(float s) { return (1.0f - s) / ((1.0f - s) + s); }
 
@@ -54,36 +47,24 @@ __device__ __forceinline__ void store_val(void* base, int dtype, int64_t idx, fl
   else reinterpret_cast<__bf16*>(base)[idx] = (__bf16)v;
 }
 
-__device__ __forceinline__ void zero_row(void* base, int esize, int64_t ld, int b, int tid) {
-  if (!base) return;
-  char* row = reinterpret_cast<char*>(base) + (int64_t)b * ld * esize;
-  int64_t bytes = ld * esize;             // callers guarantee 16-B multiple rows
-  uint4 z = make_uint4(0, 0, 0, 0);
-  for (int64_t o = (int64_t)tid * 16; o < bytes; o += (int64_t)blockDim.x * 16)
-    *reinterpret_cast<uint4*>(row + o) = z;
-}
+// grid (B, SPLIT): workgroup (b, s) handles entries s*256 + tid, step SPLIT*256, of batch row b.
+// The outputs were zeroed by hipMemsetAsync on the same stream before this launch.
+constexpr int SCATTER_SPLIT = 4;
 
 __global__ void __launch_bounds__(256) scatter_rows_kernel(ScatterArgs a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  // 1. zero this row of every requested output
-  zero_row(a.X, 4, a.ld, b, tid);
-  zero_row(a.Min, 4, a.ld, b, tid);
-  zero_row(a.Mout, 4, a.ld, b, tid);
-  zero_row(a.T, 4, a.ld, b, tid);
-  zero_row(a.Mmiss, 4, a.ld, b, tid);
-  zero_row(a.xin, a.xin_dtype == OCF_F32 ? 4 : 2, a.xin_ld, b, tid);
-  __syncthreads();   // s_waitcnt vmcnt(0) + s_barrier: zero stores complete before scatter stores
-  if (b >= a.B) return;
+  const int b = blockIdx.x;
+  const int tid = blockIdx.y * blockDim.x + threadIdx.x;
+  const int nthr = gridDim.y * blockDim.x;
   const float aux = a.aux;
   const int64_t xb = a.xin_block;
 
-  // 2. source 1
+  // source 1
   int r1 = a.rows1 ? a.rows1[b] : -1;
   if (r1 >= 0) {
     const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
     const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
     const float cut = row_cut(a, b);
-    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+    for (int64_t i = s + tid; i < e; i += nthr) {
       const int c = a.col1[i];
       const float v = a.val1[i];
       const int role = role1(a, b, i - s, bo1, cut);
@@ -118,11 +99,11 @@ __global__ void __launch_bounds__(256) scatter_rows_kernel(ScatterArgs a) {
       }
     }
   }
-  // 3. source 2 (eval targets)
+  // source 2 (eval targets)
   int r2 = a.rows2 ? a.rows2[b] : -1;
   if (r2 >= 0) {
     const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
-    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+    for (int64_t i = s + tid; i < e; i += nthr) {
       const int c = a.col2[i];
       const float v = a.val2[i];
       const bool dead = a.dup2 && a.dup2[i] >= 0;   // every source-2 entry is a target
@@ -169,14 +150,15 @@ __global__ void __launch_bounds__(1024) bucket_scan_kernel(int* tile_cnt, int* b
 }
 
 __global__ void __launch_bounds__(256) bucket_fill_kernel(ScatterArgs a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  if (b >= a.B) return;
+  const int b = blockIdx.x;
+  const int tid = blockIdx.y * blockDim.x + threadIdx.x;
+  const int nthr = gridDim.y * blockDim.x;
   int r1 = a.rows1 ? a.rows1[b] : -1;
   if (r1 >= 0 && a.mode == 0) {
     const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
     const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
     const float cut = row_cut(a, b);
-    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+    for (int64_t i = s + tid; i < e; i += nthr) {
       const int role = role1(a, b, i - s, bo1, cut);
       if (!(role & 2)) continue;
       bool later_tg = false;
@@ -193,7 +175,7 @@ __global__ void __launch_bounds__(256) bucket_fill_kernel(ScatterArgs a) {
   int r2 = a.rows2 ? a.rows2[b] : -1;
   if (r2 >= 0) {
     const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
-    for (int64_t i = s + tid; i < e; i += blockDim.x) {
+    for (int64_t i = s + tid; i < e; i += nthr) {
       if (a.dup2 && a.dup2[i] >= 0) continue;
       const int c = a.col2[i];
       int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
@@ -261,12 +243,17 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   if (a.tile_cnt) OCF_CHECK(a.bk_ptr && a.bk_cur && a.bk_rc && a.bk_t && a.bk_m && a.n_tiles > 0,
                             "ocf_scatter_batch: bucket outputs incomplete");
   if (a.B_pad == 0) return 0;
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3(a.B_pad), dim3(256), 0, s, a);
+  // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks)
+  float* dense[5] = {a.X, a.Min, a.Mout, a.T, a.Mmiss};
+  for (float* d : dense)
+    if (d) OCF_HIP(hipMemsetAsync(d, 0, (size_t)a.B_pad * a.ld * 4, s));
+  if (a.xin) OCF_HIP(hipMemsetAsync(a.xin, 0, (size_t)a.B_pad * a.xin_ld * (a.xin_dtype == OCF_F32 ? 4 : 2), s));
+  if (a.B > 0) hipLaunchKernelGGL(scatter_rows_kernel, dim3(a.B, SCATTER_SPLIT), dim3(256), 0, s, a);
   OCF_HIP(hipGetLastError());
   if (a.tile_cnt) {
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, a.tile_cnt, a.bk_ptr, a.bk_cur, a.n_tiles);
     OCF_HIP(hipGetLastError());
-    if (a.B > 0) hipLaunchKernelGGL(bucket_fill_kernel, dim3(a.B), dim3(256), 0, s, a);
+    if (a.B > 0) hipLaunchKernelGGL(bucket_fill_kernel, dim3(a.B, SCATTER_SPLIT), dim3(256), 0, s, a);
     OCF_HIP(hipGetLastError());
   }
   OCF_TRY_END

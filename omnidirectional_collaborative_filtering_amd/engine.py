@@ -10,8 +10,11 @@ Padded HBM layout (DESIGN.md "Data layout"):
   * output width     N  -> Np = roundup(N, 128); layer-0 input = k blocks of Np (concat order of
                             model.py:47-56: data | observed mask | second mask)
   * hidden widths    H  -> Hp = roundup(H, 128)
-  * W_i  fp32 [in_p][out_p] (Keras (in, out) layout), b_i fp32 [out_p]; pads are zero and stay
-    zero (their gradients are exactly zero, the optimizers map g = 0, state = 0 to no change)
+  * W_i  fp32 [in_p][out_p] (Keras (in, out) layout) for the encoder and hidden layers; the
+    decoder W_L is stored transposed, [Np][H_p] (one row per output user), so that every weight
+    stream of the step (encoder/decoder forward, decoder backward, both fused optimizers) reads
+    whole 2-KB rows instead of 512-B column pieces 555 KB apart; b_i fp32 [out_p].  Pads are zero
+    and stay zero (their gradients are exactly zero; the optimizers map g = 0, state = 0 to no change)
 Per step the loss gradient is carried unscaled (err * mask) in the compute dtype and the
 constant 2/(B*N) of Keras' MSE is folded into the weight/bias-gradient epilogues (gscale), which
 keeps f16 operands far from underflow.
@@ -88,8 +91,13 @@ class Engine:
     # ---------------------------------------------------------------- parameters
     def _alloc_params(self):
         f = dict(device=self.dev, dtype=torch.float32)
-        self.W = [torch.zeros(i, o, **f) for i, o in zip(self.pad_dims[:-1], self.pad_dims[1:])]
+        self.W = [torch.zeros(i, o, **f) for i, o in zip(self.pad_dims[:-2], self.pad_dims[1:-1])]
+        self.W.append(torch.zeros(self.pad_dims[-1], self.pad_dims[-2], **f))     # decoder, transposed
         self.b = [torch.zeros(o, **f) for o in self.pad_dims[1:]]
+
+    def _keras_view(self, i):
+        """W_i as a padded (in, out) view (the decoder is stored transposed)."""
+        return self.W[i].t() if i == len(self.W) - 1 else self.W[i]
 
     def _row_map(self, layer):
         """padded row index of each real input row of layer `layer`."""
@@ -106,8 +114,9 @@ class Engine:
     def get_weights(self):
         """Keras-layout numpy list [W0, b0, W1, b1, ...] (padding stripped)."""
         out = []
-        for i, (w, b) in enumerate(zip(self.W, self.b)):
+        for i, b in enumerate(self.b):
             rows = torch.as_tensor(self._row_map(i), device=self.dev)
+            w = self._keras_view(i)
             out.append(w.index_select(0, rows)[:, : self.real_dims[i + 1]].cpu().numpy())
             out.append(b[: self.real_dims[i + 1]].cpu().numpy())
         return out
@@ -121,7 +130,10 @@ class Engine:
                                                                          (self.real_dims[i], self.real_dims[i + 1])))
             self.W[i].zero_()
             rows = torch.as_tensor(self._row_map(i), device=self.dev)
-            self.W[i][:, : self.real_dims[i + 1]].index_copy_(0, rows, w)
+            kv = self._keras_view(i)
+            full = torch.zeros(kv.shape, device=self.dev, dtype=torch.float32)
+            full[:, : self.real_dims[i + 1]].index_copy_(0, rows, w)
+            kv.copy_(full)
             self.b[i].zero_()
             self.b[i][: self.real_dims[i + 1]] = bb
 
@@ -332,7 +344,7 @@ class Engine:
         self.n_stats += 1
 
     def _gemm_mse(self, L, gscale, with_grad):
-        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 1, self.Np, self.Bp, self.Np,
+        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 0, self.Hp[L - 1], self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], bk_ptr=self.bk_ptr,
                    bk_rc=self.bk_rc, bk_t=self.bk_t, bk_m=self.bk_m,
                    h_out=self.d_out if with_grad else None, h_dtype=self.cdt, ld_out=self.Np,
@@ -343,7 +355,7 @@ class Engine:
     def predict_dense(self, out_mask, out):
         """PREDICT epilogue: out[B][N] = out_mask * (h W + b)."""
         L = len(self.H)
-        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 1, self.Np, self.Bp, self.Np,
+        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 0, self.Hp[L - 1], self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_PREDICT, bias=self.b[L], pmask=out_mask,
                    ld_pmask=out_mask.stride(0) if out_mask is not None else 0, out=out, ld_out=out.stride(0),
                    m_real=self.B, n_real=self.N)
@@ -363,7 +375,7 @@ class Engine:
         HpL = self.Hp[L - 1]
         sstride = Bp * HpL
         with self.phase("dec_bwd_gemm"):
-            self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 0, self.Np, Bp, HpL, self.Np, _lib.EPI_SLAB,
+            self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
         db_last = self.db_h[L - 1]
         call("ocf_splitk_grad_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.a[L - 1]),
@@ -372,7 +384,7 @@ class Engine:
         # output layer bias + weights
         self._bias_update(L, self.db_out_part, Bp // TILE, self.Np, self.Np, grads_out, op)
         with self.phase("dW_out"):
-            self._weight_update(L, self.h[L - 1], HpL, self.d_out, self.Np, HpL, self.Np, gscale, grads_out, op)
+            self._weight_update(L, self.d_out, self.Np, self.h[L - 1], HpL, self.Np, HpL, gscale, grads_out, op)
         parts_last = Bp // 4
         for i in range(L - 1, 0, -1):
             # delta of hidden layer i-1 through W_i (before W_i changes)
