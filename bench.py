@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--phase-timers", type=int, default=1)
     ap.add_argument("--rmse", type=int, default=1)
+    ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
+                    help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
+                         "(replicated weights, gradient all-reduce)")
     return ap.parse_args()
 
 
@@ -88,7 +91,8 @@ def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps):
 
 def main():
     args = parse()
-    from omnidirectional_collaborative_filtering_amd.parallel import (GradBucket, dp_train_step, init_from_env,
+    from omnidirectional_collaborative_filtering_amd.parallel import (GradBucket, dp_train_step,
+                                                                      feature_shard_range, init_from_env, make_comm,
                                                                       shard_batches)
     rank, world, local = init_from_env()
     if world != args.gpus:
@@ -100,30 +104,42 @@ def main():
     from omnidirectional_collaborative_filtering_amd.model import omni_model
 
     t0 = time.time()
-    data = synthetic_fixed_split(args.config, seed=0)
-    N = data.num_cols
-    n_rows = data.train.n_rows
-    np.random.seed(1234)
-    rd = data_reader(N, n_rows, dataset=data, eval_mode="fixed_split", rng="device", device=dev)
+    data_full = synthetic_fixed_split(args.config, seed=0)
+    N = data_full.num_cols
+    n_rows = data_full.train.n_rows
+    fp = world > 1 and args.parallel == "feature"
     B, H = args.batch, args.hidden
-    om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False,
-                    dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev)
+    if fp:
+        # weak scaling: 256 rows per GPU -> global batch 256*G, each rank owns N/G users
+        c0, c1 = feature_shard_range(N, rank, world)
+        data = data_full.column_shard(c0, c1)
+        Bg, shard, comm = B * world, (c0, c1, N), make_comm(world)
+    else:
+        data, Bg, shard, comm = data_full, B, None, None
+    np.random.seed(1234)
+    rd = data_reader(data.num_cols, n_rows, dataset=data, eval_mode="fixed_split", rng="device", device=dev)
+    om = omni_model(1, H, data.num_cols, Bg, dense_activation="sigmoid", use_causal_info=False,
+                    dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev,
+                    shard=shard, comm=comm)
     m = om.model
     lr = 0.005 if args.optimizer == "adagrad" else 0.001
     m.compile(optim(args.optimizer, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
     w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
     eng = om.engine
-    gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
-    batches = shard_batches(gen.num_batches, rank, world)
-    bucket = GradBucket(eng) if world > 1 else None
+    batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)
+    bucket = GradBucket(eng) if (world > 1 and not fp) else None
     nnz_of = gen.nnz1
     setup_s = time.time() - t0
 
     def step(i):
         bi = batches[i % len(batches)]
         m._load(None, gen, bi)
-        dp_train_step(eng, bucket, world)
+        if fp:
+            eng.train_step()
+        else:
+            dp_train_step(eng, bucket, world)
         return int(nnz_of[bi])
 
     for i in range(args.warmup):
@@ -155,8 +171,8 @@ def main():
     # masked RMSE on the test split (train.py:225-255, fused form)
     rmse = None
     if args.rmse:
-        tgen = rd.data_gen(B, None, "test", True, None, -1, return_target_count=True)
-        sse, cnt = m.evaluate_sse(tgen, rd.test_set_size // B)
+        tgen = rd.data_gen(Bg, None, "test", True, None, -1, return_target_count=True)
+        sse, cnt = m.evaluate_sse(tgen, rd.test_set_size // Bg)
         rmse = float(np.sqrt(sse / cnt)) if cnt else None
 
     if rank != 0:
@@ -164,24 +180,25 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    # roofline of the dominant kernel: fused weight-gradient GEMM + optimizer update
-    P = N * H
+    # roofline of the dominant kernel: fused weight-gradient GEMM + optimizer update (per rank)
+    Nl = data.num_cols
+    P = Nl * H
     opt_b = OPT_STATE_BYTES[args.optimizer]
     dom = None
     if phases:
         cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
         dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
     alg = {
-        # bytes per launch, algorithmic (real, unpadded sizes): optimizer state r/w + streamed operand
-        "dW_in": P * opt_b + B * N * 2 + B * H * 2,
-        "dW_out": P * opt_b + B * N * 2 + B * H * 2,
-        "enc_gemm": P * 4 + B * N * 2,
-        "dec_gemm_mse": P * 4 + B * H * 2 + B * N * 2,
-        "dec_bwd_gemm": P * 4 + B * N * 2,
+        # bytes per launch, algorithmic (real, unpadded sizes of this rank): optimizer state r/w + streamed operand
+        "dW_in": P * opt_b + Bg * Nl * 2 + Bg * H * 2,
+        "dW_out": P * opt_b + Bg * Nl * 2 + Bg * H * 2,
+        "enc_gemm": P * 4 + Bg * Nl * 2,
+        "dec_gemm_mse": P * 4 + Bg * H * 2 + Bg * Nl * 2,
+        "dec_bwd_gemm": P * 4 + Bg * Nl * 2,
     }
     roof = None
     if dom is not None:
-        if world > 1 and dom in ("dW_in", "dW_out"):
+        if world > 1 and not fp and dom in ("dW_in", "dW_out"):
             alg[dom] = P * 4 + B * N * 2 + B * H * 2     # gradient store instead of the fused update
         ms = phases[dom]["mean_ms"]
         ach = alg[dom] / (ms * 1e-3) / 1e9
@@ -195,8 +212,8 @@ def main():
             if tr:
                 roof["traffic"] = tr
     ms_step = elapsed / args.steps * 1e3
-    step_flops = 10.0 * B * N * H
-    step_bytes = P * 2 * (opt_b + 4) + 2 * (3 * N * H) + 8 * (nnz / args.steps / max(world, 1))
+    step_flops = 10.0 * Bg * Nl * H
+    step_bytes = P * 2 * (opt_b + 4) + 2 * (3 * Nl * H) + 8 * (nnz / args.steps / max(world, 1))
     line = {
         "metric": METRIC, "value": round(nnz / elapsed, 1), "unit": "ratings/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -206,7 +223,7 @@ def main():
         "config": {"workload": "ml20m I-AutoRec train step (BASELINE configs[2])", "rows": n_rows, "N": N,
                    "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
                    "activation": "sigmoid", "dropout": args.dropout, "compute": args.dtype + " MFMA, fp32 accumulate",
-                   "parallelism": "dp%d" % world},
+                   "parallelism": ("feature%d" % world) if fp else ("dp%d" % world)},
         "masked_rmse": rmse,
         "roofline": roof,
         "step_roofline": {"alg_bytes": int(step_bytes), "alg_flops": int(step_flops),

@@ -83,6 +83,10 @@ typedef struct OcfScatterArgs {
   /* target buckets (nullable) */
   int* tile_cnt; int* bk_ptr; int* bk_cur; int32_t* bk_rc; float* bk_t; float* bk_m;
   int n_tiles;
+  /* column-sharded source 1 (feature parallelism): pos1[e] = position of entry e within its FULL
+   * row, used to index keep1 / the device RNG so every shard sees the same reciprocal split
+   * (nullable: position = e - row start) */
+  const int32_t* pos1;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);

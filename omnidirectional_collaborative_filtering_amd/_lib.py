@@ -38,6 +38,7 @@ class OcfScatterArgs(ctypes.Structure):
         ("X", P), ("Min", P), ("Mout", P), ("T", P), ("Mmiss", P), ("ld", I64),
         ("xin", P), ("xin_dtype", I32), ("xin_ld", I64), ("xin_block", I64), ("feed", I32), ("both", I32),
         ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
+        ("pos1", P),
     ]
 
 

@@ -34,81 +34,84 @@ BiasActParams bias_act_params(const OcfGemmArgs& g) {
   return p;
 }
 
-template <typename CT>
-void dispatch(const OcfGemmArgs& g, hipStream_t s) {
-  const bool b_f32 = g.b_dtype == OCF_F32;
-  if (!g.a_col && g.b_col) {
-    OCF_CHECK(b_f32, "ocf_gemm: [M][K] x [K][N] requires fp32 B (master weights)");
-    switch (g.epi) {
-      case OCF_EPI_SLAB: {
-        EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
-        launch<CT, false, true, float, EpiSlab>(g, p, s);
-      } break;
-      case OCF_EPI_BIAS_ACT:
-        launch<CT, false, true, float, EpiBiasAct>(g, bias_act_params(g), s);
-        break;
-      case OCF_EPI_PREDICT: {
-        EpiPredict::Params p{g.bias, g.pmask, g.ld_pmask, g.out, g.ld_out, g.m_real, g.n_real};
-        launch<CT, false, true, float, EpiPredict>(g, p, s);
-      } break;
-      case OCF_EPI_MASKED_MSE: {
-        EpiMaskedMSE::Params p;
-        p.bias = g.bias; p.bk_ptr = g.bk_ptr; p.bk_rc = g.bk_rc; p.bk_t = g.bk_t; p.bk_m = g.bk_m;
-        p.d_out = g.h_out; p.d_dtype = g.h_dtype; p.ld_d = g.ld_out; p.db_part = g.db_part; p.ld_db = g.ld_db;
-        p.gscale = g.opt.gscale; p.stats_part = g.stats_part; p.row_sse_part = g.row_sse_part;
-        OCF_CHECK(g.stats_part && g.bk_ptr, "ocf_gemm MASKED_MSE: stats_part / buckets required");
-        launch<CT, false, true, float, EpiMaskedMSE>(g, p, s);
-      } break;
-      default:
-        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[M][K] x B[K][N]");
+template <typename CT, bool ACOL, bool BCOL>
+void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
+  // weights stream in as fp32 (converted while staging); activations arrive in the compute dtype
+  const bool weight_b = g.epi == OCF_EPI_SLAB || g.epi == OCF_EPI_BIAS_ACT || g.epi == OCF_EPI_PREDICT ||
+                        g.epi == OCF_EPI_MASKED_MSE || g.epi == OCF_EPI_GRAD_ACT;
+  if (weight_b)
+    OCF_CHECK(g.b_dtype == OCF_F32, "ocf_gemm: this epilogue takes fp32 B (master weights)");
+  else
+    OCF_CHECK(g.b_dtype == g.compute_dtype, "ocf_gemm: OPTIM/GRAD take B in the compute dtype");
+  constexpr bool A_ROW = !ACOL;
+  switch (g.epi) {
+    case OCF_EPI_SLAB: {
+      EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
+      launch<CT, ACOL, BCOL, float, EpiSlab>(g, p, s);
+      return;
     }
-  } else if (!g.a_col && !g.b_col) {
-    OCF_CHECK(b_f32, "ocf_gemm: [M][K] x [N][K] requires fp32 B (master weights)");
-    switch (g.epi) {
-      case OCF_EPI_SLAB: {
-        EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
-        launch<CT, false, false, float, EpiSlab>(g, p, s);
-      } break;
-      case OCF_EPI_PREDICT: {
+    case OCF_EPI_BIAS_ACT:
+      if constexpr (A_ROW && BCOL) {
+        launch<CT, ACOL, BCOL, float, EpiBiasAct>(g, bias_act_params(g), s);
+        return;
+      }
+      break;
+    case OCF_EPI_PREDICT:
+      if constexpr (A_ROW) {
         EpiPredict::Params p{g.bias, g.pmask, g.ld_pmask, g.out, g.ld_out, g.m_real, g.n_real};
-        launch<CT, false, false, float, EpiPredict>(g, p, s);
-      } break;
-      case OCF_EPI_MASKED_MSE: {
+        launch<CT, ACOL, BCOL, float, EpiPredict>(g, p, s);
+        return;
+      }
+      break;
+    case OCF_EPI_MASKED_MSE:
+      if constexpr (A_ROW) {
         EpiMaskedMSE::Params p;
         p.bias = g.bias; p.bk_ptr = g.bk_ptr; p.bk_rc = g.bk_rc; p.bk_t = g.bk_t; p.bk_m = g.bk_m;
         p.d_out = g.h_out; p.d_dtype = g.h_dtype; p.ld_d = g.ld_out; p.db_part = g.db_part; p.ld_db = g.ld_db;
         p.gscale = g.opt.gscale; p.stats_part = g.stats_part; p.row_sse_part = g.row_sse_part;
         OCF_CHECK(g.stats_part && g.bk_ptr, "ocf_gemm MASKED_MSE: stats_part / buckets required");
-        launch<CT, false, false, float, EpiMaskedMSE>(g, p, s);
-      } break;
-      case OCF_EPI_GRAD_ACT: {
+        launch<CT, ACOL, BCOL, float, EpiMaskedMSE>(g, p, s);
+        return;
+      }
+      break;
+    case OCF_EPI_GRAD_ACT:
+      if constexpr (A_ROW && !BCOL) {
         GradActParams p;
         p.a = g.a_in; p.mask = g.mask_in; p.keep = g.keep; p.act = g.act; p.d_out = g.h_out; p.d_dtype = g.h_dtype;
         p.ld = g.ld_out; p.db_part = g.db_part; p.gscale = g.opt.gscale; p.m_real = g.m_real; p.n_real = g.n_real;
         OCF_CHECK(g.a_in && g.h_out, "ocf_gemm GRAD_ACT: a_in / h_out required");
-        launch<CT, false, false, float, EpiGradAct>(g, p, s);
-      } break;
-      default:
-        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[M][K] x B[N][K]");
-    }
-  } else if (g.a_col && g.b_col) {
-    OCF_CHECK(g.b_dtype == g.compute_dtype, "ocf_gemm: [K][M] x [K][N] requires B in the compute dtype");
-    switch (g.epi) {
-      case OCF_EPI_OPTIM: {
+        launch<CT, ACOL, BCOL, float, EpiGradAct>(g, p, s);
+        return;
+      }
+      break;
+    case OCF_EPI_OPTIM:
+      if constexpr (BCOL) {
         EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt};
         OCF_CHECK(g.p != nullptr, "ocf_gemm OPTIM: p required");
-        launch<CT, true, true, CT, EpiOptim>(g, p, s);
-      } break;
-      case OCF_EPI_GRAD: {
+        launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
+        return;
+      }
+      break;
+    case OCF_EPI_GRAD:
+      if constexpr (BCOL) {
         EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale};
-        launch<CT, true, true, CT, EpiGradStore>(g, p, s);
-      } break;
-      default:
-        throw std::runtime_error("ocf_gemm: epilogue not available for layout A[K][M] x B[K][N]");
-    }
-  } else {
-    throw std::runtime_error("ocf_gemm: layout A[K][M] x B[N][K] not instantiated");
+        launch<CT, ACOL, BCOL, CT, EpiGradStore>(g, p, s);
+        return;
+      }
+      break;
+    default:
+      break;
   }
+  throw std::runtime_error("ocf_gemm: epilogue " + std::to_string(g.epi) + " not instantiated for layout a_col=" +
+                           std::to_string(ACOL) + " b_col=" + std::to_string(BCOL));
+}
+
+template <typename CT>
+void dispatch(const OcfGemmArgs& g, hipStream_t s) {
+  if (!g.a_col && g.b_col) dispatch_layout<CT, false, true>(g, s);
+  else if (!g.a_col && !g.b_col) dispatch_layout<CT, false, false>(g, s);
+  else if (g.a_col && g.b_col) dispatch_layout<CT, true, true>(g, s);
+  else throw std::runtime_error("ocf_gemm: layout A[K][M] x B[N][K] not instantiated");
 }
 
 }  // namespace

@@ -67,12 +67,12 @@ __global__ void __launch_bounds__(256) scatter_rows_kernel(ScatterArgs a) {
     for (int64_t i = s + tid; i < e; i += nthr) {
       const int c = a.col1[i];
       const float v = a.val1[i];
-      const int role = role1(a, b, i - s, bo1, cut);
+      const int role = role1(a, b, a.pos1 ? a.pos1[i] : i - s, bo1, cut);
       // later duplicates of the same column that also write the value arrays
       bool later_in = false, later_tg = false;
       if (a.dup1) {
         for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) {
-          int rf = role1(a, b, f - s, bo1, cut);
+          int rf = role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut);
           later_in |= (rf & 1) != 0;
           later_tg |= (rf & 2) != 0;
         }
@@ -159,11 +159,12 @@ __global__ void __launch_bounds__(256) bucket_fill_kernel(ScatterArgs a) {
     const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
     const float cut = row_cut(a, b);
     for (int64_t i = s + tid; i < e; i += nthr) {
-      const int role = role1(a, b, i - s, bo1, cut);
+      const int role = role1(a, b, a.pos1 ? a.pos1[i] : i - s, bo1, cut);
       if (!(role & 2)) continue;
       bool later_tg = false;
       if (a.dup1)
-        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) later_tg |= (role1(a, b, f - s, bo1, cut) & 2) != 0;
+        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f])
+          later_tg |= (role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut) & 2) != 0;
       if (later_tg) continue;
       const int c = a.col1[i];
       int slot = atomicAdd(&a.bk_cur[c >> 7], 1);

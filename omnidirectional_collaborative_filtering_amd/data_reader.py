@@ -35,7 +35,9 @@ class _DeviceCSR:
         self.col = torch.as_tensor(csr.col, device=dev)
         self.val = torch.as_tensor(csr.val, device=dev)
         self.dup = None if csr.dup is None else torch.as_tensor(csr.dup, device=dev)
-        self.lens = csr.row_lengths()
+        self.pos = None if csr.pos is None else torch.as_tensor(csr.pos, device=dev)
+        self.lens = csr.row_lengths()          # entries held here (a column shard holds fewer)
+        self.rng_lens = csr.rng_lengths()      # entries of the full rows (RNG draws, batch offsets)
 
 
 class data_reader(object):
@@ -157,19 +159,23 @@ class BatchGenerator(object):
             self.src1, self.src2 = dev["valid_in"], dev["valid_tgt"]
         else:
             self.src1, self.src2 = dev["test_in"], dev["test_tgt"]
-        rows, boff, self.tcount, keep = self.plan(self.src1.lens, None if self.src2 is None else self.src2.lens)
+        rows, boff, self.tcount, keep = self.plan(self.src1.rng_lens,
+                                                  None if self.src2 is None else self.src2.rng_lens)
         nb = self.num_batches
         self.rows_host = rows
-        self.nnz1 = boff[:, -1].copy()
+        self.nnz_full = boff[:, -1].copy()
+        self.nnz1 = self.src1.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)   # entries held here
+        if self.src2 is not None:
+            self.tlocal = self.src2.lens[rows].sum(axis=1)
         self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
         self.boff_dev = torch.as_tensor(boff, device=r.device)
         self.keep_dev = None
         self.keep_off = None
         if keep is not None:
             self.keep_dev = torch.as_tensor(keep.astype(np.uint8), device=r.device)
-            self.keep_off = np.concatenate([[0], np.cumsum(self.nnz1)])
+            self.keep_off = np.concatenate([[0], np.cumsum(self.nnz_full)])
         self.max_targets = int(max(self.nnz1.max() if nb else 0,
-                                   self.tcount.max() if (self.tcount is not None and nb) else 0))
+                                   self.tlocal.max() if (self.src2 is not None and nb) else 0))
 
     def scatter_args(self, bi, engine_args=None, dense=None, B_pad=None):
         """OcfScatterArgs for batch bi (onto an engine's xin/buckets and/or dense outputs)."""
@@ -177,6 +183,7 @@ class BatchGenerator(object):
         B = self.B
         s1 = self.src1
         a.rp1, a.col1, a.val1, a.dup1 = ptr(s1.rp), ptr(s1.col), ptr(s1.val), ptr(s1.dup)
+        a.pos1 = ptr(s1.pos)
         a.rows1 = self.rows_dev.data_ptr() + 4 * bi * B
         a.boff1 = self.boff_dev.data_ptr() + 8 * bi * (B + 1)
         a.keep1 = None if self.keep_dev is None else self.keep_dev.data_ptr() + int(self.keep_off[bi])
@@ -214,6 +221,8 @@ class BatchGenerator(object):
         return bi
 
     def target_count(self, bi):
+        """target_count of batch bi (data_reader.py:268): list entries of the target rows (full rows;
+        under feature parallelism every rank reports the global count)"""
         return int(self.tcount[bi]) if self.tcount is not None else None
 
     # ------------------------------------------------------------ reference-compatible iteration

@@ -51,6 +51,10 @@ class RatingsCSR:
     val: np.ndarray
     keys: List = field(default_factory=list)
     dup: Optional[np.ndarray] = None
+    # column shards (feature parallelism): position of each entry within its full row, and the
+    # full rows' lengths (the NumPy reciprocal draws are taken per full row)
+    pos: Optional[np.ndarray] = None
+    full_lens: Optional[np.ndarray] = None
 
     @property
     def n_rows(self):
@@ -62,6 +66,27 @@ class RatingsCSR:
 
     def row_lengths(self):
         return np.diff(self.row_ptr)
+
+    def rng_lengths(self):
+        """entries per row as the reference's RNG sees them (full rows, also for a column shard)"""
+        return self.full_lens if self.full_lens is not None else self.row_lengths()
+
+    def column_shard(self, c0, c1):
+        """entries with c0 <= col < c1, columns re-based to 0, list order and full-row positions kept"""
+        lens = self.row_lengths()
+        rows = np.repeat(np.arange(self.n_rows), lens)
+        pos = np.arange(self.nnz, dtype=np.int64) - np.repeat(self.row_ptr[:-1], lens)
+        if self.pos is not None:
+            pos = self.pos.astype(np.int64)
+        keep = (self.col >= c0) & (self.col < c1)
+        counts = np.bincount(rows[keep], minlength=self.n_rows)
+        rp = np.zeros(self.n_rows + 1, dtype=np.int64)
+        np.cumsum(counts, out=rp[1:])
+        c = RatingsCSR(rp, (self.col[keep] - c0).astype(np.int32), self.val[keep], list(self.keys))
+        c.dup = dup_chain(rp, c.col)
+        c.pos = pos[keep].astype(np.int32)
+        c.full_lens = self.rng_lengths()
+        return c
 
     @classmethod
     def from_lists(cls, keys, lists, col_index):
@@ -127,6 +152,12 @@ class FixedSplit:
     test_in: RatingsCSR
     test_tgt: RatingsCSR
     col_ids: List = field(default_factory=list)
+
+    def column_shard(self, c0, c1):
+        """the same split restricted to columns [c0, c1) (feature-parallel rank's slice)"""
+        return FixedSplit(c1 - c0, *(getattr(self, k).column_shard(c0, c1)
+                                     for k in ("train", "valid_in", "valid_tgt", "test_in", "test_tgt")),
+                          col_ids=list(self.col_ids[c0:c1]))
 
     def save(self, path):
         arrs = {"num_cols": np.array(self.num_cols)}

@@ -55,7 +55,9 @@ def glorot_uniform(rng, fan_in, fan_out):
 
 class Engine:
     def __init__(self, N, hidden, batch_size, k_blocks=1, activation="tanh", dropout=None, l2=None,
-                 compute_dtype="float32", device=None, seed=None):
+                 compute_dtype="float32", device=None, seed=None, shard=None, comm=None):
+        """shard = (c0, c1, N_total): this engine holds output columns [c0, c1) of an N_total-wide
+        model (feature parallelism, parallel.py); comm(tensor) sums a device tensor over the ranks."""
         if not torch.cuda.is_available():
             raise RuntimeError("omnidirectional_collaborative_filtering_amd needs a ROCm GPU (MI355X); none visible")
         _lib.load()
@@ -66,6 +68,9 @@ class Engine:
         self.cdt, self.tdt = DTYPES[cd]
         self.dev = torch.device(device if device is not None else "cuda")
         self.N = int(N)
+        self.shard = shard
+        self.N_total = int(shard[2]) if shard else self.N
+        self.comm = comm
         self.Np = ru(N, TILE)
         self.k = int(k_blocks)
         self.H = [int(h) for h in hidden]
@@ -107,8 +112,18 @@ class Engine:
         return np.arange(self.real_dims[layer])
 
     def init_weights(self, rng):
-        """Keras glorot_uniform kernels, zero biases (fan in/out of the real, unpadded layer)."""
-        ws = [glorot_uniform(rng, i, o) for i, o in zip(self.real_dims[:-1], self.real_dims[1:])]
+        """Keras glorot_uniform kernels, zero biases (fan in/out of the real, unpadded layer).  A
+        column shard takes its slice of the global initialisation, so G sharded engines start from
+        exactly the single-engine weights."""
+        if self.shard:
+            c0, c1, NT = self.shard
+            dims = [self.k * NT] + self.H + [NT]
+            ws = [glorot_uniform(rng, i, o) for i, o in zip(dims[:-1], dims[1:])]
+            rows0 = np.concatenate([np.arange(b * NT + c0, b * NT + c1) for b in range(self.k)])
+            ws[0] = ws[0][rows0]
+            ws[-1] = ws[-1][:, c0:c1]
+        else:
+            ws = [glorot_uniform(rng, i, o) for i, o in zip(self.real_dims[:-1], self.real_dims[1:])]
         self.set_weights([x for w in ws for x in (w, np.zeros(w.shape[1], np.float32))])
 
     def get_weights(self):
@@ -177,6 +192,10 @@ class Engine:
         self.n_stats = 0
         self.dense_in = None
         self.timers = None          # {phase: [(start_event, end_event), ...]} when profiling
+        if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
+            self.hpre = torch.zeros(Bp, self.Hp[0], device=d, dtype=torch.float32)
+            self.dhpre = torch.zeros(Bp, self.Hp[-1], device=d, dtype=torch.float32)
+            self.zero_bias = torch.zeros(max(self.Hp), device=d, dtype=torch.float32)
 
     # ---------------------------------------------------------------- phase timing (bench.py)
     def enable_timers(self, on=True):
@@ -323,7 +342,15 @@ class Engine:
         with self.phase("enc_gemm"):
             self._gemm(self.xin, 0, self.pad_dims[0], self.W[0], _lib.DT_F32, 1, Hp0, Bp, Hp0, self.pad_dims[0],
                        _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
-        call("ocf_splitk_bias_act", ptr(self.slabs), self.splits0, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
+        src, nsplit = self.slabs, self.splits0
+        if self.comm is not None:
+            # partial pre-activation over this rank's columns -> sum over ranks -> activation
+            call("ocf_splitk_bias_act", ptr(self.slabs), self.splits0, sstride, Bp, Hp0, Hp0, ptr(self.zero_bias),
+                 _lib.ACT["linear"], 1.0, 0, 0, None, None, ptr(self.hpre), None, self.cdt, Bp, Hp0, s)
+            with self.phase("allreduce_fwd"):
+                self.comm(self.hpre)
+            src, nsplit = self.hpre, 1
+        call("ocf_splitk_bias_act", ptr(src), nsplit, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
              keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
              ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
         for i in range(1, L):
@@ -335,7 +362,7 @@ class Engine:
     def output_loss(self, with_grad):
         """Decoder GEMM with the fused masked-MSE epilogue; stats -> stats_hist[n_stats]."""
         L = len(self.H)
-        gscale = 2.0 / (self.B * self.N)
+        gscale = 2.0 / (self.B * self.N_total)
         with self.phase("dec_gemm_mse"):
             self._gemm_mse(L, gscale, with_grad)
         self._grow_stats(self.n_stats + 1)
@@ -367,7 +394,7 @@ class Engine:
         the caller all-reduces and calls apply_grads()."""
         s = cur_stream()
         L, Bp = len(self.H), self.Bp
-        gscale = 2.0 / (self.B * self.N)
+        gscale = 2.0 / (self.B * self.N_total)
         fused = grads_out is None
         op = self.opt.step_params(1.0, self.l2) if fused else None
         self._bias_op = self.opt.step_params(1.0, 0.0) if fused else None   # l2 regularises kernels only
@@ -378,7 +405,14 @@ class Engine:
             self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
         db_last = self.db_h[L - 1]
-        call("ocf_splitk_grad_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.a[L - 1]),
+        src, nsplit = self.slabs, self.splitsL
+        if self.comm is not None:
+            call("ocf_splitk_bias_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.zero_bias),
+                 _lib.ACT["linear"], 1.0, 0, 0, None, None, ptr(self.dhpre), None, self.cdt, Bp, HpL, s)
+            with self.phase("allreduce_bwd"):
+                self.comm(self.dhpre)
+            src, nsplit = self.dhpre, 1
+        call("ocf_splitk_grad_act", ptr(src), nsplit, sstride, Bp, HpL, HpL, ptr(self.a[L - 1]),
              ptr(self.mask[L - 1]), self.keep, self.act, ptr(self.dh[L - 1]), self.cdt, ptr(db_last[0]), gscale,
              self.B, self.H[L - 1], s)
         # output layer bias + weights
@@ -455,6 +489,10 @@ class Engine:
 
     def take_stats(self):
         """host copy of the per-step stats recorded since the last call: [steps, 4 + Bp]."""
-        out = self.stats_hist[: self.n_stats].cpu().numpy().astype(np.float64)
+        st = self.stats_hist[: self.n_stats]
+        if self.comm is not None and self.n_stats:
+            st = st.clone()
+            self.comm(st)          # SSE / SAE / counts / row SSE are sums over the column shards
+        out = st.cpu().numpy().astype(np.float64)
         self.n_stats = 0
         return out

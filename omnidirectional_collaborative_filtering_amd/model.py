@@ -97,9 +97,9 @@ class Model(object):
         out = {k: [] for k in self.metrics_names}
         for row in st:
             sse, sae, cnt = row[0], row[1], row[2]
-            out["loss"].append(sse / (B * e.N))
+            out["loss"].append(sse / (B * e.N_total))
             for name in self.metric_names:
-                out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N, self.rating_range))
+                out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N_total, self.rating_range))
         return {k: float(np.mean(v)) if v else float("nan") for k, v in out.items()}
 
     # ------------------------------------------------------------------ batch plumbing
@@ -326,7 +326,7 @@ class omni_model(object):
     def __init__(self, numlayers, num_hidden_units, input_shape, batch_size, dense_activation="tanh",
                  use_causal_info=True, use_timestamps=False, use_both_masks=False, l2_weight_regulatization=None,
                  sparse_representation=False, dropout_probability=None, use_sparse_masking_layer=False,
-                 compute_dtype="float32", seed=None, device=None, rating_range=1.0):
+                 compute_dtype="float32", seed=None, device=None, rating_range=1.0, shard=None, comm=None):
         if use_timestamps:
             raise NotImplementedError("use_timestamps: broken in the reference; not supported")
         if sparse_representation:
@@ -340,7 +340,7 @@ class omni_model(object):
         k = 1 + int(bool(use_causal_info)) + int(bool(use_both_masks))
         self.engine = Engine(input_shape, [num_hidden_units] * numlayers, batch_size, k_blocks=k,
                              activation=dense_activation, dropout=dropout_probability, l2=l2_weight_regulatization,
-                             compute_dtype=compute_dtype, device=device, seed=seed)
+                             compute_dtype=compute_dtype, device=device, seed=seed, shard=shard, comm=comm)
         self.model = Model(self.engine, bool(use_causal_info), bool(use_both_masks), rating_range)
 
     def save_weights(self, filename):

@@ -20,6 +20,10 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # OCF_REHEARSAL=1: rehearse an N-rank run on ONE GPU (all ranks on device 0, gloo transport);
+    # correctness only, timings meaningless
+    if os.environ.get("OCF_REHEARSAL") == "1":
+        backend, local = "gloo", 0
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -65,3 +69,35 @@ def dp_train_step(engine, bucket, world):
 def shard_batches(num_batches, rank, world):
     """batch indices of this rank within an epoch (rank-strided)."""
     return list(range(rank, num_batches - (num_batches % world), world))
+
+
+# ---------------------------------------------------------------------------------------------
+# Feature (column) parallelism -- SURVEY.md 8(e) "N-sharding".
+#
+# Rank g owns output/input columns [c0_g, c1_g) (users, in I-AutoRec): its rows of W1 and W_out,
+# their optimizer state, and the matching column shard of the rating CSR.  Every rank processes the
+# SAME global batch.  Per step the ranks exchange two [B, H] fp32 tensors: the partial encoder
+# pre-activation X[:, shard] W1[shard] (summed -> identical hidden activations everywhere) and the
+# partial backward delta  delta_out[:, shard] W_out[shard] (summed -> identical dh).  Weight
+# gradients never cross the fabric; the hidden layers are recomputed identically on every rank.
+# The result is one optimizer step on the global batch, exactly as on a single device (up to the
+# order of the fp32 sums).
+
+def feature_shard_range(N, rank, world, tile=128):
+    per = -(-N // world)
+    per = -(-per // tile) * tile
+    c0 = min(N, rank * per)
+    c1 = min(N, c0 + per)
+    if c1 <= c0:
+        raise ValueError("N=%d too small for %d feature shards of %d columns" % (N, world, per))
+    return c0, c1
+
+
+def make_comm(world):
+    """sum-all-reduce of a device tensor over the process group (RCCL for 'nccl'), or None."""
+    if world <= 1:
+        return None
+
+    def comm(t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return comm
