@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--phase-timers", type=int, default=1)
     ap.add_argument("--rmse", type=int, default=1)
+    ap.add_argument("--emulate-shards", type=int, default=0,
+                    help="diagnostic: run rank 0 of a G-way feature-parallel job alone (collectives skipped, "
+                         "numerics of a partial model); not a bench line")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient all-reduce)")
@@ -109,7 +112,13 @@ def main():
     n_rows = data_full.train.n_rows
     fp = world > 1 and args.parallel == "feature"
     B, H = args.batch, args.hidden
-    if fp:
+    if args.emulate_shards > 1:
+        G = args.emulate_shards
+        c0, c1 = feature_shard_range(N, 0, G)
+        data = data_full.column_shard(c0, c1)
+        Bg, shard, comm = B * G, (c0, c1, N), None
+        fp = True
+    elif fp:
         # weak scaling: 256 rows per GPU -> global batch 256*G, each rank owns N/G users
         c0, c1 = feature_shard_range(N, rank, world)
         data = data_full.column_shard(c0, c1)

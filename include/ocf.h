@@ -87,6 +87,12 @@ typedef struct OcfScatterArgs {
    * row, used to index keep1 / the device RNG so every shard sees the same reciprocal split
    * (nullable: position = e - row start) */
   const int32_t* pos1;
+  /* flattened launch: entries of the batch held by this CSR (local offsets, = boff1 when the CSR
+   * is not a column shard) and their counts; per-entry "live target" flags for the row-segment
+   * target mode of OCF_EPI_MASKED_MSE (nullable) */
+  const int64_t* lboff1; const int64_t* lboff2;
+  int64_t E1, E2;
+  uint8_t* tflag1; uint8_t* tflag2;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
@@ -127,6 +133,11 @@ typedef struct OcfGemmArgs {
   const float* pmask; int64_t ld_pmask;                       /* PREDICT output mask          */
   const int* bk_ptr; const int32_t* bk_rc; const float* bk_t; const float* bk_m;   /* MSE     */
   float* stats_part; float* row_sse_part;                     /* MSE                          */
+  /* MSE row-segment target mode (used when bk_ptr == NULL): the target CSR's column-sorted view
+   * (col/val/list index), its per-row tile pointers [rows][t_ntiles+1], the batch rows' CSR rows,
+   * the batch-local entry offsets and the scatter's live-target flags; every target has mask t_aux */
+  const int32_t* t_rows; const int64_t* t_rp; const int32_t* t_tptr; const int32_t* t_col; const float* t_val;
+  const int32_t* t_lidx; const uint8_t* t_flag; const int64_t* t_lboff; int t_ntiles; float t_aux;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

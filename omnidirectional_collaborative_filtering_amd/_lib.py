@@ -39,6 +39,7 @@ class OcfScatterArgs(ctypes.Structure):
         ("xin", P), ("xin_dtype", I32), ("xin_ld", I64), ("xin_block", I64), ("feed", I32), ("both", I32),
         ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
         ("pos1", P),
+        ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
     ]
 
 
@@ -55,6 +56,8 @@ class OcfGemmArgs(ctypes.Structure):
         ("p", P), ("s1", P), ("s2", P), ("opt", OcfOptParams),
         ("pmask", P), ("ld_pmask", I64),
         ("bk_ptr", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("stats_part", P), ("row_sse_part", P),
+        ("t_rows", P), ("t_rp", P), ("t_tptr", P), ("t_col", P), ("t_val", P), ("t_lidx", P), ("t_flag", P),
+        ("t_lboff", P), ("t_ntiles", I32), ("t_aux", F32),
     ]
 
 

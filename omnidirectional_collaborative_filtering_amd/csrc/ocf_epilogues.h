@@ -282,10 +282,23 @@ struct EpiMaskedMSE {
   static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 2 * GT_BN * 4 + 3 * 4 * 4;
   struct Params {
     const float* bias;        // output bias [N]
+    // bucket target mode (bk_ptr != nullptr): entries bucketed by 128-column tile
     const int* bk_ptr;        // [n_tiles+1]
     const int* bk_rc;         // (row << 7) | (col & 127)
     const float* bk_t;        // target value
     const float* bk_m;        // output-mask value
+    // row-segment target mode: each batch row's entries of this column tile, from the target
+    // CSR's column-sorted view; a thread owns a row (deterministic sums, no atomics)
+    const int32_t* t_rows;
+    const int64_t* t_rp;
+    const int32_t* t_tptr;
+    const int32_t* t_col;
+    const float* t_val;
+    const int32_t* t_lidx;
+    const uint8_t* t_flag;
+    const int64_t* t_lboff;
+    int t_ntiles;
+    float t_aux;
     void* d_out;              // dense delta [M][ld_d] compute dtype (nullable: eval)
     int d_dtype;
     int64_t ld_d;
@@ -294,24 +307,54 @@ struct EpiMaskedMSE {
     float gscale;
     float* stats_part;        // [n_tiles * gm][4]: sse, sae, nnz(T+yhat), unused
     float* row_sse_part;      // [n_tiles][M] (nullable)
+    int m_real;
   };
   struct Pre {
-    int b0, b1;
-    int rc[NPRE];
+    int b0, b1;               // bucket mode: bucket range
+    int rc[NPRE];             // bucket mode: prefetched entries; segment mode: column | -1
     float t[NPRE], m[NPRE];
+    int64_t s_lo, s_hi, lb;   // segment mode: this thread's half of its row's segment
   };
-  __device__ static Pre prologue(const Params& p, int, int tile_n, int, int, int tid, const GemmShape&) {
+  // segment mode: thread tid owns half (tid >> 7) of row (tid & 127)'s entries in this column tile
+  __device__ static int seg_col(const Params& p, int64_t e, int64_t lb) {
+    return p.t_flag[lb + p.t_lidx[e]] ? (p.t_col[e] & (GT_BN - 1)) : -1;
+  }
+  __device__ static Pre prologue(const Params& p, int, int tile_n, int m0, int, int tid, const GemmShape&) {
     Pre q;
-    q.b0 = p.bk_ptr[tile_n];
-    q.b1 = p.bk_ptr[tile_n + 1];
+    q.b0 = q.b1 = 0;
+    q.s_lo = q.s_hi = q.lb = 0;
+#pragma unroll
+    for (int k = 0; k < NPRE; ++k) { q.rc[k] = -1; q.t[k] = 0.f; q.m[k] = 0.f; }
+    if (p.bk_ptr) {
+      q.b0 = p.bk_ptr[tile_n];
+      q.b1 = p.bk_ptr[tile_n + 1];
+#pragma unroll
+      for (int k = 0; k < NPRE; ++k) {
+        int e = q.b0 + tid + k * GT_THREADS;
+        bool ok = e < q.b1;
+        q.rc[k] = ok ? p.bk_rc[e] : -1;
+        q.t[k] = ok ? p.bk_t[e] : 0.f;
+        q.m[k] = ok ? p.bk_m[e] : 0.f;
+      }
+      return q;
+    }
+    const int b = m0 + (tid & (GT_BM - 1));
+    if (b >= p.m_real) return q;
+    const int r = p.t_rows[b];
+    if (r < 0) return q;
+    const int64_t base = p.t_rp[r];
+    const int32_t* tp = p.t_tptr + (int64_t)r * (p.t_ntiles + 1) + tile_n;
+    const int64_t lo = base + tp[0], hi = base + tp[1];
+    const int64_t mid = lo + ((hi - lo + 1) >> 1);
+    q.s_lo = (tid < GT_BM) ? lo : mid;
+    q.s_hi = (tid < GT_BM) ? mid : hi;
+    q.lb = p.t_lboff[b];
 #pragma unroll
     for (int k = 0; k < NPRE; ++k) {
-      int e = q.b0 + tid + k * GT_THREADS;
-      bool ok = e < q.b1;
-      q.rc[k] = ok ? p.bk_rc[e] : -1;
-      q.t[k] = ok ? p.bk_t[e] : 0.f;
-      q.m[k] = ok ? p.bk_m[e] : 0.f;
+      const int64_t e = q.s_lo + k;
+      if (e < q.s_hi) { q.rc[k] = seg_col(p, e, q.lb); q.t[k] = p.t_val[e]; }
     }
+    q.s_lo += NPRE;
     return q;
   }
   __device__ static void entry(float* Y, uint32_t* bits, float* rsse, int m0, int rc, float t, float m, float& sse,
@@ -348,12 +391,45 @@ struct EpiMaskedMSE {
     for (int i = c.tid; i < GT_BM * 4; i += GT_THREADS) bits[i] = 0u;
     if (c.tid < GT_BM) rsse[c.tid] = 0.f;
     __syncthreads();
-    // 2. target entries of this column tile falling in this row tile (first NPRE per thread prefetched)
+    // 2. this tile's target entries
     float sse = 0.f, sae = 0.f, cnt = 0.f;
+    if (p.bk_ptr) {
 #pragma unroll
-    for (int k = 0; k < NPRE; ++k) entry(Y, bits, rsse, c.m0, q.rc[k], q.t[k], q.m[k], sse, sae, cnt);
-    for (int e = q.b0 + c.tid + NPRE * GT_THREADS; e < q.b1; e += GT_THREADS)
-      entry(Y, bits, rsse, c.m0, p.bk_rc[e], p.bk_t[e], p.bk_m[e], sse, sae, cnt);
+      for (int k = 0; k < NPRE; ++k) entry(Y, bits, rsse, c.m0, q.rc[k], q.t[k], q.m[k], sse, sae, cnt);
+      for (int e = q.b0 + c.tid + NPRE * GT_THREADS; e < q.b1; e += GT_THREADS)
+        entry(Y, bits, rsse, c.m0, p.bk_rc[e], p.bk_t[e], p.bk_m[e], sse, sae, cnt);
+    } else {
+      // segment mode: live targets of this row half, at most one per (row, column)
+      const int ml = c.tid & (GT_BM - 1);
+      const float m = p.t_aux;
+      float rs = 0.f;
+      auto one = [&](int nl, float t) {
+        if (nl < 0) return;
+        const float yhat = m * Y[ml * YS + nl];
+        const float err = yhat - t;
+        Y[ml * YS + nl] = err * m;
+        atomicOr(&bits[ml * 4 + (nl >> 5)], 1u << (nl & 31));
+        rs += err * err;
+        sae += fabsf(err);
+        cnt += (t + yhat != 0.f) ? 1.f : 0.f;
+      };
+#pragma unroll
+      for (int k = 0; k < NPRE; ++k) one(q.rc[k], q.t[k]);
+      for (int64_t e = q.s_lo; e < q.s_hi; e += 4) {
+        int nl[4];
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const bool ok = e + k < q.s_hi;
+          nl[k] = ok ? seg_col(p, e + k, q.lb) : -1;
+          t[k] = ok ? p.t_val[e + k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) one(nl[k], t[k]);
+      }
+      sse = rs;
+      atomicAdd(&rsse[ml], rs);   // exactly two addends onto 0: order-independent
+    }
     __syncthreads();
     // 3. dense delta tile (zeros where no target) -> compute dtype, 8 columns per chunk
     if (p.d_out) {

@@ -69,7 +69,13 @@ void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
         p.bias = g.bias; p.bk_ptr = g.bk_ptr; p.bk_rc = g.bk_rc; p.bk_t = g.bk_t; p.bk_m = g.bk_m;
         p.d_out = g.h_out; p.d_dtype = g.h_dtype; p.ld_d = g.ld_out; p.db_part = g.db_part; p.ld_db = g.ld_db;
         p.gscale = g.opt.gscale; p.stats_part = g.stats_part; p.row_sse_part = g.row_sse_part;
-        OCF_CHECK(g.stats_part && g.bk_ptr, "ocf_gemm MASKED_MSE: stats_part / buckets required");
+        p.t_rows = g.t_rows; p.t_rp = g.t_rp; p.t_tptr = g.t_tptr; p.t_col = g.t_col; p.t_val = g.t_val;
+        p.t_lidx = g.t_lidx; p.t_flag = g.t_flag; p.t_lboff = g.t_lboff; p.t_ntiles = g.t_ntiles; p.t_aux = g.t_aux;
+        p.m_real = g.m_real;
+        OCF_CHECK(g.stats_part, "ocf_gemm MASKED_MSE: stats_part required");
+        OCF_CHECK(g.bk_ptr || (g.t_rows && g.t_rp && g.t_tptr && g.t_col && g.t_val && g.t_lidx && g.t_flag &&
+                               g.t_lboff && g.t_ntiles * GT_BN >= g.N),
+                  "ocf_gemm MASKED_MSE: bucket or row-segment targets required");
         launch<CT, ACOL, BCOL, float, EpiMaskedMSE>(g, p, s);
         return;
       }

@@ -1,6 +1,6 @@
 // K1: sparse-rating -> dense-batch assembly (replaces data_reader.py:95-298).
 //
-// Grid (B, 4): four workgroups per batch row.  The dataset lives in HBM as row-CSR in the reference's list
+// Flattened grid (one thread per batch entry, see scatter_flat_kernel).  The dataset lives in HBM as row-CSR in the reference's list
 // order (row_ptr int64, col int32 = dense column index, val f32) plus an optional duplicate
 // chain dup[e] = next entry of the same row with the same column (or -1), so that the
 // reference's last-write-wins per array (data_reader.py:158-166, 250-266) is reproduced by a
@@ -47,76 +47,92 @@ __device__ __forceinline__ void store_val(void* base, int dtype, int64_t idx, fl
   else reinterpret_cast<__bf16*>(base)[idx] = (__bf16)v;
 }
 
-// grid (B, SPLIT): workgroup (b, s) handles entries s*256 + tid, step SPLIT*256, of batch row b.
-// The outputs were zeroed by hipMemsetAsync on the same stream before this launch.
-constexpr int SCATTER_SPLIT = 4;
+// Flattened launch: one thread per batch entry held by this CSR, 256 entries per workgroup, so the
+// load balances whatever the row lengths (full rows on one GPU, ~1/G of them per column shard).
+// Blocks [0, nblk1) take source-1 entries, the rest source-2 entries.  A thread finds its batch row
+// by binary search over the batch offsets staged in LDS.  The outputs were zeroed by
+// hipMemsetAsync on the same stream before this launch.
+constexpr int SC_THREADS = 256;
 
-__global__ void __launch_bounds__(256) scatter_rows_kernel(ScatterArgs a) {
-  const int b = blockIdx.x;
-  const int tid = blockIdx.y * blockDim.x + threadIdx.x;
-  const int nthr = gridDim.y * blockDim.x;
+__device__ __forceinline__ int find_row(const int64_t* off, int B, int64_t e) {
+  int lo = 0, hi = B;   // off[lo] <= e < off[hi]; empty rows are skipped because off[b] == off[b+1]
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (off[mid] <= e) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a, int nblk1) {
+  extern __shared__ int64_t sh_off[];
+  const bool src2 = (int)blockIdx.x >= nblk1;
+  const int64_t* lboff = src2 ? a.lboff2 : (a.lboff1 ? a.lboff1 : a.boff1);
+  const int B = a.B;
+  for (int i = threadIdx.x; i <= B; i += SC_THREADS) sh_off[i] = lboff[i];
+  __syncthreads();
+  const int64_t e = (int64_t)(src2 ? (int)blockIdx.x - nblk1 : (int)blockIdx.x) * SC_THREADS + threadIdx.x;
+  if (e >= (src2 ? a.E2 : a.E1)) return;
+  const int b = find_row(sh_off, B, e);
+  const int64_t j = e - sh_off[b];
   const float aux = a.aux;
   const int64_t xb = a.xin_block;
-
-  // source 1
-  int r1 = a.rows1 ? a.rows1[b] : -1;
-  if (r1 >= 0) {
-    const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
+  if (!src2) {
+    const int r1 = a.rows1[b];
+    const int64_t s = a.rp1[r1];
+    const int64_t i = s + j;
     const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
     const float cut = row_cut(a, b);
-    for (int64_t i = s + tid; i < e; i += nthr) {
-      const int c = a.col1[i];
-      const float v = a.val1[i];
-      const int role = role1(a, b, a.pos1 ? a.pos1[i] : i - s, bo1, cut);
-      // later duplicates of the same column that also write the value arrays
-      bool later_in = false, later_tg = false;
-      if (a.dup1) {
-        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) {
-          int rf = role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut);
-          later_in |= (rf & 1) != 0;
-          later_tg |= (rf & 2) != 0;
-        }
-      }
-      const int64_t o = (int64_t)b * a.ld + c;
-      const int64_t ox = (int64_t)b * a.xin_ld + c;
-      if (role & 1) {
-        if (a.Min) a.Min[o] = aux;
-        if (!later_in) {
-          if (a.X) a.X[o] = v;
-          if (a.xin) store_val(a.xin, a.xin_dtype, ox, v);
-        }
-        if (a.xin && a.feed == 1) store_val(a.xin, a.xin_dtype, ox + xb, aux);
-      }
-      if (role & 2) {
-        if (a.Mout) a.Mout[o] = aux;
-        if (!later_tg && a.T) a.T[o] = v;
-        if (!later_tg && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
-      }
-      if (a.Mmiss) a.Mmiss[o] = aux;
-      if (a.xin) {
-        if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
-        if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
+    const int c = a.col1[i];
+    const float v = a.val1[i];
+    const int role = role1(a, b, a.pos1 ? a.pos1[i] : j, bo1, cut);
+    // later duplicates of the same column that also write the value arrays (last write wins)
+    bool later_in = false, later_tg = false;
+    if (a.dup1) {
+      for (int f = a.dup1[i]; f >= 0; f = a.dup1[f]) {
+        int rf = role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut);
+        later_in |= (rf & 1) != 0;
+        later_tg |= (rf & 2) != 0;
       }
     }
-  }
-  // source 2 (eval targets)
-  int r2 = a.rows2 ? a.rows2[b] : -1;
-  if (r2 >= 0) {
-    const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
-    for (int64_t i = s + tid; i < e; i += nthr) {
-      const int c = a.col2[i];
-      const float v = a.val2[i];
-      const bool dead = a.dup2 && a.dup2[i] >= 0;   // every source-2 entry is a target
-      const int64_t o = (int64_t)b * a.ld + c;
-      const int64_t ox = (int64_t)b * a.xin_ld + c;
-      if (a.Mout) a.Mout[o] = aux;
-      if (!dead && a.T) a.T[o] = v;
-      if (!dead && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
-      if (a.Mmiss) a.Mmiss[o] = aux;
-      if (a.xin) {
-        if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
-        if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
+    const int64_t o = (int64_t)b * a.ld + c;
+    const int64_t ox = (int64_t)b * a.xin_ld + c;
+    if (role & 1) {
+      if (a.Min) a.Min[o] = aux;
+      if (!later_in) {
+        if (a.X) a.X[o] = v;
+        if (a.xin) store_val(a.xin, a.xin_dtype, ox, v);
       }
+      if (a.xin && a.feed == 1) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+    }
+    const bool live_tg = (role & 2) && !later_tg;
+    if (role & 2) {
+      if (a.Mout) a.Mout[o] = aux;
+      if (live_tg && a.T) a.T[o] = v;
+      if (live_tg && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
+    }
+    if (a.tflag1) a.tflag1[e] = live_tg ? 1 : 0;
+    if (a.Mmiss) a.Mmiss[o] = aux;
+    if (a.xin) {
+      if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+      if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
+    }
+  } else {
+    const int r2 = a.rows2[b];
+    const int64_t i = a.rp2[r2] + j;
+    const int c = a.col2[i];
+    const float v = a.val2[i];
+    const bool dead = a.dup2 && a.dup2[i] >= 0;   // every source-2 entry is a target
+    const int64_t o = (int64_t)b * a.ld + c;
+    const int64_t ox = (int64_t)b * a.xin_ld + c;
+    if (a.Mout) a.Mout[o] = aux;
+    if (!dead && a.T) a.T[o] = v;
+    if (!dead && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
+    if (a.tflag2) a.tflag2[e] = dead ? 0 : 1;
+    if (a.Mmiss) a.Mmiss[o] = aux;
+    if (a.xin) {
+      if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
+      if (a.both) store_val(a.xin, a.xin_dtype, ox + 2 * xb, aux);
     }
   }
 }
@@ -149,41 +165,41 @@ __global__ void __launch_bounds__(1024) bucket_scan_kernel(int* tile_cnt, int* b
   if (tid == 1023) bk_ptr[n_tiles] = part[1023];
 }
 
-__global__ void __launch_bounds__(256) bucket_fill_kernel(ScatterArgs a) {
-  const int b = blockIdx.x;
-  const int tid = blockIdx.y * blockDim.x + threadIdx.x;
-  const int nthr = gridDim.y * blockDim.x;
-  int r1 = a.rows1 ? a.rows1[b] : -1;
-  if (r1 >= 0 && a.mode == 0) {
-    const int64_t s = a.rp1[r1], e = a.rp1[r1 + 1];
+__global__ void __launch_bounds__(SC_THREADS) bucket_fill_kernel(ScatterArgs a, int nblk1) {
+  extern __shared__ int64_t sh_off[];
+  const bool src2 = (int)blockIdx.x >= nblk1;
+  const int64_t* lboff = src2 ? a.lboff2 : (a.lboff1 ? a.lboff1 : a.boff1);
+  const int B = a.B;
+  for (int i = threadIdx.x; i <= B; i += SC_THREADS) sh_off[i] = lboff[i];
+  __syncthreads();
+  const int64_t e = (int64_t)(src2 ? (int)blockIdx.x - nblk1 : (int)blockIdx.x) * SC_THREADS + threadIdx.x;
+  if (e >= (src2 ? a.E2 : a.E1)) return;
+  const int b = find_row(sh_off, B, e);
+  const int64_t j = e - sh_off[b];
+  if (!src2) {
+    if (a.mode != 0) return;
+    const int64_t s = a.rp1[a.rows1[b]];
+    const int64_t i = s + j;
     const int64_t bo1 = a.boff1 ? a.boff1[b] : 0;
     const float cut = row_cut(a, b);
-    for (int64_t i = s + tid; i < e; i += nthr) {
-      const int role = role1(a, b, a.pos1 ? a.pos1[i] : i - s, bo1, cut);
-      if (!(role & 2)) continue;
-      bool later_tg = false;
-      if (a.dup1)
-        for (int f = a.dup1[i]; f >= 0; f = a.dup1[f])
-          later_tg |= (role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut) & 2) != 0;
-      if (later_tg) continue;
-      const int c = a.col1[i];
-      int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
-      a.bk_rc[slot] = (b << 7) | (c & 127);
-      a.bk_t[slot] = a.val1[i];
-      a.bk_m[slot] = a.aux;
-    }
-  }
-  int r2 = a.rows2 ? a.rows2[b] : -1;
-  if (r2 >= 0) {
-    const int64_t s = a.rp2[r2], e = a.rp2[r2 + 1];
-    for (int64_t i = s + tid; i < e; i += nthr) {
-      if (a.dup2 && a.dup2[i] >= 0) continue;
-      const int c = a.col2[i];
-      int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
-      a.bk_rc[slot] = (b << 7) | (c & 127);
-      a.bk_t[slot] = a.val2[i];
-      a.bk_m[slot] = a.aux;
-    }
+    const int role = role1(a, b, a.pos1 ? a.pos1[i] : j, bo1, cut);
+    if (!(role & 2)) return;
+    if (a.dup1)
+      for (int f = a.dup1[i]; f >= 0; f = a.dup1[f])
+        if (role1(a, b, a.pos1 ? a.pos1[f] : f - s, bo1, cut) & 2) return;
+    const int c = a.col1[i];
+    int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
+    a.bk_rc[slot] = (b << 7) | (c & 127);
+    a.bk_t[slot] = a.val1[i];
+    a.bk_m[slot] = a.aux;
+  } else {
+    const int64_t i = a.rp2[a.rows2[b]] + j;
+    if (a.dup2 && a.dup2[i] >= 0) return;
+    const int c = a.col2[i];
+    int slot = atomicAdd(&a.bk_cur[c >> 7], 1);
+    a.bk_rc[slot] = (b << 7) | (c & 127);
+    a.bk_t[slot] = a.val2[i];
+    a.bk_m[slot] = a.aux;
   }
 }
 
@@ -244,17 +260,26 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   if (a.tile_cnt) OCF_CHECK(a.bk_ptr && a.bk_cur && a.bk_rc && a.bk_t && a.bk_m && a.n_tiles > 0,
                             "ocf_scatter_batch: bucket outputs incomplete");
   if (a.B_pad == 0) return 0;
+  OCF_CHECK(a.B <= 16384, "ocf_scatter_batch: B too large for the LDS offset table");
+  OCF_CHECK(a.E1 >= 0 && a.E2 >= 0, "ocf_scatter_batch: negative entry counts");
+  OCF_CHECK(a.E2 == 0 || (a.rows2 && a.lboff2), "ocf_scatter_batch: source 2 needs rows2 / lboff2");
+  OCF_CHECK(a.E1 == 0 || (a.rows1 && (a.lboff1 || a.boff1)), "ocf_scatter_batch: source 1 needs rows1 / offsets");
   // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks)
   float* dense[5] = {a.X, a.Min, a.Mout, a.T, a.Mmiss};
   for (float* d : dense)
     if (d) OCF_HIP(hipMemsetAsync(d, 0, (size_t)a.B_pad * a.ld * 4, s));
   if (a.xin) OCF_HIP(hipMemsetAsync(a.xin, 0, (size_t)a.B_pad * a.xin_ld * (a.xin_dtype == OCF_F32 ? 4 : 2), s));
-  if (a.B > 0) hipLaunchKernelGGL(scatter_rows_kernel, dim3(a.B, SCATTER_SPLIT), dim3(256), 0, s, a);
+  const int nblk1 = (int)((a.E1 + SC_THREADS - 1) / SC_THREADS);
+  const int nblk2 = (int)((a.E2 + SC_THREADS - 1) / SC_THREADS);
+  const size_t shm = (size_t)(a.B + 1) * sizeof(int64_t);
+  if (nblk1 + nblk2 > 0)
+    hipLaunchKernelGGL(scatter_flat_kernel, dim3(nblk1 + nblk2), dim3(SC_THREADS), shm, s, a, nblk1);
   OCF_HIP(hipGetLastError());
   if (a.tile_cnt) {
     hipLaunchKernelGGL(bucket_scan_kernel, dim3(1), dim3(1024), 0, s, a.tile_cnt, a.bk_ptr, a.bk_cur, a.n_tiles);
     OCF_HIP(hipGetLastError());
-    if (a.B > 0) hipLaunchKernelGGL(bucket_fill_kernel, dim3(a.B, SCATTER_SPLIT), dim3(256), 0, s, a);
+    if (nblk1 + nblk2 > 0)
+      hipLaunchKernelGGL(bucket_fill_kernel, dim3(nblk1 + nblk2), dim3(SC_THREADS), shm, s, a, nblk1);
     OCF_HIP(hipGetLastError());
   }
   OCF_TRY_END

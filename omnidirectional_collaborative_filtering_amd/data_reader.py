@@ -38,6 +38,20 @@ class _DeviceCSR:
         self.pos = None if csr.pos is None else torch.as_tensor(csr.pos, device=dev)
         self.lens = csr.row_lengths()          # entries held here (a column shard holds fewer)
         self.rng_lens = csr.rng_lengths()      # entries of the full rows (RNG draws, batch offsets)
+        self.dev = dev
+        self._tiles = {}
+
+    def tiles(self, n_cols):
+        """Column-sorted copy + per-row tile pointers (dataset.RatingsCSR.tile_index) on the device,
+        built once per CSR: the masked-MSE epilogue reads each batch row's targets of its column
+        tile from here (row-segment mode)."""
+        if n_cols not in self._tiles:
+            col_s, val_s, lidx_s, tptr = self.host.tile_index(n_cols)
+            d = self.dev
+            self._tiles[n_cols] = dict(t_col=torch.as_tensor(col_s, device=d), t_val=torch.as_tensor(val_s, device=d),
+                                       t_lidx=torch.as_tensor(lidx_s, device=d), t_tptr=torch.as_tensor(tptr, device=d),
+                                       t_ntiles=tptr.shape[1] - 1)
+        return self._tiles[n_cols]
 
 
 class data_reader(object):
@@ -165,10 +179,13 @@ class BatchGenerator(object):
         self.rows_host = rows
         self.nnz_full = boff[:, -1].copy()
         self.nnz1 = self.src1.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)   # entries held here
-        if self.src2 is not None:
-            self.tlocal = self.src2.lens[rows].sum(axis=1)
         self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
         self.boff_dev = torch.as_tensor(boff, device=r.device)
+        # batch-local offsets of the entries held by this CSR (one scatter thread per entry)
+        self.lboff1_dev = torch.as_tensor(self._local_offsets(self.src1.lens, rows), device=r.device)
+        if self.src2 is not None:
+            self.tlocal = self.src2.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)
+            self.lboff2_dev = torch.as_tensor(self._local_offsets(self.src2.lens, rows), device=r.device)
         self.keep_dev = None
         self.keep_off = None
         if keep is not None:
@@ -176,6 +193,12 @@ class BatchGenerator(object):
             self.keep_off = np.concatenate([[0], np.cumsum(self.nnz_full)])
         self.max_targets = int(max(self.nnz1.max() if nb else 0,
                                    self.tlocal.max() if (self.src2 is not None and nb) else 0))
+
+    @staticmethod
+    def _local_offsets(lens, rows):
+        off = np.zeros((rows.shape[0], rows.shape[1] + 1), dtype=np.int64)
+        np.cumsum(lens[rows], axis=1, out=off[:, 1:])
+        return off
 
     def scatter_args(self, bi, engine_args=None, dense=None, B_pad=None):
         """OcfScatterArgs for batch bi (onto an engine's xin/buckets and/or dense outputs)."""
@@ -186,6 +209,8 @@ class BatchGenerator(object):
         a.pos1 = ptr(s1.pos)
         a.rows1 = self.rows_dev.data_ptr() + 4 * bi * B
         a.boff1 = self.boff_dev.data_ptr() + 8 * bi * (B + 1)
+        a.lboff1 = self.lboff1_dev.data_ptr() + 8 * bi * (B + 1)
+        a.E1 = int(self.nnz1[bi])
         a.keep1 = None if self.keep_dev is None else self.keep_dev.data_ptr() + int(self.keep_off[bi])
         if self.split == "train":
             a.mode = 0
@@ -200,6 +225,8 @@ class BatchGenerator(object):
             s2 = self.src2
             a.rp2, a.col2, a.val2, a.dup2 = ptr(s2.rp), ptr(s2.col), ptr(s2.val), ptr(s2.dup)
             a.rows2 = a.rows1
+            a.lboff2 = self.lboff2_dev.data_ptr() + 8 * bi * (B + 1)
+            a.E2 = int(self.tlocal[bi])
         a.B = B
         a.aux = self.aux
         a.feed = AUX_FEED[self.aux_type]
@@ -219,6 +246,20 @@ class BatchGenerator(object):
         bi = self.i
         self.i += 1
         return bi
+
+    def targets(self, bi, n_cols):
+        """Where batch bi's target entries live, for the masked-MSE epilogue's row-segment mode:
+        the target CSR's tile index, the batch rows, their local entry offsets, the entry count and
+        which scatter flag array (1 = train entries, 2 = eval target entries) marks live targets."""
+        B = self.B
+        train = self.split == "train"
+        src = self.src1 if train else self.src2
+        lb = self.lboff1_dev if train else self.lboff2_dev
+        t = dict(src.tiles(n_cols))
+        t.update(t_rows=self.rows_dev.data_ptr() + 4 * bi * B, t_rp=ptr(src.rp),
+                 t_lboff=lb.data_ptr() + 8 * bi * (B + 1), t_aux=self.aux,
+                 E=int(self.nnz1[bi] if train else self.tlocal[bi]), flag=1 if train else 2)
+        return t
 
     def target_count(self, bi):
         """target_count of batch bi (data_reader.py:268): list entries of the target rows (full rows;

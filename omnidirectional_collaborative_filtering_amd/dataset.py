@@ -71,6 +71,25 @@ class RatingsCSR:
         """entries per row as the reference's RNG sees them (full rows, also for a column shard)"""
         return self.full_lens if self.full_lens is not None else self.row_lengths()
 
+    def tile_index(self, n_cols, tile=128):
+        """Column-sorted view for per-tile target lookup (OCF_EPI_MASKED_MSE row-segment mode).
+
+        Returns (col_s, val_s, lidx_s, tptr): the entries of every row sorted by column (stable, so
+        duplicates keep list order), each entry's position in the row's list order, and
+        tptr[r, t] = number of row-r entries with column < tile*t  (shape [rows, n_tiles + 1])."""
+        n_tiles = -(-int(n_cols) // tile)
+        lens = self.row_lengths()
+        rows = np.repeat(np.arange(self.n_rows, dtype=np.int64), lens)
+        key = rows * (int(n_cols) + 1) + self.col.astype(np.int64)
+        order = np.argsort(key, kind="stable")
+        col_s = self.col[order]
+        val_s = self.val[order]
+        lidx_s = (order - self.row_ptr[rows[order]]).astype(np.int32)
+        counts = np.bincount(rows * n_tiles + (col_s.astype(np.int64) // tile), minlength=self.n_rows * n_tiles)
+        tptr = np.zeros((self.n_rows, n_tiles + 1), dtype=np.int32)
+        np.cumsum(counts.reshape(self.n_rows, n_tiles), axis=1, out=tptr[:, 1:])
+        return col_s, val_s, lidx_s, tptr
+
     def column_shard(self, c0, c1):
         """entries with c0 <= col < c1, columns re-based to 0, list order and full-row positions kept"""
         lens = self.row_lengths()

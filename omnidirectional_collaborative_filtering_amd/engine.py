@@ -183,6 +183,8 @@ class Engine:
         self.bk_cur = torch.zeros(self.n_tiles, device=d, dtype=torch.int32)
         self.bk_cap = 0
         self._grow_buckets(1 << 16)
+        self.tflag = torch.zeros(1 << 16, device=d, dtype=torch.uint8)   # live-target flag per batch entry
+        self.tseg = None            # row-segment target descriptor of the loaded batch (None: buckets)
         gm = Bp // TILE
         self.stats_part = torch.zeros(self.n_tiles * gm * 4, device=d, dtype=torch.float32)
         self.row_sse_part = torch.zeros(self.n_tiles * Bp, device=d, dtype=torch.float32)
@@ -257,6 +259,8 @@ class Engine:
 
     # ---------------------------------------------------------------- batch assembly
     def scatter_args(self):
+        """K1 arguments onto this engine's layer-0 input; target bucketing is added by load_dense's
+        path only (generator batches use the row-segment mode, see load_batch)."""
         a = OcfScatterArgs()
         a.B = self.B
         a.B_pad = self.Bp
@@ -275,10 +279,22 @@ class Engine:
         a.s0 = a.s1 = 1.0
         return a
 
-    def load_batch(self, a, max_targets):
-        """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller)."""
-        self._grow_buckets(max_targets)
-        a.bk_rc, a.bk_t, a.bk_m = ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m)
+    def load_batch(self, a, targets):
+        """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller).
+
+        ``targets`` (BatchGenerator.targets) names the target CSR's tile index: the scatter marks
+        each target entry live/dead in self.tflag and the masked-MSE epilogue reads every batch
+        row's segment per column tile directly -- no bucketing pass, no atomics."""
+        if targets["t_ntiles"] != self.n_tiles:
+            raise ValueError("target tile index has %d tiles, engine %d" % (targets["t_ntiles"], self.n_tiles))
+        if targets["E"] > self.tflag.numel():
+            self.tflag = torch.zeros(max(targets["E"], 2 * self.tflag.numel()), device=self.dev, dtype=torch.uint8)
+        a.tile_cnt = a.bk_ptr = a.bk_cur = a.bk_rc = a.bk_t = a.bk_m = None
+        a.tflag1 = ptr(self.tflag) if targets["flag"] == 1 else None
+        a.tflag2 = ptr(self.tflag) if targets["flag"] == 2 else None
+        seg = {k: v for k, v in targets.items() if k.startswith("t_")}
+        seg["t_flag"] = self.tflag
+        self.tseg = seg
         with self.phase("scatter"):
             call("ocf_scatter_batch", a, cur_stream())
 
@@ -303,6 +319,7 @@ class Engine:
         call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
              self.Bp, s)
         self._grow_buckets(B * N)
+        self.tseg = None
         call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
              ptr(self.bk_ptr), ptr(self.bk_cur), ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m), s)
 
@@ -371,9 +388,10 @@ class Engine:
         self.n_stats += 1
 
     def _gemm_mse(self, L, gscale, with_grad):
+        tg = self.tseg if self.tseg is not None else dict(bk_ptr=self.bk_ptr, bk_rc=self.bk_rc, bk_t=self.bk_t,
+                                                          bk_m=self.bk_m)
         self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 0, self.Hp[L - 1], self.Bp, self.Np,
-                   self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], bk_ptr=self.bk_ptr,
-                   bk_rc=self.bk_rc, bk_t=self.bk_t, bk_m=self.bk_m,
+                   self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], m_real=self.B, **tg,
                    h_out=self.d_out if with_grad else None, h_dtype=self.cdt, ld_out=self.Np,
                    db_part=self.db_out_part if with_grad else None, ld_db=self.Np,
                    opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
