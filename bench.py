@@ -197,13 +197,17 @@ def main():
     if phases:
         cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
         dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
+    # weight operands: the compute-dtype shadow (2 B) written by the optimizer epilogue, fp32 in fp32 mode
+    w_b = 4 if args.dtype == "float32" else 2
+    sh_b = 0 if args.dtype == "float32" else 2
     alg = {
-        # bytes per launch, algorithmic (real, unpadded sizes of this rank): optimizer state r/w + streamed operand
-        "dW_in": P * opt_b + Bg * Nl * 2 + Bg * H * 2,
-        "dW_out": P * opt_b + Bg * Nl * 2 + Bg * H * 2,
-        "enc_gemm": P * 4 + Bg * Nl * 2,
-        "dec_gemm_mse": P * 4 + Bg * H * 2 + Bg * Nl * 2,
-        "dec_bwd_gemm": P * 4 + Bg * Nl * 2,
+        # bytes per launch, algorithmic (real, unpadded sizes of this rank): optimizer state r/w (+ shadow
+        # write) + streamed operands
+        "dW_in": P * (opt_b + sh_b) + Bg * Nl * 2 + Bg * H * 2,
+        "dW_out": P * (opt_b + sh_b) + Bg * Nl * 2 + Bg * H * 2,
+        "enc_gemm": P * w_b + Bg * Nl * 2,
+        "dec_gemm_mse": P * w_b + Bg * H * 2 + Bg * Nl * 2,
+        "dec_bwd_gemm": P * w_b + Bg * Nl * 2,
     }
     roof = None
     if dom is not None:

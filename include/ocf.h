@@ -138,6 +138,9 @@ typedef struct OcfGemmArgs {
    * the batch-local entry offsets and the scatter's live-target flags; every target has mask t_aux */
   const int32_t* t_rows; const int64_t* t_rp; const int32_t* t_tptr; const int32_t* t_col; const float* t_val;
   const int32_t* t_lidx; const uint8_t* t_flag; const int64_t* t_lboff; int t_ntiles; float t_aux;
+  /* OPTIM: also write the updated weights in the compute dtype (same layout as p, nullable), the
+   * half-width shadow the next forward / backward GEMMs stream instead of the fp32 master copy */
+  void* p_shadow;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

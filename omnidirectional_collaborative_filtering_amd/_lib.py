@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libocf.so")
+LIB_PATH = os.environ.get("OCF_LIB_PATH") or os.path.join(_HERE, "libocf.so")   # override: variant builds
 
 DT_F32, DT_F16, DT_BF16 = 0, 1, 2
 ACT = {"linear": 0, None: 0, "sigmoid": 1, "tanh": 2, "relu": 3}
@@ -58,6 +58,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("bk_ptr", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("stats_part", P), ("row_sse_part", P),
         ("t_rows", P), ("t_rp", P), ("t_tptr", P), ("t_col", P), ("t_val", P), ("t_lidx", P), ("t_flag", P),
         ("t_lboff", P), ("t_ntiles", I32), ("t_aux", F32),
+        ("p_shadow", P),
     ]
 
 

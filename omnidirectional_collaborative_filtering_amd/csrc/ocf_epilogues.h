@@ -6,6 +6,21 @@
 namespace ocf {
 
 struct NoPre {};
+// two K-steps of operand loads in flight (gemm_kernel DEEP), per epilogue family.  Off by default:
+// measured neutral on the ML-20M shapes (the K-loop is issue-bound, not latency-bound) and it costs
+// occupancy where the epilogue is register-heavy.
+#ifndef OCF_DEEP_SLAB
+#define OCF_DEEP_SLAB false
+#endif
+#ifndef OCF_DEEP_MSE
+#define OCF_DEEP_MSE false
+#endif
+#ifndef OCF_DEEP_OPTIM
+#define OCF_DEEP_OPTIM false
+#endif
+#ifndef OCF_DEEP_OTHER
+#define OCF_DEEP_OTHER false
+#endif
 #define OCF_NO_PROLOGUE                                                                            \
   using Pre = NoPre;                                                                             \
   template <class P>                                                                             \
@@ -53,6 +68,7 @@ __device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float
 
 // ---- split-K partial slab: out[split][m][n] --------------------------------------------
 struct EpiSlab {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_SLAB;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
@@ -102,6 +118,7 @@ __device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, in
 }
 
 struct EpiBiasAct {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   using Params = BiasActParams;
@@ -139,6 +156,7 @@ __device__ __forceinline__ void store_ct(void* out, int dtype, int64_t idx, floa
 }
 
 struct EpiGradAct {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 2 * GT_BN * 4;
   using Params = GradActParams;
@@ -176,6 +194,7 @@ struct EpiGradAct {
 
 // ---- raw gradient store (data-parallel path: all-reduce before the optimizer) ------------
 struct EpiGradStore {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
@@ -193,18 +212,71 @@ struct EpiGradStore {
 // thread streams 16 float4 chunks of the parameter / optimizer-state rows (512 contiguous bytes
 // per tile row, 4 chunks = 8-12 16-B loads in flight per lane), applies the Keras update and
 // writes them back.  This is the HBM-bound part of the step (16 B/param for Adagrad).
+#ifndef OCF_OPT_U
+#define OCF_OPT_U 4
+#endif
+#ifndef OCF_OPT_PRE
+#define OCF_OPT_PRE 0
+#endif
 struct EpiOptim {
-  OCF_NO_PROLOGUE
+  static constexpr bool DEEP_PIPE = OCF_DEEP_OPTIM;
   static constexpr int YS = GT_BN + 4;
   static constexpr int LDS_NEED = GT_BM * YS * 4;
+  static constexpr int CH = GT_BM * (GT_BN / 4) / GT_THREADS;   // 16 chunks of 4 per thread
+  static constexpr int U = OCF_OPT_U;                            // chunks in flight per thread
   struct Params {
     float* p;
     float* s1;
     float* s2;
     int64_t ld;
     OcfOptParams op;
+    void* shadow;      // compute-dtype copy of the updated weights (nullable), same layout as p
+    int shadow_dtype;
   };
-  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
+  // the parameter / slot values of the first chunk group do not depend on the product: with
+  // OCF_OPT_PRE they are loaded before the K-loop
+  struct Pre {
+#if OCF_OPT_PRE
+    float4 pv[U], av[U], bv[U];
+#endif
+  };
+  __device__ static int64_t chunk_off(const Params& p, int m0, int n0, int tid, int g, int u, int& ml, int& c4) {
+    const int ch = tid + (g + u) * GT_THREADS;
+    ml = ch >> 5;
+    c4 = (ch & 31) * 4;
+    return (int64_t)(m0 + ml) * p.ld + n0 + c4;
+  }
+  __device__ static void load_group(const Params& p, int m0, int n0, int tid, int g, float4 (&pv)[U], float4 (&av)[U],
+                                    float4 (&bv)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int ml, c4;
+      const int64_t off = chunk_off(p, m0, n0, tid, g, u, ml, c4);
+      pv[u] = *reinterpret_cast<const float4*>(p.p + off);
+      av[u] = p.s1 ? *reinterpret_cast<const float4*>(p.s1 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bv[u] = p.s2 ? *reinterpret_cast<const float4*>(p.s2 + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ static Pre prologue(const Params& p, int, int, int m0, int n0, int tid, const GemmShape&) {
+    Pre q;
+#if OCF_OPT_PRE
+    load_group(p, m0, n0, tid, 0, q.pv, q.av, q.bv);
+#endif
+    return q;
+  }
+  __device__ static void store_shadow(const Params& p, int64_t off, const float4& v) {
+    uint2 u;
+    if (p.shadow_dtype == OCF_F16) {
+      _Float16 h[4] = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+      __builtin_memcpy(&u, h, 8);
+    } else {
+      __bf16 h[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+      __builtin_memcpy(&u, h, 8);
+    }
+    *reinterpret_cast<uint2*>(reinterpret_cast<char*>(p.shadow) + off * 2) = u;
+  }
+  __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&,
+                               const Pre& q) {
     float* Y = reinterpret_cast<float*>(c.lds);
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
@@ -215,21 +287,26 @@ struct EpiOptim {
           Y[(c.wm + acc_row(bi, r, c.lane)) * YS + c.wn + acc_col(bj, c.lane)] = acc[bi][bj][r];
     __syncthreads();
     const OcfOptParams o = p.op;
-    constexpr int CH = GT_BM * (GT_BN / 4) / GT_THREADS;   // 16 chunks of 4 per thread
-    constexpr int U = 4;
+    const __amdgpu_buffer_rsrc_t rp = wt_rsrc(p.p), r1 = wt_rsrc(p.s1), r2 = wt_rsrc(p.s2);
 #pragma unroll 1
     for (int g = 0; g < CH; g += U) {
       float4 pv[U], av[U], bv[U], gv[U];
       int64_t off[U];
+#if OCF_OPT_PRE
+      if (g == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) { pv[u] = q.pv[u]; av[u] = q.av[u]; bv[u] = q.bv[u]; }
+      } else {
+        load_group(p, c.m0, c.n0, c.tid, g, pv, av, bv);
+      }
+#else
+      load_group(p, c.m0, c.n0, c.tid, g, pv, av, bv);
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int ch = c.tid + (g + u) * GT_THREADS;
-        const int ml = ch >> 5, c4 = (ch & 31) * 4;
-        off[u] = (int64_t)(c.m0 + ml) * p.ld + c.n0 + c4;
+        int ml, c4;
+        off[u] = chunk_off(p, c.m0, c.n0, c.tid, g, u, ml, c4);
         gv[u] = *reinterpret_cast<const float4*>(Y + ml * YS + c4);
-        pv[u] = *reinterpret_cast<const float4*>(p.p + off[u]);
-        av[u] = p.s1 ? *reinterpret_cast<const float4*>(p.s1 + off[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        bv[u] = p.s2 ? *reinterpret_cast<const float4*>(p.s2 + off[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -237,9 +314,10 @@ struct EpiOptim {
         opt_update(o, gv[u].y * o.gscale, pv[u].y, av[u].y, bv[u].y);
         opt_update(o, gv[u].z * o.gscale, pv[u].z, av[u].z, bv[u].z);
         opt_update(o, gv[u].w * o.gscale, pv[u].w, av[u].w, bv[u].w);
-        *reinterpret_cast<float4*>(p.p + off[u]) = pv[u];
-        if (p.s1) *reinterpret_cast<float4*>(p.s1 + off[u]) = av[u];
-        if (p.s2) *reinterpret_cast<float4*>(p.s2 + off[u]) = bv[u];
+        st_wt16(rp, p.p, (uint32_t)(off[u] * 4), pv[u]);
+        if (p.shadow) store_shadow(p, off[u], pv[u]);
+        if (p.s1) st_wt16(r1, p.s1, (uint32_t)(off[u] * 4), av[u]);
+        if (p.s2) st_wt16(r2, p.s2, (uint32_t)(off[u] * 4), bv[u]);
       }
     }
   }
@@ -247,6 +325,7 @@ struct EpiOptim {
 
 // ---- predict: y = mask * (acc + b) (model.py:82-86) -------------------------------------
 struct EpiPredict {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
@@ -277,9 +356,10 @@ struct EpiPredict {
 // GEMMs, its column sums give the output-bias gradient, and SSE / SAE / count_nonzero(T+yhat)
 // / per-row SSE feed the loss and the train.py metrics.
 struct EpiMaskedMSE {
+  static constexpr bool DEEP_PIPE = OCF_DEEP_MSE;
   static constexpr int YS = GT_BN + 4;   // LDS row stride (floats) of the staged tile
   static constexpr int NPRE = 2;         // bucket entries per thread loaded in the prologue
-  static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 2 * GT_BN * 4 + 3 * 4 * 4;
+  static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 4 * GT_BN * 4 + 3 * 4 * 4;
   struct Params {
     const float* bias;        // output bias [N]
     // bucket target mode (bk_ptr != nullptr): entries bucketed by 128-column tile
@@ -376,8 +456,8 @@ struct EpiMaskedMSE {
     float* Y = reinterpret_cast<float*>(c.lds);
     uint32_t* bits = reinterpret_cast<uint32_t*>(c.lds + GT_BM * YS * 4);
     float* rsse = reinterpret_cast<float*>(c.lds + GT_BM * YS * 4 + GT_BM * 16);
-    float* colp = rsse + GT_BM;          // [2][GT_BN]
-    float* red = colp + 2 * GT_BN;       // [3][4]
+    float* colp = rsse + GT_BM;          // [4 waves][GT_BN]
+    float* red = colp + 4 * GT_BN;       // [3][4]
     // 1. stage y = acc + b
 #pragma unroll
     for (int bj = 0; bj < 2; ++bj) {
@@ -431,48 +511,55 @@ struct EpiMaskedMSE {
       atomicAdd(&rsse[ml], rs);   // exactly two addends onto 0: order-independent
     }
     __syncthreads();
-    // 3. dense delta tile (zeros where no target) -> compute dtype, 8 columns per chunk
+    // 3. dense delta tile (zeros where no target) -> compute dtype, 8 columns per chunk.  A thread
+    //    keeps one 8-column group (tid % 16) over rows tid/16 + 16k, so it also accumulates the
+    //    output-bias gradient partial of those 8 columns; lanes 16 apart then 4 waves combine
+    //    in a fixed order.
     if (p.d_out) {
+      float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const int c8 = (c.tid & 15) * 8;
+      const __amdgpu_buffer_rsrc_t rd = wt_rsrc(p.d_out);
 #pragma unroll 2
-      for (int ch = c.tid; ch < GT_BM * (GT_BN / 8); ch += GT_THREADS) {
-        int ml = ch / (GT_BN / 8), c8 = (ch % (GT_BN / 8)) * 8;
+      for (int ml = c.tid >> 4; ml < GT_BM; ml += GT_THREADS / 16) {
         uint32_t w = bits[ml * 4 + (c8 >> 5)] >> (c8 & 31);
         const float4 y0 = *reinterpret_cast<const float4*>(Y + ml * YS + c8);
         const float4 y1 = *reinterpret_cast<const float4*>(Y + ml * YS + c8 + 4);
         float v[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = ((w >> j) & 1u) ? v[j] : 0.f;
+        for (int j = 0; j < 8; ++j) {
+          v[j] = ((w >> j) & 1u) ? v[j] : 0.f;
+          cs[j] += v[j];
+        }
         int64_t off = (int64_t)(c.m0 + ml) * p.ld_d + c.n0 + c8;
         if (p.d_dtype == OCF_F32) {
-          float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.d_out) + off);
-          o[0] = make_float4(v[0], v[1], v[2], v[3]);
-          o[1] = make_float4(v[4], v[5], v[6], v[7]);
+          st_wt16(rd, p.d_out, (uint32_t)(off * 4), make_float4(v[0], v[1], v[2], v[3]));
+          st_wt16(rd, p.d_out, (uint32_t)(off * 4 + 16), make_float4(v[4], v[5], v[6], v[7]));
         } else if (p.d_dtype == OCF_F16) {
           _Float16 h[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
           uint4 u; __builtin_memcpy(&u, h, 16);
-          *reinterpret_cast<uint4*>(reinterpret_cast<_Float16*>(p.d_out) + off) = u;
+          st_wt16(rd, p.d_out, (uint32_t)(off * 2), u);
         } else {
           __bf16 h[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = (__bf16)v[j];
           uint4 u; __builtin_memcpy(&u, h, 16);
-          *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(p.d_out) + off) = u;
+          st_wt16(rd, p.d_out, (uint32_t)(off * 2), u);
         }
       }
-    }
-    // 4. output-bias gradient column partials: 2 threads per column, 64 rows each, fixed order
-    if (p.db_part) {
-      const int nl = c.tid & (GT_BN - 1), half = c.tid >> 7;
-      float s0 = 0.f, s1 = 0.f;
-#pragma unroll 8
-      for (int ml = half * 64; ml < half * 64 + 64; ml += 2) {
-        uint32_t w0 = bits[ml * 4 + (nl >> 5)], w1 = bits[(ml + 1) * 4 + (nl >> 5)];
-        s0 += ((w0 >> (nl & 31)) & 1u) ? Y[ml * YS + nl] : 0.f;
-        s1 += ((w1 >> (nl & 31)) & 1u) ? Y[(ml + 1) * YS + nl] : 0.f;
+      if (p.db_part) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          cs[j] += __shfl_xor(cs[j], 16);
+          cs[j] += __shfl_xor(cs[j], 32);
+        }
+        if (c.lane < 16) {
+          const int wave = c.tid >> 6;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) colp[wave * GT_BN + c8 + j] = cs[j];
+        }
       }
-      colp[half * GT_BN + nl] = s0 + s1;
     }
     // 5. loss / metric partials: wave butterflies, then 4 wave partials in fixed order
 #pragma unroll
@@ -484,8 +571,9 @@ struct EpiMaskedMSE {
     const int wave = c.tid >> 6;
     if (c.lane == 0) { red[wave] = sse; red[4 + wave] = sae; red[8 + wave] = cnt; }
     __syncthreads();
-    if (p.db_part && c.tid < GT_BN)
-      p.db_part[(int64_t)c.tile_m * p.ld_db + c.n0 + c.tid] = (colp[c.tid] + colp[GT_BN + c.tid]) * p.gscale;
+    if (p.d_out && p.db_part && c.tid < GT_BN)
+      p.db_part[(int64_t)c.tile_m * p.ld_db + c.n0 + c.tid] =
+          ((colp[c.tid] + colp[GT_BN + c.tid]) + (colp[2 * GT_BN + c.tid] + colp[3 * GT_BN + c.tid])) * p.gscale;
     const int gm = sh.M / GT_BM;
     if (c.tid == 0) {
       float* sp = p.stats_part + ((int64_t)c.tile_n * gm + c.tile_m) * 4;

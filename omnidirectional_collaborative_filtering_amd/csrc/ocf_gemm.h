@@ -37,7 +37,13 @@ template <typename CT, int R, bool COL> struct Img {
 };
 
 // ---------------------------------------------------------------------------------------
-// global -> register -> LDS staging of one operand tile (R rows of the M/N dim x BK)
+// global -> register -> LDS staging of one operand tile (R rows of the M/N dim x BK).
+// Loads are buffer loads: a wave-uniform descriptor at the tile origin (SGPRs), a 32-bit byte
+// offset per chunk fixed for the whole K-loop (VGPRs), and the K advance as the SGPR soffset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+
 template <typename GT, typename CT, int R, bool COL> struct Stager {
   static constexpr int BK = KInfo<CT>::BK;
   static constexpr int CHUNKS = R * BK / 8;  // 8 elements per chunk
@@ -45,26 +51,35 @@ template <typename GT, typename CT, int R, bool COL> struct Stager {
   static_assert(NCH * GT_THREADS == CHUNKS, "tile/threads mismatch");
   GT v[NCH][8];
 
-  // src points at element (rdim=0, k=0) of this tile; ld in elements
-  __device__ __forceinline__ void load(const GT* __restrict__ src, int64_t ld, int tid) {
+  // byte offset of this thread's chunk i from the tile origin at k = 0; ld in elements
+  __device__ __forceinline__ static uint32_t chunk_off(int64_t ld, int tid, int i) {
+    int c = tid + i * GT_THREADS;
+    int64_t e;
+    if (!COL) {  // [R][K] k-contiguous; chunk = 8 consecutive k of one row
+      int r = c / (BK / 8), kc = c % (BK / 8);
+      e = (int64_t)r * ld + kc * 8;
+    } else {  // [K][R] r-contiguous; chunk = 8 consecutive r of one k
+      int k = c / (R / 8), rc = c % (R / 8);
+      e = (int64_t)k * ld + rc * 8;
+    }
+    return (uint32_t)(e * (int64_t)sizeof(GT));
+  }
+  // byte advance of the tile origin per K-step
+  __device__ __forceinline__ static uint32_t step_bytes(int64_t ld) {
+    return (uint32_t)((COL ? (int64_t)BK * ld : (int64_t)BK) * (int64_t)sizeof(GT));
+  }
+
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      int c = tid + i * GT_THREADS;
-      const GT* p;
-      if (!COL) {  // [R][K] k-contiguous; chunk = 8 consecutive k of one row
-        int r = c / (BK / 8), kc = c % (BK / 8);
-        p = src + (int64_t)r * ld + kc * 8;
-      } else {  // [K][R] r-contiguous; chunk = 8 consecutive r of one k
-        int k = c / (R / 8), rc = c % (R / 8);
-        p = src + (int64_t)k * ld + rc * 8;
-      }
+      const uint32_t o = chunk_off(ld, tid, i);
       if constexpr (sizeof(GT) == 4) {
-        float4 a = *reinterpret_cast<const float4*>(p);
-        float4 b = *reinterpret_cast<const float4*>(p + 4);
-        v[i][0] = a.x; v[i][1] = a.y; v[i][2] = a.z; v[i][3] = a.w;
-        v[i][4] = b.x; v[i][5] = b.y; v[i][6] = b.z; v[i][7] = b.w;
+        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+        auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, soff, 0);
+        __builtin_memcpy(&v[i][0], &a, 16);
+        __builtin_memcpy(&v[i][4], &b, 16);
       } else {
-        uint4 a = *reinterpret_cast<const uint4*>(p);
+        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
         __builtin_memcpy(&v[i][0], &a, 16);
       }
     }
@@ -216,16 +231,12 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
 
   const AGT* Ag = reinterpret_cast<const AGT*>(sh.A);
   const BGT* Bg = reinterpret_cast<const BGT*>(sh.B);
-  // tile origin pointers; advance per K-step
-  auto a_ptr = [&](int k) -> const AGT* {
-    return ACOL ? Ag + (int64_t)k * sh.lda + m0 : Ag + (int64_t)m0 * sh.lda + k;
-  };
-  auto b_ptr = [&](int k) -> const BGT* {
-    return BCOL ? Bg + (int64_t)k * sh.ldb + n0 : Bg + (int64_t)n0 * sh.ldb + k;
-  };
+  // buffer descriptors at the tile origins (k = k_begin); K-steps advance through soffset
+  const __amdgpu_buffer_rsrc_t ra =
+      tile_rsrc(ACOL ? Ag + (int64_t)k_begin * sh.lda + m0 : Ag + (int64_t)m0 * sh.lda + k_begin);
+  const __amdgpu_buffer_rsrc_t rb =
+      tile_rsrc(BCOL ? Bg + (int64_t)k_begin * sh.ldb + n0 : Bg + (int64_t)n0 * sh.ldb + k_begin);
 
-  Stager<AGT, CT, GT_BM, ACOL> sa;
-  Stager<BGT, CT, GT_BN, BCOL> sb;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   // epilogue inputs that do not depend on the product (e.g. target buckets) are loaded here, so
   // their latency hides under the K-loop
@@ -239,21 +250,8 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  if (nk > 0) {
-    sa.load(a_ptr(k_begin), sh.lda, tid);
-    sb.load(b_ptr(k_begin), sh.ldb, tid);
-    sa.store(lds, tid);
-    sb.store(lds + Cfg::ImgA::BYTES, tid);
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* bufA = lds + (kt & 1) * Cfg::BUF;
+  auto compute = [&](const char* bufA) {
     const char* bufB = bufA + Cfg::ImgA::BYTES;
-    const bool more = kt + 1 < nk;
-    if (more) {
-      sa.load(a_ptr(k_begin + (kt + 1) * BK), sh.lda, tid);
-      sb.load(b_ptr(k_begin + (kt + 1) * BK), sh.ldb, tid);
-    }
     if constexpr (sizeof(CT) == 2) {
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
@@ -286,12 +284,95 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
           for (int j = 0; j < 2; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      char* nb = lds + ((kt + 1) & 1) * Cfg::BUF;
-      sa.store(nb, tid);
-      sb.store(nb + Cfg::ImgA::BYTES, tid);
+  };
+  char* buf0 = lds;
+  char* buf1 = lds + Cfg::BUF;
+
+  // Two K-steps of operand loads in flight (two register sets used in turn, the loop unrolled by
+  // two so neither set is ever copied and every wait the compiler inserts covers exactly the set
+  // about to be written to LDS); only for 16-bit operands, where two sets fit the register budget
+  // of two workgroups per CU.
+  constexpr bool DEEP = Epi::DEEP_PIPE && sizeof(CT) == 2 && sizeof(AGT) == 2 && sizeof(BGT) == 2;
+  if constexpr (DEEP) {
+    Stager<AGT, CT, GT_BM, ACOL> sa0, sa1;
+    Stager<BGT, CT, GT_BN, BCOL> sb0, sb1;
+    // the scheduling barrier keeps the compiler from sinking a set's loads below the other set's
+    // LDS writes (which would drain the older set before the younger one is issued)
+    const uint32_t sta = decltype(sa0)::step_bytes(sh.lda), stb = decltype(sb0)::step_bytes(sh.ldb);
+    auto ld0 = [&](int kt) {
+      sa0.load(ra, sh.lda, kt * sta, tid);
+      sb0.load(rb, sh.ldb, kt * stb, tid);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto ld1 = [&](int kt) {
+      sa1.load(ra, sh.lda, kt * sta, tid);
+      sb1.load(rb, sh.ldb, kt * stb, tid);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto st0 = [&](char* b) { sa0.store(b, tid); sb0.store(b + Cfg::ImgA::BYTES, tid); };
+    auto st1 = [&](char* b) { sa1.store(b, tid); sb1.store(b + Cfg::ImgA::BYTES, tid); };
+    if (nk > 0) {
+      ld0(0);
+      if (nk > 1) ld1(1);
+      st0(buf0);
+      __syncthreads();
+      int kt = 0;
+      // steady state: buf0 holds step kt, set 1 carries step kt+1
+      for (; kt + 3 < nk; kt += 2) {
+        ld0(kt + 2);
+        compute(buf0);
+        st1(buf1);
+        __syncthreads();
+        ld1(kt + 3);
+        compute(buf1);
+        st0(buf0);
+        __syncthreads();
+      }
+      const int rem = nk - kt;   // 1, 2 or 3 steps left
+      if (rem == 3) {
+        ld0(kt + 2);
+        compute(buf0);
+        st1(buf1);
+        __syncthreads();
+        compute(buf1);
+        st0(buf0);
+        __syncthreads();
+        compute(buf0);
+      } else if (rem == 2) {
+        compute(buf0);
+        st1(buf1);
+        __syncthreads();
+        compute(buf1);
+      } else {
+        compute(buf0);
+      }
+      __syncthreads();
     }
-    __syncthreads();
+  } else {
+    Stager<AGT, CT, GT_BM, ACOL> sa;
+    Stager<BGT, CT, GT_BN, BCOL> sb;
+    const uint32_t sta = decltype(sa)::step_bytes(sh.lda), stb = decltype(sb)::step_bytes(sh.ldb);
+    if (nk > 0) {
+      sa.load(ra, sh.lda, 0, tid);
+      sb.load(rb, sh.ldb, 0, tid);
+      sa.store(buf0, tid);
+      sb.store(buf0 + Cfg::ImgA::BYTES, tid);
+      __syncthreads();
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) {
+        sa.load(ra, sh.lda, (kt + 1) * sta, tid);
+        sb.load(rb, sh.ldb, (kt + 1) * stb, tid);
+      }
+      compute((kt & 1) ? buf1 : buf0);
+      if (more) {
+        char* nb = ((kt + 1) & 1) ? buf1 : buf0;
+        sa.store(nb, tid);
+        sb.store(nb + Cfg::ImgA::BYTES, tid);
+      }
+      __syncthreads();
+    }
   }
 
   TileCtx c;

@@ -1,6 +1,7 @@
 // ocf_gemm: dispatch of the MFMA GEMM template to the layout / dtype / epilogue combinations the
 // autoencoder step uses ("GEMM inventory").
 #include <algorithm>
+#include <type_traits>
 
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
@@ -34,32 +35,29 @@ BiasActParams bias_act_params(const OcfGemmArgs& g) {
   return p;
 }
 
-template <typename CT, bool ACOL, bool BCOL>
-void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
-  // weights stream in as fp32 (converted while staging); activations arrive in the compute dtype
-  const bool weight_b = g.epi == OCF_EPI_SLAB || g.epi == OCF_EPI_BIAS_ACT || g.epi == OCF_EPI_PREDICT ||
-                        g.epi == OCF_EPI_MASKED_MSE || g.epi == OCF_EPI_GRAD_ACT;
-  if (weight_b)
-    OCF_CHECK(g.b_dtype == OCF_F32, "ocf_gemm: this epilogue takes fp32 B (master weights)");
-  else
-    OCF_CHECK(g.b_dtype == g.compute_dtype, "ocf_gemm: OPTIM/GRAD take B in the compute dtype");
+// WGT = element type the weight operand B is stored in: fp32 master weights (converted while
+// staging) or a compute-dtype shadow copy of them (SLAB / MASKED_MSE, half the bytes)
+template <typename CT, bool ACOL, bool BCOL, typename WGT>
+void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
   constexpr bool A_ROW = !ACOL;
+  constexpr bool FP32_W = std::is_same<WGT, float>::value;
+  constexpr bool ALL = FP32_W || std::is_same<CT, float>::value;   // every weight epilogue instantiated
   switch (g.epi) {
     case OCF_EPI_SLAB: {
       EpiSlab::Params p{g.out, g.ld_out, g.split_stride};
-      launch<CT, ACOL, BCOL, float, EpiSlab>(g, p, s);
+      launch<CT, ACOL, BCOL, WGT, EpiSlab>(g, p, s);
       return;
     }
     case OCF_EPI_BIAS_ACT:
-      if constexpr (A_ROW && BCOL) {
-        launch<CT, ACOL, BCOL, float, EpiBiasAct>(g, bias_act_params(g), s);
+      if constexpr (ALL && A_ROW && BCOL) {
+        launch<CT, ACOL, BCOL, WGT, EpiBiasAct>(g, bias_act_params(g), s);
         return;
       }
       break;
     case OCF_EPI_PREDICT:
-      if constexpr (A_ROW) {
+      if constexpr (ALL && A_ROW) {
         EpiPredict::Params p{g.bias, g.pmask, g.ld_pmask, g.out, g.ld_out, g.m_real, g.n_real};
-        launch<CT, ACOL, BCOL, float, EpiPredict>(g, p, s);
+        launch<CT, ACOL, BCOL, WGT, EpiPredict>(g, p, s);
         return;
       }
       break;
@@ -73,33 +71,37 @@ void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
         p.t_lidx = g.t_lidx; p.t_flag = g.t_flag; p.t_lboff = g.t_lboff; p.t_ntiles = g.t_ntiles; p.t_aux = g.t_aux;
         p.m_real = g.m_real;
         OCF_CHECK(g.stats_part, "ocf_gemm MASKED_MSE: stats_part required");
+        OCF_CHECK(!g.db_part || g.h_out, "ocf_gemm MASKED_MSE: db_part needs the delta output (h_out)");
+        OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm MASKED_MSE: delta block over 2 GiB");
         OCF_CHECK(g.bk_ptr || (g.t_rows && g.t_rp && g.t_tptr && g.t_col && g.t_val && g.t_lidx && g.t_flag &&
                                g.t_lboff && g.t_ntiles * GT_BN >= g.N),
                   "ocf_gemm MASKED_MSE: bucket or row-segment targets required");
-        launch<CT, ACOL, BCOL, float, EpiMaskedMSE>(g, p, s);
+        launch<CT, ACOL, BCOL, WGT, EpiMaskedMSE>(g, p, s);
         return;
       }
       break;
     case OCF_EPI_GRAD_ACT:
-      if constexpr (A_ROW && !BCOL) {
+      if constexpr (ALL && A_ROW && !BCOL) {
         GradActParams p;
         p.a = g.a_in; p.mask = g.mask_in; p.keep = g.keep; p.act = g.act; p.d_out = g.h_out; p.d_dtype = g.h_dtype;
         p.ld = g.ld_out; p.db_part = g.db_part; p.gscale = g.opt.gscale; p.m_real = g.m_real; p.n_real = g.n_real;
         OCF_CHECK(g.a_in && g.h_out, "ocf_gemm GRAD_ACT: a_in / h_out required");
-        launch<CT, ACOL, BCOL, float, EpiGradAct>(g, p, s);
+        launch<CT, ACOL, BCOL, WGT, EpiGradAct>(g, p, s);
         return;
       }
       break;
     case OCF_EPI_OPTIM:
-      if constexpr (BCOL) {
-        EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt};
+      if constexpr (!FP32_W || std::is_same<CT, float>::value) if constexpr (BCOL) {
+        EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt, g.p_shadow, g.compute_dtype};
         OCF_CHECK(g.p != nullptr, "ocf_gemm OPTIM: p required");
+        OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm OPTIM: parameter block over 2 GiB");
+        OCF_CHECK(!g.p_shadow || g.compute_dtype != OCF_F32, "ocf_gemm OPTIM: shadow weights need f16/bf16 compute");
         launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
         return;
       }
       break;
     case OCF_EPI_GRAD:
-      if constexpr (BCOL) {
+      if constexpr (!FP32_W || std::is_same<CT, float>::value) if constexpr (BCOL) {
         EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale};
         launch<CT, ACOL, BCOL, CT, EpiGradStore>(g, p, s);
         return;
@@ -109,8 +111,22 @@ void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
       break;
   }
   throw std::runtime_error("ocf_gemm: epilogue " + std::to_string(g.epi) + " not instantiated for layout a_col=" +
-                           std::to_string(ACOL) + " b_col=" + std::to_string(BCOL));
+                           std::to_string(ACOL) + " b_col=" + std::to_string(BCOL) + " b_dtype=" +
+                           std::to_string(g.b_dtype));
 }
+
+template <typename CT, bool ACOL, bool BCOL>
+void dispatch_layout(const OcfGemmArgs& g, hipStream_t s) {
+  // weight epilogues: B = fp32 master weights or their compute-dtype shadow; OPTIM/GRAD: B is an
+  // activation in the compute dtype
+  const bool weight_b = g.epi == OCF_EPI_SLAB || g.epi == OCF_EPI_BIAS_ACT || g.epi == OCF_EPI_PREDICT ||
+                        g.epi == OCF_EPI_MASKED_MSE || g.epi == OCF_EPI_GRAD_ACT;
+  if (weight_b && g.b_dtype == OCF_F32) return dispatch_epi<CT, ACOL, BCOL, float>(g, s);
+  OCF_CHECK(g.b_dtype == g.compute_dtype, weight_b ? "ocf_gemm: weight B must be fp32 or the compute dtype"
+                                                   : "ocf_gemm: OPTIM/GRAD take B in the compute dtype");
+  dispatch_epi<CT, ACOL, BCOL, CT>(g, s);
+}
+
 
 template <typename CT>
 void dispatch(const OcfGemmArgs& g, hipStream_t s) {

@@ -99,6 +99,24 @@ class Engine:
         self.W = [torch.zeros(i, o, **f) for i, o in zip(self.pad_dims[:-2], self.pad_dims[1:-1])]
         self.W.append(torch.zeros(self.pad_dims[-1], self.pad_dims[-2], **f))     # decoder, transposed
         self.b = [torch.zeros(o, **f) for o in self.pad_dims[1:]]
+        # half-width shadows of the two N-sized weights (f16/bf16 compute): the MFMA operand would be
+        # rounded to the compute dtype while staging anyway, so streaming a copy rounded once by the
+        # optimizer epilogue gives bit-identical products at half the bytes
+        self.Wsh = [None] * len(self.W)
+        if self.cdt != _lib.DT_F32:
+            for i in sorted({0, len(self.W) - 1}):
+                self.Wsh[i] = torch.zeros(self.W[i].shape, device=self.dev, dtype=self.tdt)
+
+    def _refresh_shadows(self):
+        for w, sh in zip(self.W, self.Wsh):
+            if sh is not None:
+                sh.copy_(w)
+
+    def _wop(self, i):
+        """(tensor, dtype code) of weight i as a GEMM operand: the shadow when there is one."""
+        if self.Wsh[i] is not None:
+            return self.Wsh[i], self.cdt
+        return self.W[i], _lib.DT_F32
 
     def _keras_view(self, i):
         """W_i as a padded (in, out) view (the decoder is stored transposed)."""
@@ -151,6 +169,7 @@ class Engine:
             kv.copy_(full)
             self.b[i].zero_()
             self.b[i][: self.real_dims[i + 1]] = bb
+        self._refresh_shadows()
 
     def set_optimizer(self, opt):
         self.opt = opt
@@ -357,7 +376,7 @@ class Engine:
         Hp0 = self.Hp[0]
         sstride = Bp * Hp0
         with self.phase("enc_gemm"):
-            self._gemm(self.xin, 0, self.pad_dims[0], self.W[0], _lib.DT_F32, 1, Hp0, Bp, Hp0, self.pad_dims[0],
+            self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
                        _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
         src, nsplit = self.slabs, self.splits0
         if self.comm is not None:
@@ -390,7 +409,7 @@ class Engine:
     def _gemm_mse(self, L, gscale, with_grad):
         tg = self.tseg if self.tseg is not None else dict(bk_ptr=self.bk_ptr, bk_rc=self.bk_rc, bk_t=self.bk_t,
                                                           bk_m=self.bk_m)
-        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 0, self.Hp[L - 1], self.Bp, self.Np,
+        self._gemm(self.h[L - 1], 0, self.Hp[L - 1], *self._wop(L), 0, self.Hp[L - 1], self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], m_real=self.B, **tg,
                    h_out=self.d_out if with_grad else None, h_dtype=self.cdt, ld_out=self.Np,
                    db_part=self.db_out_part if with_grad else None, ld_db=self.Np,
@@ -420,7 +439,7 @@ class Engine:
         HpL = self.Hp[L - 1]
         sstride = Bp * HpL
         with self.phase("dec_bwd_gemm"):
-            self._gemm(self.d_out, 0, self.Np, self.W[L], _lib.DT_F32, 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
+            self._gemm(self.d_out, 0, self.Np, *self._wop(L), 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
         db_last = self.db_h[L - 1]
         src, nsplit = self.slabs, self.splitsL
@@ -472,7 +491,7 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o)
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i])
         else:
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
                        opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale))
@@ -486,6 +505,7 @@ class Engine:
             call("ocf_opt_step", ptr(self.W[i]), ptr(grads[2 * i]), ptr(sw[0]), ptr(sw[1]), self.W[i].numel(), op, s)
             ob = self.opt.step_params(scale, 0.0)
             call("ocf_opt_step", ptr(self.b[i]), ptr(grads[2 * i + 1]), ptr(sb[0]), ptr(sb[1]), self.b[i].numel(), ob, s)
+        self._refresh_shadows()
         self.opt.iterations += 1
 
     def grad_buffers(self):
