@@ -17,6 +17,7 @@ processed / max-over-ranks wall time of the K timed steps.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -52,6 +53,8 @@ def parse():
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="diagnostic: run rank 0 of a G-way feature-parallel job alone (collectives skipped, "
                          "numerics of a partial model); not a bench line")
+    ap.add_argument("--sparse-clear", type=int, default=0,
+                    help="clear the previous batch's layer-0 entries instead of a dense memset")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient all-reduce)")
@@ -135,6 +138,7 @@ def main():
     m.compile(optim(args.optimizer, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
     w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
     eng = om.engine
+    eng.sparse_clear = bool(args.sparse_clear)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)
@@ -151,22 +155,30 @@ def main():
             dp_train_step(eng, bucket, world)
         return int(nnz_of[bi])
 
+    # warm-up (untimed): every phase bracketed by HIP events -> per-phase breakdown and the dominant
+    # kernel.  The timed region then brackets only that kernel, so the timers cost ~2 events/step.
+    eng.enable_timers(bool(args.phase_timers))
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    phases = eng.phase_times_ms(skip=1 if args.warmup > 1 else 0)
+    cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
+    dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
     if world > 1:
         torch.distributed.barrier()
-    eng.enable_timers(bool(args.phase_timers))
+    eng.enable_timers(dom is not None, only=[dom] if dom else None)
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     nnz = 0
     for i in range(args.steps):
         nnz += step(args.warmup + i)
+    t_issued = time.perf_counter()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t_start
-    phases = eng.phase_times_ms()
+    host_ms = (t_issued - t_start) / args.steps * 1e3    # host time to issue one step (diagnostic)
+    dom_timed = eng.phase_times_ms().get(dom) if dom else None
     eng.timers = None
     tot = torch.tensor([elapsed, float(nnz)], device=dev, dtype=torch.float64)
     if world > 1:
@@ -193,10 +205,6 @@ def main():
     Nl = data.num_cols
     P = Nl * H
     opt_b = OPT_STATE_BYTES[args.optimizer]
-    dom = None
-    if phases:
-        cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
-        dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
     # weight operands: the compute-dtype shadow (2 B) written by the optimizer epilogue, fp32 in fp32 mode
     w_b = 4 if args.dtype == "float32" else 2
     sh_b = 0 if args.dtype == "float32" else 2
@@ -210,20 +218,22 @@ def main():
         "dec_bwd_gemm": P * w_b + Bg * Nl * 2,
     }
     roof = None
-    if dom is not None:
+    if dom is not None and dom_timed:
         if world > 1 and not fp and dom in ("dW_in", "dW_out"):
             alg[dom] = P * 4 + B * N * 2 + B * H * 2     # gradient store instead of the fused update
-        ms = phases[dom]["mean_ms"]
+        ms = dom_timed["mean_ms"]
         ach = alg[dom] / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
                 "kernel_mean_us": round(ms * 1e3, 1), "alg_bytes_per_launch": int(alg[dom])}
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
+        # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
+        pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
+        if pmcs and world == 1:
+            with open(pmcs[-1]) as f:
                 tr = json.load(f).get(dom)
             if tr:
-                roof["traffic"] = tr
+                roof["traffic"] = tr["hbm_bytes"]
+                roof["traffic_source"] = os.path.relpath(pmcs[-1], ROOT)
     ms_step = elapsed / args.steps * 1e3
     step_flops = 10.0 * Bg * Nl * H
     step_bytes = P * 2 * (opt_b + 4) + 2 * (3 * Nl * H) + 8 * (nnz / args.steps / max(world, 1))
@@ -246,7 +256,10 @@ def main():
                                                             step_flops / (MFMA_F16_PEAK_TFS * 1e12))
                                                         / (ms_step * 1e-3), 4)},
         "phases_ms": {k: round(v["mean_ms"], 4) for k, v in phases.items()},
+        "phases_from": "warm-up steps 2..%d, every phase bracketed by HIP events (timed region: only %s)"
+                       % (args.warmup, dom),
         "setup_s": round(setup_s, 1),
+        "host_issue_ms_per_step": round(host_ms, 4),
     }
     if world == 1 and args.cpu_baseline:
         rows_b = [gen.rows_host[bi] for bi in batches[: args.cpu_steps]]

@@ -93,9 +93,17 @@ typedef struct OcfScatterArgs {
   const int64_t* lboff1; const int64_t* lboff2;
   int64_t E1, E2;
   uint8_t* tflag1; uint8_t* tflag2;
+  /* 1: xin is already zero (the caller cleared the previous batch with ocf_scatter_clear), so the
+   * [B_pad][xin_ld] memset is skipped */
+  int xin_clean;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
+
+/* Zero the xin entries a previous ocf_scatter_batch call with the same arguments wrote (every
+ * block of every source entry's column): a sparse clear replacing the dense memset of the next
+ * batch.  Only xin is touched. */
+int ocf_scatter_clear(const OcfScatterArgs* args, void* stream);
 
 /* Target buckets from dense target / output-mask arrays (Model.train_on_batch on user arrays). */
 int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,

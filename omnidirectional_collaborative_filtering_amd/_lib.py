@@ -40,6 +40,7 @@ class OcfScatterArgs(ctypes.Structure):
         ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
         ("pos1", P),
         ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
+        ("xin_clean", I32),
     ]
 
 
@@ -65,6 +66,7 @@ class OcfGemmArgs(ctypes.Structure):
 # every symbol include/ocf.h declares, with its ctypes signature
 SIGNATURES = {
     "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
+    "ocf_scatter_clear": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
     "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P]),
     "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),

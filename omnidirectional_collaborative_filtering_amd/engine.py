@@ -203,6 +203,13 @@ class Engine:
         self.bk_cap = 0
         self._grow_buckets(1 << 16)
         self.tflag = torch.zeros(1 << 16, device=d, dtype=torch.uint8)   # live-target flag per batch entry
+        # xin is zeroed once; afterwards each generator batch clears only the previous batch's entries
+        self._xin_clean = True
+        self._xin_prev = None       # (OcfScatterArgs copy, owner keeping its device buffers alive)
+        # sparse clear (ocf_scatter_clear) instead of the dense memset: measured ~4% SLOWER per step on
+        # ML-20M -- the memset leaves xin resident in the Infinity Cache, so the encoder GEMM reads it
+        # on-die; after a sparse clear it streams from HBM.  Off by default.
+        self.sparse_clear = False
         self.tseg = None            # row-segment target descriptor of the loaded batch (None: buckets)
         gm = Bp // TILE
         self.stats_part = torch.zeros(self.n_tiles * gm * 4, device=d, dtype=torch.float32)
@@ -213,27 +220,37 @@ class Engine:
         self.n_stats = 0
         self.dense_in = None
         self.timers = None          # {phase: [(start_event, end_event), ...]} when profiling
+        self.timer_only = None
+        # side stream for the small kernels that do not feed the next GEMM (stats, bias updates, the
+        # delta split-K reduction): they overlap the weight-gradient GEMMs instead of adding kernel
+        # boundaries to the main chain.  Joined at the end of every step.
+        self.side = torch.cuda.Stream(device=d) if d.type == "cuda" else None
+        self._side_busy = False
         if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
             self.hpre = torch.zeros(Bp, self.Hp[0], device=d, dtype=torch.float32)
             self.dhpre = torch.zeros(Bp, self.Hp[-1], device=d, dtype=torch.float32)
             self.zero_bias = torch.zeros(max(self.Hp), device=d, dtype=torch.float32)
 
     # ---------------------------------------------------------------- phase timing (bench.py)
-    def enable_timers(self, on=True):
+    def enable_timers(self, on=True, only=None):
+        """HIP-event timing of phases (every phase, or the names in `only`)."""
         self.timers = {} if on else None
+        self.timer_only = set(only) if only else None
 
     class _Phase:
         def __init__(self, eng, name):
             self.eng, self.name = eng, name
 
         def __enter__(self):
-            if self.eng.timers is not None:
+            e = self.eng
+            self.on = e.timers is not None and (e.timer_only is None or self.name in e.timer_only)
+            if self.on:
                 self.s = torch.cuda.Event(enable_timing=True)
                 self.s.record()
             return self
 
         def __exit__(self, *exc):
-            if self.eng.timers is not None:
+            if self.on:
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 self.eng.timers.setdefault(self.name, []).append((self.s, e))
@@ -242,11 +259,28 @@ class Engine:
     def phase(self, name):
         return Engine._Phase(self, name)
 
-    def phase_times_ms(self):
-        """mean / total milliseconds per phase (call after synchronize)."""
+    # ---------------------------------------------------------------- side stream
+    def _fork(self):
+        """side stream waits for everything issued so far on the current stream"""
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        self._side_busy = True
+
+    def _join(self):
+        """current stream waits for the side stream"""
+        if self._side_busy:
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            torch.cuda.current_stream().wait_event(ev)
+            self._side_busy = False
+
+    def phase_times_ms(self, skip=0):
+        """mean / total milliseconds per phase (call after synchronize), dropping the first `skip`
+        launches of each phase."""
         out = {}
         for k, v in (self.timers or {}).items():
-            ts = [a.elapsed_time(b) for a, b in v]
+            ts = [a.elapsed_time(b) for a, b in v[skip:]] or [a.elapsed_time(b) for a, b in v]
             out[k] = {"mean_ms": float(np.mean(ts)), "total_ms": float(np.sum(ts)), "n": len(ts)}
         return out
 
@@ -298,7 +332,7 @@ class Engine:
         a.s0 = a.s1 = 1.0
         return a
 
-    def load_batch(self, a, targets):
+    def load_batch(self, a, targets, owner=None):
         """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller).
 
         ``targets`` (BatchGenerator.targets) names the target CSR's tile index: the scatter marks
@@ -315,7 +349,13 @@ class Engine:
         seg["t_flag"] = self.tflag
         self.tseg = seg
         with self.phase("scatter"):
+            if self._xin_prev is not None:
+                call("ocf_scatter_clear", self._xin_prev[0], cur_stream())
+                self._xin_clean = True
+            a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
+        self._xin_prev = (type(a).from_buffer_copy(a), owner) if self.sparse_clear else None
+        self._xin_clean = False
 
     def load_dense(self, inputs, out_mask, targets):
         """API path: dense arrays (torch/numpy) in the model.py input order."""
@@ -337,6 +377,7 @@ class Engine:
         s = cur_stream()
         call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
              self.Bp, s)
+        self._xin_prev, self._xin_clean = None, False      # xin written densely
         self._grow_buckets(B * N)
         self.tseg = None
         call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
@@ -402,8 +443,15 @@ class Engine:
         with self.phase("dec_gemm_mse"):
             self._gemm_mse(L, gscale, with_grad)
         self._grow_stats(self.n_stats + 1)
-        call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
-             self.n_tiles, self.Bp, ptr(self.stats_hist[self.n_stats]), cur_stream())
+        dst = self.stats_hist[self.n_stats]
+        if self.side is not None:
+            self._fork()
+            with torch.cuda.stream(self.side):
+                call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE),
+                     ptr(self.row_sse_part), self.n_tiles, self.Bp, ptr(dst), cur_stream())
+        else:
+            call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
+                 self.n_tiles, self.Bp, ptr(dst), cur_stream())
         self.n_stats += 1
 
     def _gemm_mse(self, L, gscale, with_grad):
@@ -443,6 +491,23 @@ class Engine:
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
         db_last = self.db_h[L - 1]
         src, nsplit = self.slabs, self.splitsL
+        if fused and L == 1 and self.comm is None and self.side is not None:
+            # side stream: delta reduction + both bias updates, overlapping the output-layer GEMM
+            self._fork()
+            with torch.cuda.stream(self.side):
+                call("ocf_splitk_grad_act", ptr(src), nsplit, sstride, Bp, HpL, HpL, ptr(self.a[0]),
+                     ptr(self.mask[0]), self.keep, self.act, ptr(self.dh[0]), self.cdt, ptr(db_last[0]), gscale,
+                     self.B, self.H[0], cur_stream())
+                self._bias_update(1, self.db_out_part, Bp // TILE, self.Np, self.Np, grads_out, op)
+                self._bias_update(0, db_last, Bp // 4, self.Hp[0], self.Hp[0], grads_out, op)
+            with self.phase("dW_out"):
+                self._weight_update(1, self.d_out, self.Np, self.h[0], HpL, self.Np, HpL, gscale, grads_out, op)
+            self._join()
+            with self.phase("dW_in"):
+                self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0],
+                                    self.Hp[0], gscale, grads_out, op)
+            self.opt.iterations += 1
+            return
         if self.comm is not None:
             call("ocf_splitk_bias_act", ptr(self.slabs), self.splitsL, sstride, Bp, HpL, HpL, ptr(self.zero_bias),
                  _lib.ACT["linear"], 1.0, 0, 0, None, None, ptr(self.dhpre), None, self.cdt, Bp, HpL, s)
@@ -519,11 +584,13 @@ class Engine:
         self.forward(training=True)
         self.output_loss(with_grad=True)
         self.backward_update(grads_out)
+        self._join()
         self.step_count += 1
 
     def eval_step(self):
         self.forward(training=False)
         self.output_loss(with_grad=False)
+        self._join()
 
     def take_stats(self):
         """host copy of the per-step stats recorded since the last call: [steps, 4 + Bp]."""

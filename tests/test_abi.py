@@ -42,7 +42,7 @@ def test_library_exports_every_symbol():
 STRUCTS = {
     "OcfOptParams": (_lib.OcfOptParams, ["kind", "lr", "gscale"]),
     "OcfScatterArgs": (_lib.OcfScatterArgs, ["keep1", "s0", "seed", "mode", "rows2", "aux", "ld", "xin_dtype",
-                                             "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2"]),
+                                             "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean"]),
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
                                        "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part", "t_rows", "t_lboff", "t_ntiles",
                                        "t_aux", "p_shadow"]),
