@@ -55,6 +55,8 @@ def parse():
                          "numerics of a partial model); not a bench line")
     ap.add_argument("--sparse-clear", type=int, default=0,
                     help="clear the previous batch's layer-0 entries instead of a dense memset")
+    ap.add_argument("--nt-operands", type=int, default=0,
+                    help="non-temporal loads for GEMM operands at their last use in the step")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient all-reduce)")
@@ -139,6 +141,7 @@ def main():
     w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
     eng = om.engine
     eng.sparse_clear = bool(args.sparse_clear)
+    eng.nt_operands = bool(args.nt_operands)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)

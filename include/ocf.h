@@ -149,6 +149,9 @@ typedef struct OcfGemmArgs {
   /* OPTIM: also write the updated weights in the compute dtype (same layout as p, nullable), the
    * half-width shadow the next forward / backward GEMMs stream instead of the fp32 master copy */
   void* p_shadow;
+  /* 1: load operand A / B with the non-temporal cache policy (its last use in the step, so it
+   * should not displace reusable data from the Infinity Cache) */
+  int a_nt, b_nt;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

@@ -101,6 +101,33 @@ typedef unsigned int ocf_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
 }
+// 16-B store / load with an explicit cache policy (aux bits: 2 = nt, 16 = sc1; 0 = plain)
+template <int AUX, typename T16>
+__device__ __forceinline__ void st_pol16(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, const T16& v) {
+  static_assert(sizeof(T16) == 16, "16-byte store");
+  if constexpr (AUX == 0) {
+    (void)r;
+    *reinterpret_cast<T16*>(reinterpret_cast<char*>(base) + byte_off) = v;
+  } else {
+    (void)base;
+    ocf_u4 u;
+    __builtin_memcpy(&u, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, AUX);
+  }
+}
+template <int AUX>
+__device__ __forceinline__ float4 ld_pol16(__amdgpu_buffer_rsrc_t r, const void* base, uint32_t byte_off) {
+  if constexpr (AUX == 0) {
+    (void)r;
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + byte_off);
+  } else {
+    (void)base;
+    ocf_u4 u = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX);
+    float4 f;
+    __builtin_memcpy(&f, &u, 16);
+    return f;
+  }
+}
 template <typename T16>
 __device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, const T16& v) {
   static_assert(sizeof(T16) == 16, "16-byte store");

@@ -69,20 +69,26 @@ template <typename GT, typename CT, int R, bool COL> struct Stager {
     return (uint32_t)((COL ? (int64_t)BK * ld : (int64_t)BK) * (int64_t)sizeof(GT));
   }
 
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid) {
+  template <int AUX>
+  __device__ __forceinline__ void load_pol(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const uint32_t o = chunk_off(ld, tid, i);
       if constexpr (sizeof(GT) == 4) {
-        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
-        auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, soff, 0);
+        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, AUX);
+        auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, soff, AUX);
         __builtin_memcpy(&v[i][0], &a, 16);
         __builtin_memcpy(&v[i][4], &b, 16);
       } else {
-        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, 0);
+        auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, AUX);
         __builtin_memcpy(&v[i][0], &a, 16);
       }
     }
+  }
+  // nt: wave-uniform choice of the non-temporal cache policy (the operand's last use in the step)
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid, bool nt) {
+    if (nt) load_pol<2>(rs, ld, soff, tid);
+    else load_pol<0>(rs, ld, soff, tid);
   }
 
   __device__ __forceinline__ void store(char* img, int tid) const {
@@ -188,6 +194,7 @@ struct GemmShape {
   int64_t lda, ldb;
   int M, N, K;
   int kchunk;    // K elements per split (multiple of BK)
+  int a_nt, b_nt;  // non-temporal operand loads
   int order;     // 0: n-fastest tile order, 1: m-fastest (XCD-local neighbours)
 };
 
@@ -300,13 +307,13 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     // LDS writes (which would drain the older set before the younger one is issued)
     const uint32_t sta = decltype(sa0)::step_bytes(sh.lda), stb = decltype(sb0)::step_bytes(sh.ldb);
     auto ld0 = [&](int kt) {
-      sa0.load(ra, sh.lda, kt * sta, tid);
-      sb0.load(rb, sh.ldb, kt * stb, tid);
+      sa0.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
+      sb0.load(rb, sh.ldb, kt * stb, tid, sh.b_nt);
       __builtin_amdgcn_sched_barrier(0);
     };
     auto ld1 = [&](int kt) {
-      sa1.load(ra, sh.lda, kt * sta, tid);
-      sb1.load(rb, sh.ldb, kt * stb, tid);
+      sa1.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
+      sb1.load(rb, sh.ldb, kt * stb, tid, sh.b_nt);
       __builtin_amdgcn_sched_barrier(0);
     };
     auto st0 = [&](char* b) { sa0.store(b, tid); sb0.store(b + Cfg::ImgA::BYTES, tid); };
@@ -353,8 +360,8 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     Stager<BGT, CT, GT_BN, BCOL> sb;
     const uint32_t sta = decltype(sa)::step_bytes(sh.lda), stb = decltype(sb)::step_bytes(sh.ldb);
     if (nk > 0) {
-      sa.load(ra, sh.lda, 0, tid);
-      sb.load(rb, sh.ldb, 0, tid);
+      sa.load(ra, sh.lda, 0, tid, sh.a_nt);
+      sb.load(rb, sh.ldb, 0, tid, sh.b_nt);
       sa.store(buf0, tid);
       sb.store(buf0 + Cfg::ImgA::BYTES, tid);
       __syncthreads();
@@ -362,8 +369,8 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk;
       if (more) {
-        sa.load(ra, sh.lda, (kt + 1) * sta, tid);
-        sb.load(rb, sh.ldb, (kt + 1) * stb, tid);
+        sa.load(ra, sh.lda, (kt + 1) * sta, tid, sh.a_nt);
+        sb.load(rb, sh.ldb, (kt + 1) * stb, tid, sh.b_nt);
       }
       compute((kt & 1) ? buf1 : buf0);
       if (more) {

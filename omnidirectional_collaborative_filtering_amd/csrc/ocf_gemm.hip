@@ -18,6 +18,7 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   GemmShape sh;
   sh.A = g.A; sh.B = g.B; sh.lda = g.lda; sh.ldb = g.ldb;
   sh.M = g.M; sh.N = g.N; sh.K = g.K; sh.order = g.order;
+  sh.a_nt = g.a_nt != 0; sh.b_nt = g.b_nt != 0;
   const int splits = std::max(1, g.splits);
   const int ksteps = g.K / Cfg::BK;
   const int per = (ksteps + splits - 1) / splits;

@@ -210,6 +210,8 @@ class Engine:
         # ML-20M -- the memset leaves xin resident in the Infinity Cache, so the encoder GEMM reads it
         # on-die; after a sparse clear it streams from HBM.  Off by default.
         self.sparse_clear = False
+        # non-temporal loads for operands at their last use in the step (A/B switch)
+        self.nt_operands = False   # measured neutral-to-worse: nt loads forfeit Infinity-Cache hits
         self.tseg = None            # row-segment target descriptor of the loaded batch (None: buckets)
         gm = Bp // TILE
         self.stats_part = torch.zeros(self.n_tiles * gm * 4, device=d, dtype=torch.float32)
@@ -418,7 +420,8 @@ class Engine:
         sstride = Bp * Hp0
         with self.phase("enc_gemm"):
             self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
-                       _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride)
+                       _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride,
+                       b_nt=int(self.nt_operands))
         src, nsplit = self.slabs, self.splits0
         if self.comm is not None:
             # partial pre-activation over this rank's columns -> sum over ranks -> activation
@@ -488,7 +491,8 @@ class Engine:
         sstride = Bp * HpL
         with self.phase("dec_bwd_gemm"):
             self._gemm(self.d_out, 0, self.Np, *self._wop(L), 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
-                       splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride)
+                       splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride,
+                       b_nt=int(self.nt_operands))
         db_last = self.db_h[L - 1]
         src, nsplit = self.slabs, self.splitsL
         if fused and L == 1 and self.comm is None and self.side is not None:
@@ -556,7 +560,7 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o, p_shadow=self.Wsh[i])
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i], a_nt=int(self.nt_operands and i in (0, len(self.W) - 1)))
         else:
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
                        opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale))
