@@ -152,6 +152,10 @@ typedef struct OcfGemmArgs {
   /* 1: load operand A / B with the non-temporal cache policy (its last use in the step, so it
    * should not displace reusable data from the Infinity Cache) */
   int a_nt, b_nt;
+  /* B is a 16-bit compute-dtype array stored 64x64-blocked (blocks of 64 rows x 64 columns, each
+   * 8 KB contiguous and row-major inside, blocks row-major; ldb = columns); OPTIM: write p_shadow in
+   * that layout */
+  int b_blocked, shadow_blocked;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

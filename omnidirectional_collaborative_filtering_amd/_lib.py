@@ -59,7 +59,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("bk_ptr", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("stats_part", P), ("row_sse_part", P),
         ("t_rows", P), ("t_rp", P), ("t_tptr", P), ("t_col", P), ("t_val", P), ("t_lidx", P), ("t_flag", P),
         ("t_lboff", P), ("t_ntiles", I32), ("t_aux", F32),
-        ("p_shadow", P), ("a_nt", I32), ("b_nt", I32),
+        ("p_shadow", P), ("a_nt", I32), ("b_nt", I32), ("b_blocked", I32), ("shadow_blocked", I32),
     ]
 
 

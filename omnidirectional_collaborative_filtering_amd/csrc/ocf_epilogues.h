@@ -240,8 +240,9 @@ struct EpiOptim {
     float* s2;
     int64_t ld;
     OcfOptParams op;
-    void* shadow;      // compute-dtype copy of the updated weights (nullable), same layout as p
+    void* shadow;      // compute-dtype copy of the updated weights (nullable)
     int shadow_dtype;
+    bool shadow_blocked;  // shadow in the 64x64-blocked layout (else the layout of p)
   };
   // the parameter / slot values of the first chunk group do not depend on the product: with
   // OCF_OPT_PRE they are loaded before the K-loop
@@ -275,7 +276,10 @@ struct EpiOptim {
 #endif
     return q;
   }
-  __device__ static void store_shadow(const Params& p, int64_t off, const float4& v) {
+  __device__ static void store_shadow(const Params& p, int row, int col, const float4& v) {
+    const int64_t off = p.shadow_blocked
+                            ? (((int64_t)(row >> 6) * (p.ld >> 6) + (col >> 6)) << 12) + (row & 63) * 64 + (col & 63)
+                            : (int64_t)row * p.ld + col;
     uint2 u;
     if (p.shadow_dtype == OCF_F16) {
       _Float16 h[4] = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
@@ -303,6 +307,7 @@ struct EpiOptim {
     for (int g = 0; g < CH; g += U) {
       float4 pv[U], av[U], bv[U], gv[U];
       int64_t off[U];
+      int rw[U], cl[U];
 #if OCF_OPT_PRE
       if (g == 0) {
 #pragma unroll
@@ -317,6 +322,8 @@ struct EpiOptim {
       for (int u = 0; u < U; ++u) {
         int ml, c4;
         off[u] = chunk_off(p, c.m0, c.n0, c.tid, g, u, ml, c4);
+        rw[u] = c.m0 + ml;
+        cl[u] = c.n0 + c4;
         gv[u] = *reinterpret_cast<const float4*>(Y + ml * YS + c4);
       }
 #pragma unroll
@@ -326,7 +333,7 @@ struct EpiOptim {
         opt_update(o, gv[u].z * o.gscale, pv[u].z, av[u].z, bv[u].z);
         opt_update(o, gv[u].w * o.gscale, pv[u].w, av[u].w, bv[u].w);
         st_pol16<OCF_OPT_ST_POL>(rp, p.p, (uint32_t)(off[u] * 4), pv[u]);
-        if (p.shadow) store_shadow(p, off[u], pv[u]);
+        if (p.shadow) store_shadow(p, rw[u], cl[u], pv[u]);
         if (p.s1) st_pol16<OCF_OPT_ST_POL>(r1, p.s1, (uint32_t)(off[u] * 4), av[u]);
         if (p.s2) st_pol16<OCF_OPT_ST_POL>(r2, p.s2, (uint32_t)(off[u] * 4), bv[u]);
       }

@@ -23,6 +23,10 @@ constexpr int GT_BM = 128;
 constexpr int GT_BN = 128;
 constexpr int GT_THREADS = 256;
 
+#ifndef OCF_FRAG_PREFETCH
+#define OCF_FRAG_PREFETCH 1
+#endif
+
 template <typename CT> struct KInfo { static constexpr int BK = 64; };
 template <> struct KInfo<float> { static constexpr int BK = 32; };
 
@@ -51,9 +55,21 @@ template <typename GT, typename CT, int R, bool COL> struct Stager {
   static_assert(NCH * GT_THREADS == CHUNKS, "tile/threads mismatch");
   GT v[NCH][8];
 
-  // byte offset of this thread's chunk i from the tile origin at k = 0; ld in elements
-  __device__ __forceinline__ static uint32_t chunk_off(int64_t ld, int tid, int i) {
+  // byte offset of this thread's chunk i from the tile origin at k = 0; ld in elements.
+  // blk: the operand is stored 64x64-blocked (rows in blocks of 64, columns in blocks of 64, each
+  // block 64 rows x 128 B contiguous, blocks row-major; 16-bit elements): a K-step tile is two
+  // contiguous 8 KB blocks instead of 64-128 strided row pieces.
+  __device__ __forceinline__ static uint32_t chunk_off(int64_t ld, int tid, int i, bool blk) {
     int c = tid + i * GT_THREADS;
+    if (blk) {
+      if (!COL) {  // [R][K]: r within the tile, kc = 16-B chunk of the 64-wide K-step
+        int r = c / (BK / 8), kc = c % (BK / 8);
+        return (uint32_t)((r >> 6) * ld * 128 + (r & 63) * 128 + kc * 16);
+      } else {     // [K][R]: k within the K-step, 8 consecutive r
+        int k = c / (R / 8), rr = (c % (R / 8)) * 8;
+        return (uint32_t)((rr >> 6) * 8192 + k * 128 + (rr & 63) * 2);
+      }
+    }
     int64_t e;
     if (!COL) {  // [R][K] k-contiguous; chunk = 8 consecutive k of one row
       int r = c / (BK / 8), kc = c % (BK / 8);
@@ -65,15 +81,21 @@ template <typename GT, typename CT, int R, bool COL> struct Stager {
     return (uint32_t)(e * (int64_t)sizeof(GT));
   }
   // byte advance of the tile origin per K-step
-  __device__ __forceinline__ static uint32_t step_bytes(int64_t ld) {
+  __device__ __forceinline__ static uint32_t step_bytes(int64_t ld, bool blk) {
+    if (blk) return (uint32_t)(COL ? ld * 128 : 8192);
     return (uint32_t)((COL ? (int64_t)BK * ld : (int64_t)BK) * (int64_t)sizeof(GT));
+  }
+  // byte offset of the tile origin (rdim0 along R, k0 along K) in a 64x64-blocked array
+  __device__ __forceinline__ static int64_t blocked_origin(int64_t ld, int rdim0, int k0) {
+    return COL ? (int64_t)(k0 >> 6) * ld * 128 + (int64_t)(rdim0 >> 6) * 8192
+               : (int64_t)(rdim0 >> 6) * ld * 128 + (int64_t)(k0 >> 6) * 8192;
   }
 
   template <int AUX>
-  __device__ __forceinline__ void load_pol(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid) {
+  __device__ __forceinline__ void load_pol(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid, bool blk) {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const uint32_t o = chunk_off(ld, tid, i);
+      const uint32_t o = chunk_off(ld, tid, i, blk);
       if constexpr (sizeof(GT) == 4) {
         auto a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, soff, AUX);
         auto b = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, soff, AUX);
@@ -86,9 +108,10 @@ template <typename GT, typename CT, int R, bool COL> struct Stager {
     }
   }
   // nt: wave-uniform choice of the non-temporal cache policy (the operand's last use in the step)
-  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid, bool nt) {
-    if (nt) load_pol<2>(rs, ld, soff, tid);
-    else load_pol<0>(rs, ld, soff, tid);
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t rs, int64_t ld, uint32_t soff, int tid, bool nt,
+                                       bool blk = false) {
+    if (nt) load_pol<2>(rs, ld, soff, tid, blk);
+    else load_pol<0>(rs, ld, soff, tid, blk);
   }
 
   __device__ __forceinline__ void store(char* img, int tid) const {
@@ -195,6 +218,7 @@ struct GemmShape {
   int M, N, K;
   int kchunk;    // K elements per split (multiple of BK)
   int a_nt, b_nt;  // non-temporal operand loads
+  int b_blk;       // B stored 64x64-blocked (16-bit compute-dtype shadows)
   int order;     // 0: n-fastest tile order, 1: m-fastest (XCD-local neighbours)
 };
 
@@ -241,8 +265,11 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   // buffer descriptors at the tile origins (k = k_begin); K-steps advance through soffset
   const __amdgpu_buffer_rsrc_t ra =
       tile_rsrc(ACOL ? Ag + (int64_t)k_begin * sh.lda + m0 : Ag + (int64_t)m0 * sh.lda + k_begin);
+  const bool bblk = sizeof(BGT) == 2 && sh.b_blk;
   const __amdgpu_buffer_rsrc_t rb =
-      tile_rsrc(BCOL ? Bg + (int64_t)k_begin * sh.ldb + n0 : Bg + (int64_t)n0 * sh.ldb + k_begin);
+      bblk ? tile_rsrc(reinterpret_cast<const char*>(Bg) +
+                       Stager<BGT, CT, GT_BN, BCOL>::blocked_origin(sh.ldb, n0, k_begin))
+           : tile_rsrc(BCOL ? Bg + (int64_t)k_begin * sh.ldb + n0 : Bg + (int64_t)n0 * sh.ldb + k_begin);
 
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   // epilogue inputs that do not depend on the product (e.g. target buckets) are loaded here, so
@@ -260,6 +287,28 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   auto compute = [&](const char* bufA) {
     const char* bufB = bufA + Cfg::ImgA::BYTES;
     if constexpr (sizeof(CT) == 2) {
+#if OCF_FRAG_PREFETCH
+      // all fragments of the K-step first (one LDS latency per step instead of one per 16-deep slice)
+      typename Frag<CT>::T fa[BK / 16][2], fb[BK / 16][2];
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[ks][i] = read_frag16<CT, GT_BM, ACOL>(bufA, wm + 32 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[ks][j] = read_frag16<CT, GT_BN, BCOL>(bufB, wn + 32 * j, ks, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if constexpr (std::is_same<CT, _Float16>::value)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+          }
+#else
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         typename Frag<CT>::T fa[2], fb[2];
@@ -277,6 +326,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
           }
       }
+#endif
     } else {
       float fa[2][16], fb[2][16];
 #pragma unroll
@@ -305,15 +355,15 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     Stager<BGT, CT, GT_BN, BCOL> sb0, sb1;
     // the scheduling barrier keeps the compiler from sinking a set's loads below the other set's
     // LDS writes (which would drain the older set before the younger one is issued)
-    const uint32_t sta = decltype(sa0)::step_bytes(sh.lda), stb = decltype(sb0)::step_bytes(sh.ldb);
+    const uint32_t sta = decltype(sa0)::step_bytes(sh.lda, false), stb = decltype(sb0)::step_bytes(sh.ldb, bblk);
     auto ld0 = [&](int kt) {
       sa0.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
-      sb0.load(rb, sh.ldb, kt * stb, tid, sh.b_nt);
+      sb0.load(rb, sh.ldb, kt * stb, tid, sh.b_nt, bblk);
       __builtin_amdgcn_sched_barrier(0);
     };
     auto ld1 = [&](int kt) {
       sa1.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
-      sb1.load(rb, sh.ldb, kt * stb, tid, sh.b_nt);
+      sb1.load(rb, sh.ldb, kt * stb, tid, sh.b_nt, bblk);
       __builtin_amdgcn_sched_barrier(0);
     };
     auto st0 = [&](char* b) { sa0.store(b, tid); sb0.store(b + Cfg::ImgA::BYTES, tid); };
@@ -358,21 +408,24 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   } else {
     Stager<AGT, CT, GT_BM, ACOL> sa;
     Stager<BGT, CT, GT_BN, BCOL> sb;
-    const uint32_t sta = decltype(sa)::step_bytes(sh.lda), stb = decltype(sb)::step_bytes(sh.ldb);
+    const uint32_t sta = decltype(sa)::step_bytes(sh.lda, false), stb = decltype(sb)::step_bytes(sh.ldb, bblk);
     if (nk > 0) {
       sa.load(ra, sh.lda, 0, tid, sh.a_nt);
-      sb.load(rb, sh.ldb, 0, tid, sh.b_nt);
+      sb.load(rb, sh.ldb, 0, tid, sh.b_nt, bblk);
       sa.store(buf0, tid);
       sb.store(buf0 + Cfg::ImgA::BYTES, tid);
       __syncthreads();
     }
+#ifndef OCF_KLOOP_EXP
+#define OCF_KLOOP_EXP 0   // diagnostics only: 1 = no operand traffic in the loop, 2 = no MFMA
+#endif
     for (int kt = 0; kt < nk; ++kt) {
-      const bool more = kt + 1 < nk;
+      const bool more = kt + 1 < nk && OCF_KLOOP_EXP != 1;
       if (more) {
         sa.load(ra, sh.lda, (kt + 1) * sta, tid, sh.a_nt);
-        sb.load(rb, sh.ldb, (kt + 1) * stb, tid, sh.b_nt);
+        sb.load(rb, sh.ldb, (kt + 1) * stb, tid, sh.b_nt, bblk);
       }
-      compute((kt & 1) ? buf1 : buf0);
+      if (OCF_KLOOP_EXP != 2) compute((kt & 1) ? buf1 : buf0);
       if (more) {
         char* nb = ((kt + 1) & 1) ? buf1 : buf0;
         sa.store(nb, tid);

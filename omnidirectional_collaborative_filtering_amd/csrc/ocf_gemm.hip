@@ -19,6 +19,9 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   sh.A = g.A; sh.B = g.B; sh.lda = g.lda; sh.ldb = g.ldb;
   sh.M = g.M; sh.N = g.N; sh.K = g.K; sh.order = g.order;
   sh.a_nt = g.a_nt != 0; sh.b_nt = g.b_nt != 0;
+  sh.b_blk = g.b_blocked != 0;
+  if (sh.b_blk)
+    OCF_CHECK(sizeof(BGT) == 2 && g.ldb % 64 == 0, "ocf_gemm: blocked B needs a 16-bit compute-dtype B and ldb % 64 == 0");
   const int splits = std::max(1, g.splits);
   const int ksteps = g.K / Cfg::BK;
   const int per = (ksteps + splits - 1) / splits;
@@ -93,10 +96,11 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
       break;
     case OCF_EPI_OPTIM:
       if constexpr (!FP32_W || std::is_same<CT, float>::value) if constexpr (BCOL) {
-        EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt, g.p_shadow, g.compute_dtype};
+        EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt, g.p_shadow, g.compute_dtype, g.shadow_blocked != 0};
         OCF_CHECK(g.p != nullptr, "ocf_gemm OPTIM: p required");
         OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm OPTIM: parameter block over 2 GiB");
         OCF_CHECK(!g.p_shadow || g.compute_dtype != OCF_F32, "ocf_gemm OPTIM: shadow weights need f16/bf16 compute");
+        OCF_CHECK(!g.shadow_blocked || g.ld_out % 64 == 0, "ocf_gemm OPTIM: blocked shadow needs ld_out % 64 == 0");
         launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
         return;
       }

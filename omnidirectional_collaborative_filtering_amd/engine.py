@@ -103,6 +103,9 @@ class Engine:
         # rounded to the compute dtype while staging anyway, so streaming a copy rounded once by the
         # optimizer epilogue gives bit-identical products at half the bytes
         self.Wsh = [None] * len(self.W)
+        # shadows stored 64x64-blocked: a GEMM K-step reads two contiguous 8 KB blocks instead of 64-128
+        # strided row pieces (tools/probes/hbm_pattern.hip: 5.0 vs 3.7-4.0 TB/s from HBM)
+        self.shadow_blocked = True
         if self.cdt != _lib.DT_F32:
             for i in sorted({0, len(self.W) - 1}):
                 self.Wsh[i] = torch.zeros(self.W[i].shape, device=self.dev, dtype=self.tdt)
@@ -110,7 +113,14 @@ class Engine:
     def _refresh_shadows(self):
         for w, sh in zip(self.W, self.Wsh):
             if sh is not None:
-                sh.copy_(w)
+                if self.shadow_blocked:     # 64x64 blocks, 8 KB contiguous each (ocf.h b_blocked)
+                    R, C = w.shape
+                    sh.view(R // 64, C // 64, 64, 64).copy_(w.view(R // 64, 64, C // 64, 64).permute(0, 2, 1, 3))
+                else:
+                    sh.copy_(w)
+
+    def _wblk(self, i):
+        return int(self.Wsh[i] is not None and self.shadow_blocked)
 
     def _wop(self, i):
         """(tensor, dtype code) of weight i as a GEMM operand: the shadow when there is one."""
@@ -421,7 +431,7 @@ class Engine:
         with self.phase("enc_gemm"):
             self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
                        _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride,
-                       b_nt=int(self.nt_operands))
+                       b_nt=int(self.nt_operands), b_blocked=self._wblk(0))
         src, nsplit = self.slabs, self.splits0
         if self.comm is not None:
             # partial pre-activation over this rank's columns -> sum over ranks -> activation
@@ -462,6 +472,7 @@ class Engine:
                                                           bk_m=self.bk_m)
         self._gemm(self.h[L - 1], 0, self.Hp[L - 1], *self._wop(L), 0, self.Hp[L - 1], self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_MASKED_MSE, order=1, bias=self.b[L], m_real=self.B, **tg,
+                   b_blocked=self._wblk(L),
                    h_out=self.d_out if with_grad else None, h_dtype=self.cdt, ld_out=self.Np,
                    db_part=self.db_out_part if with_grad else None, ld_db=self.Np,
                    opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
@@ -492,7 +503,7 @@ class Engine:
         with self.phase("dec_bwd_gemm"):
             self._gemm(self.d_out, 0, self.Np, *self._wop(L), 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride,
-                       b_nt=int(self.nt_operands))
+                       b_nt=int(self.nt_operands), b_blocked=self._wblk(L))
         db_last = self.db_h[L - 1]
         src, nsplit = self.slabs, self.splitsL
         if fused and L == 1 and self.comm is None and self.side is not None:
@@ -560,7 +571,8 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o, p_shadow=self.Wsh[i], a_nt=int(self.nt_operands and i in (0, len(self.W) - 1)))
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i], a_nt=int(self.nt_operands and i in (0, len(self.W) - 1)),
+                       shadow_blocked=self._wblk(i))
         else:
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
                        opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale))

@@ -45,7 +45,7 @@ STRUCTS = {
                                              "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean"]),
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
                                        "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part", "t_rows", "t_lboff", "t_ntiles",
-                                       "t_aux", "p_shadow", "b_nt"]),
+                                       "t_aux", "p_shadow", "b_nt", "shadow_blocked"]),
 }
 
 
