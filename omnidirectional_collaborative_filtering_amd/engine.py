@@ -99,6 +99,9 @@ class Engine:
         self.W = [torch.zeros(i, o, **f) for i, o in zip(self.pad_dims[:-2], self.pad_dims[1:-1])]
         self.W.append(torch.zeros(self.pad_dims[-1], self.pad_dims[-2], **f))     # decoder, transposed
         self.b = [torch.zeros(o, **f) for o in self.pad_dims[1:]]
+        # Keras layer.trainable per dense layer (model.py:107-170): a frozen layer still propagates
+        # deltas to the layers below it, but its kernel and bias receive no update and no slot state
+        self.trainable = [True] * len(self.W)
         # half-width shadows of the two N-sized weights (f16/bf16 compute): the MFMA operand would be
         # rounded to the compute dtype while staging anyway, so streaming a copy rounded once by the
         # optimizer epilogue gives bit-identical products at half the bytes
@@ -556,6 +559,8 @@ class Engine:
             self.opt.iterations += 1
 
     def _bias_update(self, i, part, parts, ld, n, grads_out, op):
+        if grads_out is None and not self.trainable[i]:
+            return
         s = cur_stream()
         sw, sb = self.slots[i] if self.slots else ([None, None], [None, None])
         if grads_out is None:
@@ -566,6 +571,8 @@ class Engine:
                  ptr(grads_out[2 * i + 1]), _lib.OcfOptParams(), s)
 
     def _weight_update(self, i, A, lda, Bm, ldb, M, N, gscale, grads_out, op):
+        if grads_out is None and not self.trainable[i]:
+            return
         K = self.Bp
         if grads_out is None:
             sw, _ = self.slots[i]
@@ -582,6 +589,8 @@ class Engine:
         s = cur_stream()
         op = self.opt.step_params(scale, self.l2)
         for i in range(len(self.W)):
+            if not self.trainable[i]:
+                continue
             sw, sb = self.slots[i]
             call("ocf_opt_step", ptr(self.W[i]), ptr(grads[2 * i]), ptr(sw[0]), ptr(sw[1]), self.W[i].numel(), op, s)
             ob = self.opt.step_params(scale, 0.0)

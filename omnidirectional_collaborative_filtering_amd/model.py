@@ -348,3 +348,58 @@ class omni_model(object):
 
     def load_weights(self, weights):
         self.model.set_weights(weights)
+
+    # ---- transfer / denoising-autoencoder helpers (model.py:107-170) ------------------------
+    # Every dense layer of the omni model has an input or output width equal to the hidden width, so
+    # the reference's layer filter selects all of them, in order: hidden layers, then the output
+    # layer.  ``trainable`` takes effect immediately (Keras needs a recompile, model.py:135).
+    @staticmethod
+    def _dense_weights(donor):
+        eng = donor.engine if hasattr(donor, "engine") else donor
+        w = eng.get_weights()
+        return [[w[2 * i], w[2 * i + 1]] for i in range(len(w) // 2)]
+
+    def _set_layer(self, i, wb):
+        w = self.model.get_weights()
+        w[2 * i], w[2 * i + 1] = wb
+        self.model.set_weights(w)
+
+    def replace_dense_layer_weights(self, donor_model, layers_to_replace, make_layers_trainable=False):
+        """model.py:107-125: copy the selected dense layers from the donor; set their trainable flag."""
+        donor = self._dense_weights(donor_model)
+        if layers_to_replace == "all":
+            layers_to_replace = [True] * len(donor)
+        for i in range(len(self.engine.W)):
+            if i < len(layers_to_replace) and layers_to_replace[i]:
+                self._set_layer(i, donor[i])
+                self.engine.trainable[i] = bool(make_layers_trainable)
+                print("Loaded weights for dense layer ", i)
+
+    def manually_load_all_weights(self, donor_model):
+        """model.py:127-132: every layer's weights from the donor (same architecture)."""
+        eng = donor_model.engine if hasattr(donor_model, "engine") else donor_model
+        self.model.set_weights(eng.get_weights())
+
+    def make_trainable(self):
+        """model.py:134-138: layers whose OUTPUT width is the hidden width become trainable (the
+        output layer keeps its flag -- the reference's filter)."""
+        for i in range(len(self.engine.W) - 1):
+            self.engine.trainable[i] = True
+
+    def load_and_fix_for_denoising_autoencoders(self, donor_model):
+        """model.py:140-170: the outer floor(D/2) donor layers on each side are copied into this
+        model's first / last layers and frozen; the middle layers stay trainable."""
+        donor = self._dense_weights(donor_model)
+        print("Number of weight layers to donate", len(donor))
+        k = len(donor) // 2
+        n_new = len(self.engine.W)
+        for i in range(n_new):
+            if i < k:
+                self._set_layer(i, donor[i])
+                self.engine.trainable[i] = False
+                print("Loaded and fixed weights for dense layer ", i, " from donor dense layer ", i)
+            elif i >= n_new - k:
+                src = len(donor) - (n_new - i)
+                self._set_layer(i, donor[src])
+                self.engine.trainable[i] = False
+                print("Loaded and fixed weights for dense layer ", i, " from donor dense layer ", src)

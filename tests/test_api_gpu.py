@@ -94,3 +94,40 @@ def test_jester_style_fit_and_checkpoint(gpu, tmp_path):
     for a, b in zip(w, om2.model.get_weights()):
         np.testing.assert_array_equal(a, b)
     assert om2.model.optimizer.iterations == m.optimizer.iterations
+
+
+@pytest.mark.gpu
+def test_denoising_transfer_freezes_outer_layers(gpu):
+    """model.py:140-170 (load_and_fix_for_denoising_autoencoders) + Keras trainable=False: a 3-layer
+    model takes the outer layers of a 1-hidden-layer donor and freezes them; one Adagrad step then
+    equals the oracle step restricted to the trainable (middle) layers, and the frozen weights do not
+    move."""
+    import numpy as np
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    from omnidirectional_collaborative_filtering_amd.optimizers import Adagrad
+    from oracle.model_oracle import AdagradOracle, OmniOracle
+    B, N, H = 16, 40, 12
+    rng = np.random.RandomState(0)
+    donor = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype="float32", seed=3)
+    om = omni_model(2, H, N, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype="float32", seed=4)
+    om.load_and_fix_for_denoising_autoencoders(donor)
+    assert om.engine.trainable == [False, True, False]
+    w0 = om.model.get_weights()
+    dw = donor.model.get_weights()
+    np.testing.assert_array_equal(w0[0], dw[0])
+    np.testing.assert_array_equal(w0[4], dw[2])
+    om.model.compile(Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error")
+    x = (rng.rand(B, N) < 0.3) * rng.randint(1, 6, size=(B, N)).astype(np.float32)
+    m = -1.0 * (x != 0)
+    om.model.train_on_batch([x, m], x)
+    w1 = om.model.get_weights()
+    ora = OmniOracle([N, H, H, N], "sigmoid", None, None, np.float64).set_params(w0[0::2], w0[1::2])
+    _, _, gW, gb = ora.loss_and_grads(x, m, x)
+    opt = AdagradOracle(lr=0.01, epsilon=1e-8)
+    new_w, new_b = opt.step([w0[2], w0[3]], [gW[1], gb[1]])
+    for i in (0, 1, 4, 5):
+        np.testing.assert_array_equal(w1[i], w0[i])
+    np.testing.assert_allclose(w1[2], new_w, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(w1[3], new_b, rtol=1e-5, atol=1e-6)
+    om.make_trainable()
+    assert om.engine.trainable == [True, True, False]
