@@ -96,6 +96,9 @@ typedef struct OcfScatterArgs {
   /* 1: xin is already zero (the caller cleared the previous batch with ocf_scatter_clear), so the
    * [B_pad][xin_ld] memset is skipped */
   int xin_clean;
+  /* per batch-local source-1 entry: its rating if it is a live input (the value X keeps after
+   * duplicate resolution), else 0 -- the row-gather encoder's input (nullable) */
+  float* xval1;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
@@ -104,6 +107,54 @@ int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
  * block of every source entry's column): a sparse clear replacing the dense memset of the next
  * batch.  Only xin is touched. */
 int ocf_scatter_clear(const OcfScatterArgs* args, void* stream);
+
+/*
+ * Row-gather products for sparse batches (csrc/ocf_sparse.hip): the encoder sum over a batch row's
+ * live input entries, and the decoder's per-target forward / loss / delta with the delta times W_out
+ * row accumulated for the hidden-layer delta (model.py:64-86, train.py:49).  Work is split into
+ * chunks of <= 256 entries of one batch row (ch_row / ch_j0 / ch_j1: batch row and local entry range);
+ * each chunk writes an fp32 partial [H] and ocf_rows_reduce sums a row's chunks in order.
+ */
+typedef struct OcfGatherArgs {
+  const int32_t* rows;       /* [B] CSR row of each batch row (-1 = empty)                        */
+  const int64_t* rp; const int32_t* col; const float* val;   /* the CSR holding the entries     */
+  const int64_t* lboff;      /* [B+1] batch-local entry offsets of this CSR                       */
+  const float* xval;         /* encoder: per batch-local entry input value, 0 = not a live input  */
+  const uint8_t* flag;       /* decoder: per batch-local entry live-target flag                   */
+  const int32_t* ch_row; const int32_t* ch_j0; const int32_t* ch_j1;
+  int n_chunks;
+  const void* W; int w_dtype; int64_t ldw; int w_blocked;   /* weights, one row per column n      */
+  int H;                     /* padded hidden width (multiple of 128, <= 512)                     */
+  float* part;               /* [n_chunks][H] fp32 partial sums                                   */
+  /* decoder only */
+  const void* h; int h_dtype;                 /* [Bp][H] hidden activations (compute dtype)       */
+  const float* bias; float aux;               /* output bias, output-mask value (train.py:47)     */
+  float* delta_e;            /* per batch-local entry delta err*m (nullable)                      */
+  float* chunk_stats;        /* [n_chunks][4]: SSE, SAE, count_nonzero(T + yhat), 0               */
+  void* d_out; int d_dtype; int64_t ld_d;     /* optional dense delta (zero elsewhere)            */
+} OcfGatherArgs;
+
+int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);
+int ocf_gather_decoder(const OcfGatherArgs* args, void* stream);
+
+enum { OCF_REDUCE_RAW = 0, OCF_REDUCE_BIAS_ACT = 1, OCF_REDUCE_GRAD_ACT = 2 };
+
+typedef struct OcfRowsReduceArgs {
+  const float* part; const int32_t* row_cptr;  /* chunk partials, [B+1] first chunk of each row   */
+  int B, Bp, H, mode;
+  float* out;                /* RAW: [Bp][H] fp32 row sums                                        */
+  /* BIAS_ACT (layer forward) / GRAD_ACT (delta through activation + dropout) */
+  const float* bias; int act; float keep; uint64_t seed, stream;
+  const uint8_t* mask_in; uint8_t* mask_out; float* a_out; const float* a_in;
+  void* h_out; int h_dtype; int n_real;
+  float* db_part; float gscale;             /* GRAD_ACT: [Bp][H] bias-gradient rows * gscale     */
+  const float* chunk_stats; float* stats_part; float* row_sse;   /* decoder stats -> per row      */
+} OcfRowsReduceArgs;
+
+int ocf_rows_reduce(const OcfRowsReduceArgs* args, void* stream);
+
+/* out[n] = gscale * sum_{b < B} d[b][n] for a dense [*][ld] array in dtype (output-bias gradient) */
+int ocf_colsum(const void* d, int dtype, int64_t ld, int B, int N, float gscale, float* out, void* stream);
 
 /* Target buckets from dense target / output-mask arrays (Model.train_on_batch on user arrays). */
 int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,
@@ -156,6 +207,16 @@ typedef struct OcfGemmArgs {
    * 8 KB contiguous and row-major inside, blocks row-major; ldb = columns); OPTIM: write p_shadow in
    * that layout */
   int b_blocked, shadow_blocked;
+  /* OPTIM / GRAD with a_col = 1: A ([K][M], K = batch row, M = column) is not read from memory but
+   * built per K-step in LDS from a CSR's column-sorted view (RatingsCSR.tile_index): for batch row b
+   * (CSR row sp_rows[b], b < sp_krows) and the M tile t, the entries [sp_rp[r] + sp_tptr[r][t],
+   * sp_rp[r] + sp_tptr[r][t+1]) of sp_col / sp_lidx, with value sp_vals[sp_lboff[b] + lidx] (0 = none).
+   * sp_colsum (nullable): opt.gscale * column sums of A (the output-bias gradient) */
+  int a_sparse;
+  const int32_t* sp_rows; const int64_t* sp_rp; const int32_t* sp_tptr; const int32_t* sp_col;
+  const int32_t* sp_lidx; const int64_t* sp_lboff; const float* sp_vals;
+  int sp_ntiles, sp_krows;
+  float* sp_colsum;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

@@ -40,7 +40,29 @@ class OcfScatterArgs(ctypes.Structure):
         ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
         ("pos1", P),
         ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
-        ("xin_clean", I32),
+        ("xin_clean", I32), ("xval1", P),
+    ]
+
+
+class OcfGatherArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", P), ("rp", P), ("col", P), ("val", P), ("lboff", P), ("xval", P), ("flag", P),
+        ("ch_row", P), ("ch_j0", P), ("ch_j1", P), ("n_chunks", I32),
+        ("W", P), ("w_dtype", I32), ("ldw", I64), ("w_blocked", I32), ("H", I32), ("part", P),
+        ("h", P), ("h_dtype", I32), ("bias", P), ("aux", F32), ("delta_e", P), ("chunk_stats", P),
+        ("d_out", P), ("d_dtype", I32), ("ld_d", I64),
+    ]
+
+
+REDUCE_RAW, REDUCE_BIAS_ACT, REDUCE_GRAD_ACT = 0, 1, 2
+
+
+class OcfRowsReduceArgs(ctypes.Structure):
+    _fields_ = [
+        ("part", P), ("row_cptr", P), ("B", I32), ("Bp", I32), ("H", I32), ("mode", I32), ("out", P),
+        ("bias", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64),
+        ("mask_in", P), ("mask_out", P), ("a_out", P), ("a_in", P), ("h_out", P), ("h_dtype", I32), ("n_real", I32),
+        ("db_part", P), ("gscale", F32), ("chunk_stats", P), ("stats_part", P), ("row_sse", P),
     ]
 
 
@@ -60,6 +82,8 @@ class OcfGemmArgs(ctypes.Structure):
         ("t_rows", P), ("t_rp", P), ("t_tptr", P), ("t_col", P), ("t_val", P), ("t_lidx", P), ("t_flag", P),
         ("t_lboff", P), ("t_ntiles", I32), ("t_aux", F32),
         ("p_shadow", P), ("a_nt", I32), ("b_nt", I32), ("b_blocked", I32), ("shadow_blocked", I32),
+        ("a_sparse", I32), ("sp_rows", P), ("sp_rp", P), ("sp_tptr", P), ("sp_col", P), ("sp_lidx", P),
+        ("sp_lboff", P), ("sp_vals", P), ("sp_ntiles", I32), ("sp_krows", I32), ("sp_colsum", P),
     ]
 
 
@@ -75,6 +99,10 @@ SIGNATURES = {
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),
     "ocf_bias_opt_from_partials": (I32, [P, P, I32, I64, I32, P, P, P, ctypes.POINTER(OcfOptParams), P]),
     "ocf_stats_finalize": (I32, [P, I32, P, I32, I32, P, P]),
+    "ocf_gather_encoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
+    "ocf_gather_decoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
+    "ocf_rows_reduce": (I32, [ctypes.POINTER(OcfRowsReduceArgs), P]),
+    "ocf_colsum": (I32, [P, I32, I64, I32, I32, F32, P, P]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

@@ -149,6 +149,12 @@ __device__ __forceinline__ float grad_act_value(const GradActParams& p, int m, i
   return d * act_grad(p.act, p.a[idx]);
 }
 
+__device__ __forceinline__ float load_ct(const void* in, int dtype, int64_t idx) {
+  if (dtype == OCF_F32) return reinterpret_cast<const float*>(in)[idx];
+  if (dtype == OCF_F16) return (float)reinterpret_cast<const _Float16*>(in)[idx];
+  return (float)reinterpret_cast<const __bf16*>(in)[idx];
+}
+
 __device__ __forceinline__ void store_ct(void* out, int dtype, int64_t idx, float v) {
   if (dtype == OCF_F32) reinterpret_cast<float*>(out)[idx] = v;
   else if (dtype == OCF_F16) reinterpret_cast<_Float16*>(out)[idx] = (_Float16)v;

@@ -220,7 +220,46 @@ struct GemmShape {
   int a_nt, b_nt;  // non-temporal operand loads
   int b_blk;       // B stored 64x64-blocked (16-bit compute-dtype shadows)
   int order;     // 0: n-fastest tile order, 1: m-fastest (XCD-local neighbours)
+  // sparse A (gemm_kernel SPA): A = [K][M] built in LDS from a CSR's column-sorted view.  K index =
+  // batch row b, M index = column n; value = sp_vals[sp_lboff[b] + list index] (0 = no entry)
+  const int32_t* sp_rows; const int64_t* sp_rp; const int32_t* sp_tptr; const int32_t* sp_col;
+  const int32_t* sp_lidx; const int64_t* sp_lboff; const float* sp_vals;
+  int sp_ntiles, sp_krows;   // column tiles per CSR row; batch rows that exist (K beyond is padding)
+  float* sp_colsum;          // nullable: out[m] = colsum_scale * sum_k A[k][m] (tile_n == 0 workgroups)
+  float colsum_scale;
 };
+
+// Fill the A image of one K-step from sparse entries: zero it, then 4 threads per batch row walk the
+// row's entries of this 128-column tile (each (k, m) has at most one nonzero: duplicates and
+// non-entries carry value 0 and are skipped).  Caller synchronises before and after.
+template <typename CT, int R, int BK>
+__device__ __forceinline__ void sparse_a_zero(char* img, int tid) {
+  using I = Img<CT, R, true>;
+  uint4* p = reinterpret_cast<uint4*>(img);
+  constexpr int N16 = I::BYTES / 16;
+  for (int i = tid; i < N16; i += GT_THREADS) p[i] = make_uint4(0, 0, 0, 0);
+}
+template <typename CT, int R, int BK>
+__device__ __forceinline__ void sparse_a_fill(const GemmShape& sh, char* img, int k0, int m0, int tid) {
+  using I = Img<CT, R, true>;
+  const int k = tid >> 2, sub = tid & 3;
+  if (k >= BK) return;
+  const int b = k0 + k;
+  if (b >= sh.sp_krows) return;
+  const int r = sh.sp_rows[b];
+  if (r < 0) return;
+  const int t = m0 / R;
+  const int32_t* tp = sh.sp_tptr + (int64_t)r * (sh.sp_ntiles + 1) + t;
+  const int64_t base = sh.sp_rp[r];
+  const int64_t lo = base + tp[0], hi = base + tp[1];
+  const int64_t lb = sh.sp_lboff[b];
+  for (int64_t e = lo + sub; e < hi; e += 4) {
+    const float v = sh.sp_vals[lb + sh.sp_lidx[e]];
+    if (v == 0.f) continue;
+    const int m = sh.sp_col[e] - m0;
+    *reinterpret_cast<CT*>(img + k * I::STRIDE + m * (int)sizeof(CT)) = CvtT<CT>::to(v);
+  }
+}
 
 template <typename CT, bool ACOL, bool BCOL, typename AGT, typename BGT> struct GemmCfg {
   using ImgA = Img<CT, GT_BM, ACOL>;
@@ -238,7 +277,7 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + (orig >> 3);
 }
 
-template <typename CT, bool ACOL, bool BCOL, typename AGT, typename BGT, class Epi, int LDS_BYTES>
+template <typename CT, bool ACOL, bool BCOL, typename AGT, typename BGT, class Epi, int LDS_BYTES, bool SPA = false>
 __global__ void __launch_bounds__(GT_THREADS)
 gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   using Cfg = GemmCfg<CT, ACOL, BCOL, AGT, BGT>;
@@ -349,7 +388,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   // two so neither set is ever copied and every wait the compiler inserts covers exactly the set
   // about to be written to LDS); only for 16-bit operands, where two sets fit the register budget
   // of two workgroups per CU.
-  constexpr bool DEEP = Epi::DEEP_PIPE && sizeof(CT) == 2 && sizeof(AGT) == 2 && sizeof(BGT) == 2;
+  constexpr bool DEEP = !SPA && Epi::DEEP_PIPE && sizeof(CT) == 2 && sizeof(AGT) == 2 && sizeof(BGT) == 2;
   if constexpr (DEEP) {
     Stager<AGT, CT, GT_BM, ACOL> sa0, sa1;
     Stager<BGT, CT, GT_BN, BCOL> sb0, sb1;
@@ -409,12 +448,34 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     Stager<AGT, CT, GT_BM, ACOL> sa;
     Stager<BGT, CT, GT_BN, BCOL> sb;
     const uint32_t sta = decltype(sa)::step_bytes(sh.lda, false), stb = decltype(sb)::step_bytes(sh.ldb, bblk);
+    // sparse A: output-column sums of A for the tile_n == 0 workgroups (bias gradient)
+    const bool colsum = ACOL && sh.sp_colsum && tile_n == 0;
+    float csum = 0.f;
+    auto fill_a = [&](char* img, int kt) {   // SPA: zero + scatter the A image of K-step kt
+      if constexpr (SPA) {
+        sparse_a_zero<CT, GT_BM, BK>(img, tid);
+        __syncthreads();
+        sparse_a_fill<CT, GT_BM, BK>(sh, img, k_begin + kt * BK, m0, tid);
+      }
+    };
+    auto sum_a = [&](const char* img) {      // column sums of the A image (fixed k order), [K][M] A only
+      if constexpr (ACOL) {
+        if (colsum && tid < GT_BM) {
+          using I = Img<CT, GT_BM, true>;
+          float s0 = 0.f;
+          for (int k = 0; k < BK; ++k) s0 += (float)*reinterpret_cast<const CT*>(img + k * I::STRIDE + tid * (int)sizeof(CT));
+          csum += s0;
+        }
+      }
+    };
     if (nk > 0) {
-      sa.load(ra, sh.lda, 0, tid, sh.a_nt);
+      if constexpr (!SPA) sa.load(ra, sh.lda, 0, tid, sh.a_nt);
       sb.load(rb, sh.ldb, 0, tid, sh.b_nt, bblk);
-      sa.store(buf0, tid);
+      if constexpr (SPA) fill_a(buf0, 0);
+      else sa.store(buf0, tid);
       sb.store(buf0 + Cfg::ImgA::BYTES, tid);
       __syncthreads();
+      sum_a(buf0);
     }
 #ifndef OCF_KLOOP_EXP
 #define OCF_KLOOP_EXP 0   // diagnostics only: 1 = no operand traffic in the loop, 2 = no MFMA
@@ -422,17 +483,20 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     for (int kt = 0; kt < nk; ++kt) {
       const bool more = kt + 1 < nk && OCF_KLOOP_EXP != 1;
       if (more) {
-        sa.load(ra, sh.lda, (kt + 1) * sta, tid, sh.a_nt);
+        if constexpr (!SPA) sa.load(ra, sh.lda, (kt + 1) * sta, tid, sh.a_nt);
         sb.load(rb, sh.ldb, (kt + 1) * stb, tid, sh.b_nt, bblk);
       }
       if (OCF_KLOOP_EXP != 2) compute((kt & 1) ? buf1 : buf0);
       if (more) {
         char* nb = ((kt + 1) & 1) ? buf1 : buf0;
-        sa.store(nb, tid);
+        if constexpr (SPA) fill_a(nb, kt + 1);
+        else sa.store(nb, tid);
         sb.store(nb + Cfg::ImgA::BYTES, tid);
       }
       __syncthreads();
+      if (more) sum_a(((kt + 1) & 1) ? buf1 : buf0);
     }
+    if (colsum && tid < GT_BM) sh.sp_colsum[m0 + tid] = csum * sh.colsum_scale;
   }
 
   TileCtx c;

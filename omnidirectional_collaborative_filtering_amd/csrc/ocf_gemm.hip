@@ -10,7 +10,7 @@ using namespace ocf;
 
 namespace {
 
-template <typename CT, bool ACOL, bool BCOL, typename BGT, class Epi>
+template <typename CT, bool ACOL, bool BCOL, typename BGT, class Epi, bool SPA = false>
 void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s) {
   using Cfg = GemmCfg<CT, ACOL, BCOL, CT, BGT>;
   constexpr int LDS = std::max(Cfg::OPER_LDS, Epi::LDS_NEED);
@@ -27,7 +27,18 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   const int per = (ksteps + splits - 1) / splits;
   sh.kchunk = per * Cfg::BK;
   const int ntile = (g.M / GT_BM) * (g.N / GT_BN);
-  hipLaunchKernelGGL((gemm_kernel<CT, ACOL, BCOL, CT, BGT, Epi, LDS>), dim3(ntile, splits), dim3(GT_THREADS), 0, s, sh, ep);
+  sh.sp_colsum = nullptr;
+  if constexpr (ACOL) {          // column sums of A (output-bias gradient), dense or sparse A
+    sh.sp_colsum = g.sp_colsum;
+    sh.colsum_scale = g.opt.gscale;
+  }
+  if constexpr (SPA) {
+    sh.sp_rows = g.sp_rows; sh.sp_rp = g.sp_rp; sh.sp_tptr = g.sp_tptr; sh.sp_col = g.sp_col;
+    sh.sp_lidx = g.sp_lidx; sh.sp_lboff = g.sp_lboff; sh.sp_vals = g.sp_vals;
+    sh.sp_ntiles = g.sp_ntiles; sh.sp_krows = g.sp_krows;
+  }
+  hipLaunchKernelGGL((gemm_kernel<CT, ACOL, BCOL, CT, BGT, Epi, LDS, SPA>), dim3(ntile, splits), dim3(GT_THREADS), 0, s,
+                     sh, ep);
   OCF_HIP(hipGetLastError());
 }
 
@@ -101,6 +112,12 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
         OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm OPTIM: parameter block over 2 GiB");
         OCF_CHECK(!g.p_shadow || g.compute_dtype != OCF_F32, "ocf_gemm OPTIM: shadow weights need f16/bf16 compute");
         OCF_CHECK(!g.shadow_blocked || g.ld_out % 64 == 0, "ocf_gemm OPTIM: blocked shadow needs ld_out % 64 == 0");
+        if constexpr (ACOL) {
+          if (g.a_sparse) {
+            launch<CT, ACOL, BCOL, CT, EpiOptim, true>(g, p, s);
+            return;
+          }
+        }
         launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
         return;
       }
@@ -108,6 +125,12 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
     case OCF_EPI_GRAD:
       if constexpr (!FP32_W || std::is_same<CT, float>::value) if constexpr (BCOL) {
         EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale};
+        if constexpr (ACOL) {
+          if (g.a_sparse) {
+            launch<CT, ACOL, BCOL, CT, EpiGradStore, true>(g, p, s);
+            return;
+          }
+        }
         launch<CT, ACOL, BCOL, CT, EpiGradStore>(g, p, s);
         return;
       }
@@ -146,7 +169,7 @@ void dispatch(const OcfGemmArgs& g, hipStream_t s) {
 extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   OCF_TRY_BEGIN
   const OcfGemmArgs& g = *args;
-  OCF_CHECK(g.A && g.B, "ocf_gemm: null operand");
+  OCF_CHECK((g.A || g.a_sparse) && g.B, "ocf_gemm: null operand");
   OCF_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "ocf_gemm: empty shape");
   OCF_CHECK(g.M % GT_BM == 0 && g.N % GT_BN == 0, "ocf_gemm: M and N must be multiples of 128");
   const int bk = g.compute_dtype == OCF_F32 ? 32 : 64;
@@ -155,6 +178,13 @@ extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   OCF_CHECK(g.lda % 8 == 0 && g.ldb % 8 == 0, "ocf_gemm: leading dimensions must be multiples of 8");
   OCF_CHECK(g.splits >= 1, "ocf_gemm: splits >= 1");
   OCF_CHECK(g.splits == 1 || g.epi == OCF_EPI_SLAB, "ocf_gemm: split-K only with the SLAB epilogue");
+  if (g.a_sparse) {
+    OCF_CHECK(g.a_col && (g.epi == OCF_EPI_OPTIM || g.epi == OCF_EPI_GRAD),
+              "ocf_gemm: sparse A only for OPTIM / GRAD with a_col = 1");
+    OCF_CHECK(g.sp_rows && g.sp_rp && g.sp_tptr && g.sp_col && g.sp_lidx && g.sp_lboff && g.sp_vals &&
+                  g.sp_ntiles * GT_BM >= g.M && g.sp_krows <= g.K,
+              "ocf_gemm: sparse A descriptor incomplete");
+  }
   hipStream_t s = (hipStream_t)stream;
   switch (g.compute_dtype) {
     case OCF_F16: dispatch<_Float16>(g, s); break;

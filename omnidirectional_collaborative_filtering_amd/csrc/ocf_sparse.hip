@@ -1,0 +1,426 @@
+// Row-gather forms of the weight-streaming products for sparse batches (model.py:64-86 on the
+// batch's rating entries instead of the dense [B][N] arrays).
+//
+//   encoder   hpre[b, :]  = sum over live input entries (b, n, x) of x * W1[n, :]
+//   decoder   y = h[b, :] . W_out[n, :] + b_out[n] at every live target (b, n, t);
+//             err = m*y - t, delta = err*m, loss/metric sums, and
+//             dhpre[b, :] += delta * W_out[n, :]  (the same W_out row, still in registers)
+//
+// The masked output of model.py:84-86 is m (aux) at target positions and 0 elsewhere, so y off the
+// targets never reaches the loss or a gradient: the dense decoder GEMM and the dense delta are
+// replaced by these per-entry products, exactly (fp32 accumulation).  Each W row is read once per
+// entry (1 KB at H = 512, f16 shadow), about the bytes of the dense product, without its MFMA-issue
+// bound at B = 256.
+//
+// Work unit: a chunk of <= 256 consecutive entries of one batch row (host-built chunk tables, so a
+// row with 60k ratings spreads over many workgroups).  A workgroup = 16 groups of 16 lanes; a group
+// owns one entry at a time and each lane holds PPL 16-byte pieces of the row (pieces l, l+16, ...:
+// every load instruction of a group reads 256 contiguous bytes).  Chunk partials are reduced in a
+// fixed order per row by ocf_rows_reduce, which also applies the layer epilogue.
+#include "ocf_epilogues.h"
+#include "ocf_internal.h"
+
+namespace ocf {
+
+constexpr int RG_THREADS = 256;
+constexpr int RG_GROUPS = RG_THREADS / 16;
+constexpr int RG_MAX_H = 512;
+#ifndef OCF_RG_U
+#define OCF_RG_U 4
+#endif
+constexpr int RG_U = OCF_RG_U;   // entries per group in flight
+
+template <typename WT> struct EPc { static constexpr int v = 16 / (int)sizeof(WT); };
+
+// piece p (16 bytes) of row n of a weight array: row-major [rows][ldw] or 64x64-blocked (16-bit)
+template <typename WT>
+__device__ __forceinline__ void load_piece(const WT* W, int64_t ldw, int blocked, int n, int p,
+                                           float (&out)[EPc<WT>::v]) {
+  constexpr int E = EPc<WT>::v;
+  const char* base;
+  if (blocked) {
+    const int h = p * 8;
+    base = reinterpret_cast<const char*>(W) + ((((int64_t)(n >> 6) * (ldw >> 6)) + (h >> 6)) << 13) + (n & 63) * 128 +
+           (h & 63) * 2;
+  } else {
+    base = reinterpret_cast<const char*>(W + (int64_t)n * ldw) + p * 16;
+  }
+  const uint4 u = *reinterpret_cast<const uint4*>(base);
+  if constexpr (sizeof(WT) == 4) {
+    __builtin_memcpy(out, &u, 16);
+  } else {
+    WT e[E];
+    __builtin_memcpy(e, &u, 16);
+#pragma unroll
+    for (int k = 0; k < E; ++k) out[k] = (float)e[k];
+  }
+}
+
+// raw 16-byte piece (kept packed in registers until used: half the VGPRs for 16-bit weights)
+template <typename WT>
+__device__ __forceinline__ uint4 load_piece_raw(const WT* W, int64_t ldw, int blocked, int n, int p) {
+  const char* base;
+  if (blocked) {
+    const int h = p * 8;
+    base = reinterpret_cast<const char*>(W) + ((((int64_t)(n >> 6) * (ldw >> 6)) + (h >> 6)) << 13) + (n & 63) * 128 +
+           (h & 63) * 2;
+  } else {
+    base = reinterpret_cast<const char*>(W + (int64_t)n * ldw) + p * 16;
+  }
+  return *reinterpret_cast<const uint4*>(base);
+}
+template <typename WT>
+__device__ __forceinline__ void unpack_piece(const uint4& u, float (&out)[EPc<WT>::v]) {
+  if constexpr (sizeof(WT) == 4) {
+    __builtin_memcpy(out, &u, 16);
+  } else {
+    WT e[EPc<WT>::v];
+    __builtin_memcpy(e, &u, 16);
+#pragma unroll
+    for (int k = 0; k < EPc<WT>::v; ++k) out[k] = (float)e[k];
+  }
+}
+
+// the same pieces of a compute-dtype activation row h[b] (row-major, ld = H)
+template <typename HT, int E>
+__device__ __forceinline__ void load_act_piece(const void* h, int64_t ld, int b, int p, float (&out)[E]) {
+  const HT* row = reinterpret_cast<const HT*>(h) + (int64_t)b * ld + p * E;
+#pragma unroll
+  for (int k = 0; k < E; ++k) out[k] = (float)row[k];
+}
+
+// fixed-order reduction of the groups' per-lane vectors into part[chunk][H]
+template <int G, int V, int E, int PPL>
+__device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red, float* part, int c, int H, int grp,
+                                              int l) {
+  constexpr int NG = RG_THREADS / G;
+#pragma unroll
+  for (int i = 0; i < PPL; ++i)
+#pragma unroll
+    for (int k = 0; k < E; ++k) red[grp * H + (l + G * i) * E + k] = acc[i * E + k];
+  __syncthreads();
+  for (int x = threadIdx.x; x < H; x += RG_THREADS) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int g = 0; g < NG; g += 2) {
+      s0 += red[g * H + x];
+      if (g + 1 < NG) s1 += red[(g + 1) * H + x];
+    }
+    part[(int64_t)c * H + x] = s0 + s1;
+  }
+}
+
+// A group of G lanes owns one entry at a time (RG_U entries in flight); lane l holds pieces
+// l, l+G, ... (PPL of them) of the weight row, so a group's load instruction reads G*16
+// contiguous bytes.
+template <typename WT, int G, int PPL>
+__global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArgs a) {
+  constexpr int E = EPc<WT>::v;
+  constexpr int V = PPL * E;
+  constexpr int NG = RG_THREADS / G;
+  __shared__ float red[NG * RG_MAX_H];
+  const int c = blockIdx.x;
+  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
+  const int grp = threadIdx.x / G, l = threadIdx.x % G;
+  const int r = a.rows[b];
+  const int64_t s = r >= 0 ? a.rp[r] : 0;
+  const int64_t lb = a.lboff[b];
+  const WT* W = reinterpret_cast<const WT*>(a.W);
+  float acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
+    float x[RG_U];
+    int n[RG_U];
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u) {
+      const int ju = j + u * NG;
+      const bool ok = ju < j1;
+      x[u] = ok ? a.xval[lb + ju] : 0.f;
+      n[u] = ok ? a.col[s + ju] : 0;
+    }
+    uint4 w[RG_U][PPL];
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u)
+#pragma unroll
+      for (int i = 0; i < PPL; ++i)
+        w[u][i] = x[u] != 0.f ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u)
+#pragma unroll
+      for (int i = 0; i < PPL; ++i) {
+        float f[E];
+        unpack_piece<WT>(w[u][i], f);
+#pragma unroll
+        for (int k = 0; k < E; ++k) acc[i * E + k] += x[u] * f[k];
+      }
+  }
+  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l);
+}
+
+template <typename WT, typename HT, int G, int PPL>
+__global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a) {
+  constexpr int E = EPc<WT>::v;
+  constexpr int V = PPL * E;
+  constexpr int NG = RG_THREADS / G;
+  __shared__ float red[NG * RG_MAX_H];
+  __shared__ float st[NG][3];
+  const int c = blockIdx.x;
+  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
+  const int grp = threadIdx.x / G, l = threadIdx.x % G;
+  const int r = a.rows[b];
+  const int64_t s = r >= 0 ? a.rp[r] : 0;
+  const int64_t lb = a.lboff[b];
+  const WT* W = reinterpret_cast<const WT*>(a.W);
+  const float m = a.aux;
+  float hv[V];
+#pragma unroll
+  for (int i = 0; i < PPL; ++i) {
+    float t[E];
+    load_act_piece<HT, E>(a.h, a.H, b, l + G * i, t);
+#pragma unroll
+    for (int k = 0; k < E; ++k) hv[i * E + k] = t[k];
+  }
+  float acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  float sse = 0.f, sae = 0.f, cnt = 0.f;
+  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
+    bool live[RG_U];
+    int n[RG_U];
+    float t[RG_U];
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u) {
+      const int ju = j + u * NG;
+      const bool ok = ju < j1;
+      live[u] = ok && a.flag[lb + ju];
+      n[u] = ok ? a.col[s + ju] : 0;
+      t[u] = ok ? a.val[s + ju] : 0.f;
+    }
+    uint4 w[RG_U][PPL];
+    float dot[RG_U];
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u)
+#pragma unroll
+      for (int i = 0; i < PPL; ++i)
+        w[u][i] = live[u] ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u) {
+      float d0 = 0.f;
+#pragma unroll
+      for (int i = 0; i < PPL; ++i) {
+        float f[E];
+        unpack_piece<WT>(w[u][i], f);
+#pragma unroll
+        for (int k = 0; k < E; ++k) d0 += hv[i * E + k] * f[k];
+      }
+      dot[u] = d0;
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int u = 0; u < RG_U; ++u) dot[u] += __shfl_xor(dot[u], off, G);
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u) {
+      const int ju = j + u * NG;
+      if (ju >= j1) break;
+      float d = 0.f;
+      if (live[u]) {
+        const float yh = m * (dot[u] + a.bias[n[u]]);
+        const float err = yh - t[u];
+        d = err * m;
+        if (l == 0) {
+          sse += err * err;
+          sae += fabsf(err);
+          cnt += (t[u] + yh != 0.f) ? 1.f : 0.f;
+          if (a.d_out) store_ct(a.d_out, a.d_dtype, (int64_t)b * a.ld_d + n[u], d);
+        }
+      }
+      if (l == 0 && a.delta_e) a.delta_e[lb + ju] = d;
+#pragma unroll
+      for (int i = 0; i < PPL; ++i) {
+        float f[E];
+        unpack_piece<WT>(w[u][i], f);
+#pragma unroll
+        for (int k = 0; k < E; ++k) acc[i * E + k] += d * f[k];
+      }
+    }
+  }
+  if (l == 0) {
+    st[grp][0] = sse;
+    st[grp][1] = sae;
+    st[grp][2] = cnt;
+  }
+  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l);
+  if (threadIdx.x < 3) {
+    float v = 0.f;
+    for (int g = 0; g < NG; ++g) v += st[g][threadIdx.x];
+    a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
+  }
+}
+
+// per batch row: fixed-order sum of its chunk partials, then the layer epilogue
+__global__ void __launch_bounds__(256) rows_reduce_kernel(OcfRowsReduceArgs a) {
+  const int b = blockIdx.x;
+  const bool real = b < a.B;
+  const int c0 = real ? a.row_cptr[b] : 0, c1 = real ? a.row_cptr[b + 1] : 0;
+  for (int x = threadIdx.x; x < a.H; x += blockDim.x) {
+    float v = 0.f;
+    for (int c = c0; c < c1; ++c) v += a.part[(int64_t)c * a.H + x];
+    if (a.mode == OCF_REDUCE_RAW) {
+      a.out[(int64_t)b * a.H + x] = v;
+    } else if (a.mode == OCF_REDUCE_BIAS_ACT) {
+      BiasActParams p;
+      p.bias = a.bias; p.act = a.act; p.keep = a.keep; p.seed = a.seed; p.stream = a.stream;
+      p.mask_in = a.mask_in; p.mask_out = a.mask_out; p.a_out = a.a_out; p.h_out = a.h_out;
+      p.h_dtype = a.h_dtype; p.ld = a.H; p.m_real = a.B; p.n_real = a.n_real;
+      bias_act_store(p, b, x, v);
+    } else {
+      GradActParams p;
+      p.a = a.a_in; p.mask = a.mask_in; p.keep = a.keep; p.act = a.act; p.d_out = a.h_out; p.d_dtype = a.h_dtype;
+      p.ld = a.H; p.db_part = nullptr; p.gscale = a.gscale; p.m_real = a.B; p.n_real = a.n_real;
+      const float d = grad_act_value(p, b, x, v);
+      store_ct(a.h_out, a.h_dtype, (int64_t)b * a.H + x, d);
+      if (a.db_part) a.db_part[(int64_t)b * a.H + x] = d * a.gscale;
+    }
+  }
+  if (a.chunk_stats && threadIdx.x < 4) {
+    float v = 0.f;
+    if (threadIdx.x < 3)
+      for (int c = c0; c < c1; ++c) v += a.chunk_stats[(int64_t)c * 4 + threadIdx.x];
+    a.stats_part[(int64_t)b * 4 + threadIdx.x] = v;
+    if (threadIdx.x == 0 && a.row_sse) a.row_sse[b] = v;
+  }
+}
+
+// (group width G, pieces per lane PPL) for a row of H elements of WT: the widest group (<= 64
+// lanes) that the row's 16-byte pieces fill
+template <typename WT> bool gather_shape(int H, int& G, int& ppl) {
+  const int pieces = H / EPc<WT>::v;
+  for (int g : {64, 32, 16})
+    if (pieces % g == 0) {
+      G = g;
+      ppl = pieces / g;
+      return ppl <= 3;
+    }
+  return false;
+}
+
+template <template <int, int> class L>
+void by_shape(int G, int ppl, const OcfGatherArgs& a, hipStream_t s) {
+  if (G == 64 && ppl == 1) L<64, 1>::go(a, s);
+  else if (G == 64 && ppl == 2) L<64, 2>::go(a, s);
+  else if (G == 32 && ppl == 1) L<32, 1>::go(a, s);
+  else if (G == 32 && ppl == 3) L<32, 3>::go(a, s);
+  else if (G == 16 && ppl == 1) L<16, 1>::go(a, s);
+  else if (G == 16 && ppl == 3) L<16, 3>::go(a, s);
+  else throw std::runtime_error("row gather: unsupported H / weight dtype combination");
+}
+
+template <typename WT> struct Enc {
+  template <int G, int P> struct L {
+    static void go(const OcfGatherArgs& a, hipStream_t s) {
+      hipLaunchKernelGGL((gather_encoder_kernel<WT, G, P>), dim3(a.n_chunks), dim3(RG_THREADS), 0, s, a);
+    }
+  };
+};
+template <typename WT, typename HT> struct Dec {
+  template <int G, int P> struct L {
+    static void go(const OcfGatherArgs& a, hipStream_t s) {
+      hipLaunchKernelGGL((gather_decoder_kernel<WT, HT, G, P>), dim3(a.n_chunks), dim3(RG_THREADS), 0, s, a);
+    }
+  };
+};
+
+void check_gather(const OcfGatherArgs& a, const char* who) {
+  OCF_CHECK(a.rows && a.rp && a.col && a.lboff && a.ch_row && a.ch_j0 && a.ch_j1 && a.W && a.part,
+            std::string(who) + ": null pointer");
+  OCF_CHECK(a.H > 0 && a.H <= RG_MAX_H && a.H % 128 == 0, std::string(who) + ": H must be a multiple of 128, <= 512");
+  OCF_CHECK(a.w_dtype == OCF_F32 || a.w_dtype == OCF_F16 || a.w_dtype == OCF_BF16, std::string(who) + ": w_dtype");
+  OCF_CHECK(!a.w_blocked || a.w_dtype != OCF_F32, std::string(who) + ": blocked weights are 16-bit");
+  OCF_CHECK(a.ldw >= a.H && a.ldw % 8 == 0, std::string(who) + ": ldw");
+}
+
+template <typename WT> void shape_or_throw(const OcfGatherArgs& a, int& G, int& ppl) {
+  if (!gather_shape<WT>(a.H, G, ppl)) throw std::runtime_error("row gather: unsupported H " + std::to_string(a.H));
+}
+
+}  // namespace ocf
+
+using namespace ocf;
+
+extern "C" int ocf_gather_encoder(const OcfGatherArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfGatherArgs& a = *args;
+  check_gather(a, "ocf_gather_encoder");
+  OCF_CHECK(a.xval != nullptr, "ocf_gather_encoder: xval required");
+  if (a.n_chunks == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  int G, ppl;
+  if (a.w_dtype == OCF_F32) { shape_or_throw<float>(a, G, ppl); by_shape<Enc<float>::L>(G, ppl, a, s); }
+  else if (a.w_dtype == OCF_F16) { shape_or_throw<_Float16>(a, G, ppl); by_shape<Enc<_Float16>::L>(G, ppl, a, s); }
+  else { shape_or_throw<__bf16>(a, G, ppl); by_shape<Enc<__bf16>::L>(G, ppl, a, s); }
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+extern "C" int ocf_gather_decoder(const OcfGatherArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfGatherArgs& a = *args;
+  check_gather(a, "ocf_gather_decoder");
+  OCF_CHECK(a.flag && a.val && a.h && a.bias && a.chunk_stats, "ocf_gather_decoder: flag/val/h/bias/chunk_stats required");
+  OCF_CHECK(a.h_dtype == a.w_dtype, "ocf_gather_decoder: h and W must share the compute dtype");
+  if (a.n_chunks == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  int G, ppl;
+  if (a.w_dtype == OCF_F32) { shape_or_throw<float>(a, G, ppl); by_shape<Dec<float, float>::L>(G, ppl, a, s); }
+  else if (a.w_dtype == OCF_F16) {
+    shape_or_throw<_Float16>(a, G, ppl);
+    by_shape<Dec<_Float16, _Float16>::L>(G, ppl, a, s);
+  } else {
+    shape_or_throw<__bf16>(a, G, ppl);
+    by_shape<Dec<__bf16, __bf16>::L>(G, ppl, a, s);
+  }
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+extern "C" int ocf_rows_reduce(const OcfRowsReduceArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfRowsReduceArgs& a = *args;
+  OCF_CHECK(a.part && a.row_cptr && a.H > 0 && a.B <= a.Bp, "ocf_rows_reduce: bad arguments");
+  OCF_CHECK(a.mode != OCF_REDUCE_RAW || a.out, "ocf_rows_reduce: RAW needs out");
+  OCF_CHECK(a.mode == OCF_REDUCE_RAW || a.h_out, "ocf_rows_reduce: BIAS_ACT / GRAD_ACT need h_out");
+  OCF_CHECK(!a.chunk_stats || a.stats_part, "ocf_rows_reduce: chunk_stats needs stats_part");
+  if (a.Bp == 0) return 0;
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3(a.Bp), dim3(256), 0, (hipStream_t)stream, a);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+// output-bias gradient from a dense delta: db[n] = gscale * sum_{b < B} d[b][n] (fixed order)
+namespace ocf {
+__global__ void __launch_bounds__(256) colsum_kernel(const void* d, int dtype, int64_t ld, int B, int N, float gscale,
+                                                     float* out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s0 = 0.f, s1 = 0.f;
+  int b = 0;
+  for (; b + 2 <= B; b += 2) {
+    s0 += load_ct(d, dtype, (int64_t)b * ld + n);
+    s1 += load_ct(d, dtype, (int64_t)(b + 1) * ld + n);
+  }
+  if (b < B) s0 += load_ct(d, dtype, (int64_t)b * ld + n);
+  out[n] = (s0 + s1) * gscale;
+}
+}  // namespace ocf
+
+extern "C" int ocf_colsum(const void* d, int dtype, int64_t ld, int B, int N, float gscale, float* out, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(d && out && ld >= N, "ocf_colsum: bad arguments");
+  if (N == 0) return 0;
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, d, dtype, ld, B, N, gscale,
+                     out);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}

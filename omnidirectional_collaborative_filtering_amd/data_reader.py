@@ -26,6 +26,7 @@ from .dataset import FixedSplit, load_reference_json
 from .engine import TILE, cur_stream, ptr, ru
 
 AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
+GATHER_CHUNK = 256     # entries per row-gather work unit (ocf_gather_*)
 
 
 class _DeviceCSR:
@@ -186,6 +187,9 @@ class BatchGenerator(object):
         if self.src2 is not None:
             self.tlocal = self.src2.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)
             self.lboff2_dev = torch.as_tensor(self._local_offsets(self.src2.lens, rows), device=r.device)
+        # row-gather chunk tables (inputs from source 1; targets from source 1 in training, else source 2)
+        self.chunks1 = self._chunk_tables(self.src1.lens, rows, r.device)
+        self.chunks2 = self.chunks1 if self.src2 is None else self._chunk_tables(self.src2.lens, rows, r.device)
         self.keep_dev = None
         self.keep_off = None
         if keep is not None:
@@ -193,6 +197,42 @@ class BatchGenerator(object):
             self.keep_off = np.concatenate([[0], np.cumsum(self.nnz_full)])
         self.max_targets = int(max(self.nnz1.max() if nb else 0,
                                    self.tlocal.max() if (self.src2 is not None and nb) else 0))
+
+    @staticmethod
+    def _chunk_tables(lens, rows, dev, chunk=GATHER_CHUNK):
+        """Every batch's rows cut into chunks of <= `chunk` entries: (batch row, first, end local entry)
+        per chunk, [nb][B+1] first chunk of each row (relative to the batch), per-batch chunk base."""
+        nb, B = rows.shape
+        L = lens[rows].astype(np.int64).reshape(-1)                  # [nb*B]
+        nc = (L + chunk - 1) // chunk
+        row_cptr = np.zeros((nb, B + 1), dtype=np.int32)
+        np.cumsum(nc.reshape(nb, B), axis=1, out=row_cptr[:, 1:])
+        cbase = np.zeros(nb + 1, dtype=np.int64)
+        np.cumsum(row_cptr[:, -1], out=cbase[1:])
+        tot = int(cbase[-1])
+        rep = np.repeat(np.arange(nb * B, dtype=np.int64), nc)
+        first = np.repeat(np.cumsum(nc) - nc, nc)
+        k = np.arange(tot, dtype=np.int64) - first
+        j0 = k * chunk
+        j1 = np.minimum(j0 + chunk, L[rep])
+        t = lambda x: torch.as_tensor(np.ascontiguousarray(x, dtype=np.int32), device=dev)
+        return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase)
+
+    def gather_tables(self, bi):
+        """pointer sets for the row-gather kernels of batch bi: 'enc' (source-1 inputs) and 'dec'
+        (the target CSR)"""
+        B = self.B
+        out = {}
+        for key, src, ch, lb in (("enc", self.src1, self.chunks1, self.lboff1_dev),
+                                 ("dec", self.src1 if self.src2 is None else self.src2, self.chunks2,
+                                  self.lboff1_dev if self.src2 is None else self.lboff2_dev)):
+            c0 = int(ch["cbase"][bi])
+            out[key] = dict(rows=self.rows_dev.data_ptr() + 4 * bi * B, rp=ptr(src.rp), col=ptr(src.col),
+                            val=ptr(src.val), lboff=lb.data_ptr() + 8 * bi * (B + 1),
+                            ch_row=ch["ch_row"].data_ptr() + 4 * c0, ch_j0=ch["ch_j0"].data_ptr() + 4 * c0,
+                            ch_j1=ch["ch_j1"].data_ptr() + 4 * c0, n_chunks=int(ch["cbase"][bi + 1]) - c0,
+                            row_cptr=ch["row_cptr"].data_ptr() + 4 * bi * (B + 1))
+        return out
 
     @staticmethod
     def _local_offsets(lens, rows):

@@ -226,6 +226,20 @@ class Engine:
         # non-temporal loads for operands at their last use in the step (A/B switch)
         self.nt_operands = False   # measured neutral-to-worse: nt loads forfeit Infinity-Cache hits
         self.tseg = None            # row-segment target descriptor of the loaded batch (None: buckets)
+        # row-gather (sparse batch) path: chunk tables of the loaded batch (None: dense GEMM path)
+        self.gt = None
+        self.sparse_ok = self.k == 1 and self.Hp[0] <= 512 and self.Hp[-1] <= 512
+        self.use_sparse = True
+        # dW_out / dW_in operand A: built in LDS from the entries (sparse A, ocf.h a_sparse; no dense
+        # [B][N] arrays, no memsets) or the dense d_out / xin.  Measured on ML-20M: 0.747 vs 0.756 ms/step.
+        self.sparse_dw = True
+        self._gbuf = {}
+        HpL = self.Hp[-1]
+        self.db_rows = torch.zeros(Bp, HpL, device=d, dtype=torch.float32)      # hidden-bias grad rows
+        self.dh_raw = torch.zeros(Bp, HpL, device=d, dtype=torch.float32)       # decoder RAW reduce target
+        self.stats_rows = torch.zeros(Bp, 4, device=d, dtype=torch.float32)
+        self.row_sse_rows = torch.zeros(Bp, device=d, dtype=torch.float32)
+        self.db_out_col = torch.zeros(1, self.Np, device=d, dtype=torch.float32)
         gm = Bp // TILE
         self.stats_part = torch.zeros(self.n_tiles * gm * 4, device=d, dtype=torch.float32)
         self.row_sse_part = torch.zeros(self.n_tiles * Bp, device=d, dtype=torch.float32)
@@ -306,6 +320,14 @@ class Engine:
         s = max(1, min(ksteps // 8, max(1, 512 // tiles)))
         return s
 
+    def _buf(self, name, n, dtype=torch.float32):
+        """grow-only device scratch"""
+        t = self._gbuf.get(name)
+        if t is None or t.numel() < n:
+            t = torch.zeros(max(n, 1 << 12), device=self.dev, dtype=dtype)
+            self._gbuf[name] = t
+        return t
+
     def _grow_buckets(self, n):
         if n <= self.bk_cap:
             return
@@ -347,7 +369,7 @@ class Engine:
         a.s0 = a.s1 = 1.0
         return a
 
-    def load_batch(self, a, targets, owner=None):
+    def load_batch(self, a, targets, owner=None, gather=None):
         """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller).
 
         ``targets`` (BatchGenerator.targets) names the target CSR's tile index: the scatter marks
@@ -363,6 +385,13 @@ class Engine:
         seg = {k: v for k, v in targets.items() if k.startswith("t_")}
         seg["t_flag"] = self.tflag
         self.tseg = seg
+        self.gt = None
+        if gather is not None and self.sparse_ok and self.use_sparse:
+            xval = self._buf("xval", int(a.E1))
+            a.xval1 = ptr(xval)
+            if self.sparse_dw:
+                a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
+            self.gt = dict(gather, xval=xval, aux=float(targets["t_aux"]), E=int(targets["E"]))
         with self.phase("scatter"):
             if self._xin_prev is not None:
                 call("ocf_scatter_clear", self._xin_prev[0], cur_stream())
@@ -431,43 +460,124 @@ class Engine:
         # layer 0: split-K over the (k x Np)-wide input
         Hp0 = self.Hp[0]
         sstride = Bp * Hp0
-        with self.phase("enc_gemm"):
-            self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
-                       _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride,
-                       b_nt=int(self.nt_operands), b_blocked=self._wblk(0))
+        if self.gt is not None:
+            self._forward_gather(keep, stream_id)
+        else:
+            with self.phase("enc_gemm"):
+                self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
+                           _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride,
+                           b_nt=int(self.nt_operands), b_blocked=self._wblk(0))
         src, nsplit = self.slabs, self.splits0
-        if self.comm is not None:
+        if self.gt is not None and self.comm is None:
+            pass                      # fused bias/activation/dropout already applied by the row reduce
+        elif self.gt is not None:
+            with self.phase("allreduce_fwd"):
+                self.comm(self.hpre)
+            call("ocf_splitk_bias_act", ptr(self.hpre), 1, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
+                 keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
+                 ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
+        elif self.comm is not None:
             # partial pre-activation over this rank's columns -> sum over ranks -> activation
             call("ocf_splitk_bias_act", ptr(self.slabs), self.splits0, sstride, Bp, Hp0, Hp0, ptr(self.zero_bias),
                  _lib.ACT["linear"], 1.0, 0, 0, None, None, ptr(self.hpre), None, self.cdt, Bp, Hp0, s)
             with self.phase("allreduce_fwd"):
                 self.comm(self.hpre)
             src, nsplit = self.hpre, 1
-        call("ocf_splitk_bias_act", ptr(src), nsplit, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
-             keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
-             ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
+        if self.gt is None:
+            call("ocf_splitk_bias_act", ptr(src), nsplit, sstride, Bp, Hp0, Hp0, ptr(self.b[0]), self.act,
+                 keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
+                 ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
         for i in range(1, L):
             self._gemm(self.h[i - 1], 0, self.Hp[i - 1], self.W[i], _lib.DT_F32, 1, self.Hp[i], Bp, self.Hp[i],
                        self.Hp[i - 1], _lib.EPI_BIAS_ACT, bias=self.b[i], act=self.act, keep=keep, seed=self.seed,
                        stream=stream_id + i, mask_out=self.mask[i] if keep < 1 else None, a_out=self.a[i],
                        h_out=self.h[i], h_dtype=self.cdt, ld_out=self.Hp[i], m_real=self.B, n_real=self.H[i])
 
+    # ---------------------------------------------------------------- row-gather (sparse batch) path
+    def _gather_args(self, tab, layer, part, n_cols):
+        g = _lib.OcfGatherArgs()
+        for k in ("rows", "rp", "col", "val", "lboff", "ch_row", "ch_j0", "ch_j1", "n_chunks"):
+            setattr(g, k, tab[k])
+        Wt, wdt = self._wop(layer)
+        g.W, g.w_dtype, g.ldw, g.w_blocked = ptr(Wt), wdt, Wt.shape[1], self._wblk(layer)
+        g.H = n_cols
+        g.part = ptr(part)
+        return g
+
+    def _reduce_args(self, tab, part, H, mode):
+        r = _lib.OcfRowsReduceArgs()
+        r.part, r.row_cptr, r.B, r.Bp, r.H, r.mode = ptr(part), tab["row_cptr"], self.B, self.Bp, H, mode
+        return r
+
+    def _forward_gather(self, keep, stream_id):
+        """layer 0 as a row gather over the batch's live input entries + fused bias/act/dropout"""
+        tab = self.gt["enc"]
+        Hp0 = self.Hp[0]
+        part = self._buf("part_enc", tab["n_chunks"] * Hp0)
+        with self.phase("enc_gemm"):
+            g = self._gather_args(tab, 0, part, Hp0)
+            g.xval = ptr(self.gt["xval"])
+            call("ocf_gather_encoder", g, cur_stream())
+            if self.comm is not None:            # partial over this rank's columns -> all-reduce
+                r = self._reduce_args(tab, part, Hp0, _lib.REDUCE_RAW)
+                r.out = ptr(self.hpre)
+            else:
+                r = self._reduce_args(tab, part, Hp0, _lib.REDUCE_BIAS_ACT)
+                r.bias, r.act, r.keep, r.seed, r.stream = ptr(self.b[0]), self.act, keep, self.seed, stream_id
+                r.mask_out = ptr(self.mask[0]) if keep < 1 else None
+                r.a_out, r.h_out, r.h_dtype, r.n_real = ptr(self.a[0]), ptr(self.h[0]), self.cdt, self.H[0]
+            call("ocf_rows_reduce", r, cur_stream())
+
+    def _output_gather(self, with_grad, gscale):
+        """decoder at the live targets: y, loss/metric sums, delta, and delta x W_out rows -> the last
+        hidden layer's delta (through its activation and dropout) in the same pass"""
+        L = len(self.H)
+        HpL = self.Hp[L - 1]
+        tab = self.gt["dec"]
+        part = self._buf("part_dec", tab["n_chunks"] * HpL)
+        cst = self._buf("chunk_stats", tab["n_chunks"] * 4)
+        g = self._gather_args(tab, L, part, HpL)
+        g.flag = ptr(self.tflag)
+        g.h, g.h_dtype, g.bias, g.aux = ptr(self.h[L - 1]), self.cdt, ptr(self.b[L]), self.gt["aux"]
+        g.chunk_stats = ptr(cst)
+        if with_grad and self.sparse_dw:
+            g.delta_e = ptr(self._buf("delta_e", self.gt["E"]))
+        elif with_grad:               # dense delta for the output-layer weight-gradient GEMM
+            self.d_out.zero_()
+            g.d_out, g.d_dtype, g.ld_d = ptr(self.d_out), self.cdt, self.Np
+        call("ocf_gather_decoder", g, cur_stream())
+        if with_grad and self.comm is None:
+            r = self._reduce_args(tab, part, HpL, _lib.REDUCE_GRAD_ACT)
+            r.a_in = ptr(self.a[L - 1])
+            r.mask_in = ptr(self.mask[L - 1]) if self.keep < 1 else None
+            r.act, r.keep, r.h_out, r.h_dtype, r.n_real = self.act, self.keep, ptr(self.dh[L - 1]), self.cdt, self.H[L - 1]
+            r.db_part, r.gscale = ptr(self.db_rows), gscale
+        else:
+            r = self._reduce_args(tab, part, HpL, _lib.REDUCE_RAW)
+            r.out = ptr(self.dhpre if (with_grad and self.comm is not None) else self.dh_raw)
+        r.chunk_stats, r.stats_part, r.row_sse = ptr(cst), ptr(self.stats_rows), ptr(self.row_sse_rows)
+        call("ocf_rows_reduce", r, cur_stream())
+
     def output_loss(self, with_grad):
-        """Decoder GEMM with the fused masked-MSE epilogue; stats -> stats_hist[n_stats]."""
+        """Decoder (dense GEMM with the fused masked-MSE epilogue, or the row gather for sparse
+        batches); stats -> stats_hist[n_stats]."""
         L = len(self.H)
         gscale = 2.0 / (self.B * self.N_total)
         with self.phase("dec_gemm_mse"):
-            self._gemm_mse(L, gscale, with_grad)
+            if self.gt is not None:
+                self._output_gather(with_grad, gscale)
+                sp, n_sp, rs, n_rs = self.stats_rows, self.Bp, self.row_sse_rows, 1
+            else:
+                self._gemm_mse(L, gscale, with_grad)
+                sp, n_sp, rs, n_rs = self.stats_part, self.n_tiles * (self.Bp // TILE), self.row_sse_part, self.n_tiles
         self._grow_stats(self.n_stats + 1)
         dst = self.stats_hist[self.n_stats]
         if self.side is not None:
             self._fork()
             with torch.cuda.stream(self.side):
-                call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE),
-                     ptr(self.row_sse_part), self.n_tiles, self.Bp, ptr(dst), cur_stream())
+                call("ocf_stats_finalize", ptr(sp), n_sp, ptr(rs), n_rs, self.Bp, ptr(dst), cur_stream())
         else:
-            call("ocf_stats_finalize", ptr(self.stats_part), self.n_tiles * (self.Bp // TILE), ptr(self.row_sse_part),
-                 self.n_tiles, self.Bp, ptr(dst), cur_stream())
+            call("ocf_stats_finalize", ptr(sp), n_sp, ptr(rs), n_rs, self.Bp, ptr(dst), cur_stream())
         self.n_stats += 1
 
     def _gemm_mse(self, L, gscale, with_grad):
@@ -500,6 +610,8 @@ class Engine:
         fused = grads_out is None
         op = self.opt.step_params(1.0, self.l2) if fused else None
         self._bias_op = self.opt.step_params(1.0, 0.0) if fused else None   # l2 regularises kernels only
+        if self.gt is not None:
+            return self._backward_gather(grads_out, op, gscale)
         # delta of the last hidden layer: split-K over Np
         HpL = self.Hp[L - 1]
         sstride = Bp * HpL
@@ -555,6 +667,80 @@ class Engine:
         with self.phase("dW_in"):
             self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0],
                                 self.Hp[0], gscale, grads_out, op)
+        if fused:
+            self.opt.iterations += 1
+
+    def _weight_update_sparse(self, i, vals, Bm, ldb, N, gscale, grads_out, op, colsum=None):
+        """EPI_OPTIM / EPI_GRAD for a first/last layer whose A operand (the batch entries: deltas or
+        inputs, [B][N] transposed) is built in LDS from the target CSR's column-sorted view"""
+        if grads_out is None and not self.trainable[i]:
+            return
+        M, K = self.Np, self.Bp
+        if self.sparse_dw:
+            t = self.tseg
+            sp = dict(a_sparse=1, sp_rows=t["t_rows"], sp_rp=t["t_rp"], sp_tptr=t["t_tptr"], sp_col=t["t_col"],
+                      sp_lidx=t["t_lidx"], sp_lboff=t["t_lboff"], sp_vals=vals, sp_ntiles=t["t_ntiles"],
+                      sp_krows=self.B, sp_colsum=colsum)
+            A = Bm                    # not read (sparse A); any valid pointer
+        else:                         # dense operand: the decoder's delta or the scattered layer-0 input
+            sp = dict(sp_colsum=colsum)
+            A = self.d_out if i == len(self.W) - 1 else self.xin
+        if grads_out is None:
+            sw, _ = self.slots[i]
+            o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
+            self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp)
+        else:
+            self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
+                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), **sp)
+
+    def _backward_gather(self, grads_out, op, gscale):
+        """backward after the row-gather decoder: the last hidden delta already exists (single GPU) or
+        its partial sum does (feature parallel: all-reduce, then activation/dropout)"""
+        s = cur_stream()
+        L, Bp = len(self.H), self.Bp
+        HpL = self.Hp[L - 1]
+        fused = grads_out is None
+        if self.comm is not None:
+            with self.phase("allreduce_bwd"):
+                self.comm(self.dhpre)
+            call("ocf_splitk_grad_act", ptr(self.dhpre), 1, Bp * HpL, Bp, HpL, HpL, ptr(self.a[L - 1]),
+                 ptr(self.mask[L - 1]), self.keep, self.act, ptr(self.dh[L - 1]), self.cdt, ptr(self.db_h[L - 1][0]),
+                 gscale, self.B, self.H[L - 1], s)
+            db_last, parts_last = self.db_h[L - 1], Bp // 4
+        else:
+            db_last, parts_last = self.db_rows, Bp
+        delta = self._buf("delta_e", self.gt["E"]) if self.sparse_dw else None
+        xval = self.gt["xval"]
+        if fused and L == 1 and self.comm is None and self.side is not None:
+            self._fork()
+            with torch.cuda.stream(self.side):
+                self._bias_update(0, db_last, parts_last, HpL, HpL, grads_out, op)
+            with self.phase("dW_out"):        # also the output-bias gradient (column sums of the deltas)
+                self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col)
+            self._fork()
+            with torch.cuda.stream(self.side):
+                self._bias_update(1, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+            with self.phase("dW_in"):
+                self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
+            self.opt.iterations += 1
+            return
+        with self.phase("dW_out"):
+            self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op, self.db_out_col)
+        self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+        for i in range(L - 1, 0, -1):
+            self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
+                       self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
+                       act=self.act, h_out=self.dh[i - 1], h_dtype=self.cdt, ld_out=self.Hp[i - 1],
+                       db_part=self.db_h[i - 1], opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
+                       m_real=self.B, n_real=self.H[i - 1])
+            self._bias_update(i, db_last, parts_last, self.Hp[i], self.Hp[i], grads_out, op)
+            self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
+                                self.Hp[i], gscale, grads_out, op)
+            db_last, parts_last = self.db_h[i - 1], Bp // TILE
+        self._bias_update(0, db_last, parts_last, self.Hp[0], self.Hp[0], grads_out, op)
+        with self.phase("dW_in"):
+            self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
         if fused:
             self.opt.iterations += 1
 

@@ -122,7 +122,7 @@ class Model(object):
         e = self.engine
         if gen is not None:
             args = gen.scatter_args(bi, engine_args=e.scatter_args())
-            e.load_batch(args, gen.targets(bi, e.N), owner=gen)
+            e.load_batch(args, gen.targets(bi, e.N), owner=gen, gather=gen.gather_tables(bi))
             return gen.target_count(bi)
         x, y = item[0], item[1]
         blocks, out_mask = self._split_inputs(x)

@@ -42,10 +42,16 @@ def test_library_exports_every_symbol():
 STRUCTS = {
     "OcfOptParams": (_lib.OcfOptParams, ["kind", "lr", "gscale"]),
     "OcfScatterArgs": (_lib.OcfScatterArgs, ["keep1", "s0", "seed", "mode", "rows2", "aux", "ld", "xin_dtype",
-                                             "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean"]),
+                                             "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean",
+                                             "xval1"]),
+    "OcfGatherArgs": (_lib.OcfGatherArgs, ["rows", "n_chunks", "ldw", "w_blocked", "H", "part", "aux", "delta_e",
+                                           "ld_d"]),
+    "OcfRowsReduceArgs": (_lib.OcfRowsReduceArgs, ["mode", "out", "keep", "seed", "stream", "n_real", "gscale",
+                                                   "row_sse"]),
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
                                        "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part", "t_rows", "t_lboff", "t_ntiles",
-                                       "t_aux", "p_shadow", "b_nt", "shadow_blocked"]),
+                                       "t_aux", "p_shadow", "b_nt", "shadow_blocked", "a_sparse",
+                                       "sp_lboff", "sp_krows", "sp_colsum"]),
 }
 
 

@@ -61,9 +61,11 @@ def test_dense_train_on_batch_equals_generator_path(gpu):
         _, m_out, x, t, _ = scatter_rows_numpy(data.train.row_ptr, data.train.col, data.train.val, gen.rows_host[bi],
                                                N, aux=-1.0)
         lbs.append(b.train_on_batch([x, m_out], t))
-    assert abs(la - np.mean(lbs)) <= 1e-6 * abs(la)
+    # the generator path computes the first and last layers as row gathers over the batch's rating
+    # entries, the dense path as MFMA GEMMs: the same fp32 sums in another order
+    assert abs(la - np.mean(lbs)) <= 1e-5 * abs(la)
     for wa, wb in zip(a.get_weights(), b.get_weights()):
-        np.testing.assert_array_equal(wa, wb)
+        np.testing.assert_allclose(wa, wb, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.gpu
