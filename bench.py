@@ -55,8 +55,9 @@ def parse():
                          "numerics of a partial model); not a bench line")
     ap.add_argument("--sparse-clear", type=int, default=0,
                     help="clear the previous batch's layer-0 entries instead of a dense memset")
-    ap.add_argument("--sparse-dw", type=int, default=1,
-                    help="weight-gradient GEMMs build their batch operand in LDS from the entries")
+    ap.add_argument("--sparse-dw", type=int, default=-1,
+                    help="weight-gradient GEMMs build their batch operand in LDS from the entries (-1: engine's "
+                         "choice by batch size)")
     ap.add_argument("--gather", type=int, default=1,
                     help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
     ap.add_argument("--nt-operands", type=int, default=0,
@@ -146,7 +147,8 @@ def main():
     eng = om.engine
     eng.sparse_clear = bool(args.sparse_clear)
     eng.nt_operands = bool(args.nt_operands)
-    eng.sparse_dw = bool(args.sparse_dw)
+    if args.sparse_dw >= 0:
+        eng.sparse_dw = bool(args.sparse_dw)
     eng.use_sparse = bool(args.gather)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()

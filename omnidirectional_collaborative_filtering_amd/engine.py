@@ -231,8 +231,10 @@ class Engine:
         self.sparse_ok = self.k == 1 and self.Hp[0] <= 512 and self.Hp[-1] <= 512
         self.use_sparse = True
         # dW_out / dW_in operand A: built in LDS from the entries (sparse A, ocf.h a_sparse; no dense
-        # [B][N] arrays, no memsets) or the dense d_out / xin.  Measured on ML-20M: 0.747 vs 0.756 ms/step.
-        self.sparse_dw = True
+        # [B][N] arrays, no memsets) or the dense d_out / xin.  The sparse fill pays a chain of dependent
+        # index loads per K-step, so it wins only for short K loops: ML-20M, 1 GPU (K = 256): 0.774 vs
+        # 0.811 ms/step; 8-way feature parallel (K = 2,048 global rows): 0.538 vs 0.389 ms/step.
+        self.sparse_dw = Bp <= 256
         self._gbuf = {}
         HpL = self.Hp[-1]
         self.db_rows = torch.zeros(Bp, HpL, device=d, dtype=torch.float32)      # hidden-bias grad rows
