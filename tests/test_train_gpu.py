@@ -32,7 +32,8 @@ def _our_opt(name):
             "adam": lambda: O.Adam(lr=0.001)}[name]()
 
 
-def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_type=None, causal=False):
+def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_type=None, causal=False,
+               gather=True, sparse_dw=None):
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     data = _dataset()
@@ -42,6 +43,9 @@ def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_
     om = omni_model(layers, H, N, B, dense_activation=act, use_causal_info=causal, compute_dtype=compute_dtype,
                     seed=11)
     m = om.model
+    om.engine.use_sparse = gather
+    if sparse_dw is not None:
+        om.engine.sparse_dw = sparse_dw
     m.compile(_our_opt(opt_name), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
     w0 = m.get_weights()
     gen = rd.data_gen(B, [1.0, 1.0], "train", True, aux_type, -1, pass_through_input_training=True)
@@ -105,3 +109,17 @@ def test_low_precision_close(gpu, cd, tol):
     loss_g, loss_o, r_g, r_o, w, ora = run_parity(cd, "adagrad", 1, "sigmoid")
     assert abs(loss_g - loss_o) <= tol * abs(loss_o), (loss_g, loss_o)
     assert abs(r_g - r_o) <= tol * r_o, (r_g, r_o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather,sparse_dw", [(False, None), (True, False), (True, True)])
+def test_fp32_parity_operand_paths(gpu, gather, sparse_dw):
+    """The three first/last-layer operand paths of the generator step -- dense MFMA GEMMs
+    (gather off), row gathers with dense weight-gradient operands (the feature-parallel global
+    batch), row gathers with sparse-A weight gradients (short K) -- each meet the fp32 bar."""
+    loss_g, loss_o, r_g, r_o, w, ora = run_parity("float32", "adagrad", 1, "sigmoid", gather=gather,
+                                                 sparse_dw=sparse_dw)
+    assert abs(loss_g - loss_o) <= 1e-5 * abs(loss_o), (loss_g, loss_o)
+    assert abs(r_g - r_o) <= 1e-5, (r_g, r_o)
+    for wg, wo in zip(w[0::2], ora.W):
+        assert np.quantile(np.abs(wg - wo), 0.999) < 1e-5

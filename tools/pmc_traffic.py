@@ -4,9 +4,11 @@ Usage: python tools/pmc_traffic.py FETCH_counter_collection.csv WRITE_counter_co
 
 Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B streaming
-stores.  Both counters are in KiB.  The two GEMM kernels that run twice per step share a symbol, so
-phases are assigned by launch order within the step: SLAB GEMMs alternate enc_gemm / dec_bwd_gemm,
-OPTIM GEMMs alternate dW_out / dW_in.  Values are mean bytes per launch over the profiled steps
+stores.  Both counters are in KiB.  Kernels that run twice per step share a symbol, so phases are
+assigned by launch order within the step: SLAB GEMMs alternate enc_gemm / dec_bwd_gemm (dense path),
+row reductions alternate enc_reduce / dec_reduce (row-gather path), OPTIM GEMMs alternate
+dW_out / dW_in.  Row-gather path: gather_encoder -> enc_gemm, gather_decoder -> dec_gemm_mse (the
+phase names the engine's timers use).  Values are mean bytes per launch over the profiled steps
 (warm-up launches included; they move the same bytes)."""
 import csv
 import json
@@ -25,6 +27,13 @@ def per_dispatch(path, counter):
 
 
 def phase_of(name, seen):
+    if "gather_encoder" in name:
+        return "enc_gemm"
+    if "gather_decoder" in name:
+        return "dec_gemm_mse"
+    if "rows_reduce" in name:
+        k = seen["red"] = seen.get("red", -1) + 1
+        return ("enc_reduce", "dec_reduce")[k % 2]
     if "EpiMaskedMSE" in name:
         return "dec_gemm_mse"
     if "EpiSlab" in name:
