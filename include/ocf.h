@@ -217,6 +217,20 @@ typedef struct OcfGemmArgs {
   const int32_t* sp_lidx; const int64_t* sp_lboff; const float* sp_vals;
   int sp_ntiles, sp_krows;
   float* sp_colsum;
+  /* optional (OPTIM, 16-bit compute): the same sparse A bucketed by (M tile, K-step) by
+   * ocf_sparse_tiles (sp_bptr [M/128 * K/64 + 1], sp_ent pairs (value index, k | m_local << 8));
+   * with them the persistent role-split kernel runs (ocf_set_tuning "optim_ws") */
+  const int32_t* sp_bptr; const int32_t* sp_ent;
+  /* OPTIM: small jobs of the step done by the same launch (folded into the persistent kernel, else
+   * launched separately on the same stream), each nullable by its first pointer:
+   *   cb_p: bias optimizer on the sp_colsum outputs (the output-layer bias: cb_p[m] for m < M),
+   *         = ocf_bias_opt_from_partials(cb_p, sp_colsum, 1, M, M, cb_s1, cb_s2, NULL, &cb_op)
+   *   jb_part: = ocf_bias_opt_from_partials(jb_p, jb_part, jb_parts, jb_ld, jb_n, jb_s1, jb_s2, NULL, &jb_op)
+   *   js_sp: = ocf_stats_finalize(js_sp, js_nparts, js_rs, js_ntiles, js_M, js_out) */
+  float* cb_p; float* cb_s1; float* cb_s2; OcfOptParams cb_op;
+  const float* jb_part; int jb_parts, jb_n; int64_t jb_ld; float* jb_p; float* jb_s1; float* jb_s2;
+  OcfOptParams jb_op;
+  const float* js_sp; const float* js_rs; float* js_out; int js_nparts, js_ntiles, js_M;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
@@ -243,6 +257,29 @@ int ocf_bias_opt_from_partials(float* b, const float* db_part, int parts, int64_
 /* reduce OCF_EPI_MASKED_MSE partials to out[4 + M] = {sse, sae, nnz(T+yhat), 0, row_sse[M]}. */
 int ocf_stats_finalize(const float* stats_part, int n_parts, const float* row_sse_part, int n_tiles, int M,
                        float* out, void* stream);
+
+/* ocf_sparse_tiles -- bucket a batch's sparse A operand (the OcfGemmArgs sp_* descriptor) by
+ * (M tile t < gm, K-step kt < nk): bucket t*nk + kt holds, for the batch rows b in [64 kt, 64 kt + 64)
+ * in order and each row's entries of tile t in column order, the pair (sp_lboff[b] + lidx,
+ * (b - 64 kt) | (col - 128 t) << 8).  Deterministic (no atomics).  cnt: scratch [gm*nk]; bptr:
+ * [gm*nk + 1]; ent: [cap][2] with cap >= the batch's entries in tiles < gm.  Built once per batch
+ * and shared by both weight-gradient GEMMs (train split: inputs and targets share the descriptor).
+ * Extension (no reference counterpart): feeds the persistent dW kernel. */
+typedef struct OcfTileBucketArgs {
+  const int32_t* rows; const int64_t* rp; const int32_t* tptr; const int32_t* col; const int32_t* lidx;
+  const int64_t* lboff;
+  int krows, ntiles, gm, nk;
+  int32_t* cnt; int32_t* bptr; int32_t* ent;
+  int64_t cap;
+} OcfTileBucketArgs;
+int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
+
+/* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
+ *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on
+ *               [K][M] x [K][N] operands with 16-bit compute run on the persistent role-split kernel
+ *               (ocf_optim_ws.h); 0 = the generic tile kernel.  Bit-identical results.
+ * previous (nullable) receives the old value. */
+int ocf_set_tuning(const char* key, int value, int* previous);
 
 int ocf_version(void);
 const char* ocf_last_error(void);

@@ -84,6 +84,19 @@ class OcfGemmArgs(ctypes.Structure):
         ("p_shadow", P), ("a_nt", I32), ("b_nt", I32), ("b_blocked", I32), ("shadow_blocked", I32),
         ("a_sparse", I32), ("sp_rows", P), ("sp_rp", P), ("sp_tptr", P), ("sp_col", P), ("sp_lidx", P),
         ("sp_lboff", P), ("sp_vals", P), ("sp_ntiles", I32), ("sp_krows", I32), ("sp_colsum", P),
+        ("sp_bptr", P), ("sp_ent", P),
+        ("cb_p", P), ("cb_s1", P), ("cb_s2", P), ("cb_op", OcfOptParams),
+        ("jb_part", P), ("jb_parts", I32), ("jb_n", I32), ("jb_ld", I64), ("jb_p", P), ("jb_s1", P), ("jb_s2", P),
+        ("jb_op", OcfOptParams),
+        ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
+    ]
+
+
+class OcfTileBucketArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
+        ("krows", I32), ("ntiles", I32), ("gm", I32), ("nk", I32),
+        ("cnt", P), ("bptr", P), ("ent", P), ("cap", I64),
     ]
 
 
@@ -103,6 +116,8 @@ SIGNATURES = {
     "ocf_gather_decoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
     "ocf_rows_reduce": (I32, [ctypes.POINTER(OcfRowsReduceArgs), P]),
     "ocf_colsum": (I32, [P, I32, I64, I32, I32, F32, P, P]),
+    "ocf_sparse_tiles": (I32, [ctypes.POINTER(OcfTileBucketArgs), P]),
+    "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

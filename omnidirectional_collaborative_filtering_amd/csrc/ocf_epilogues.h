@@ -41,28 +41,36 @@ __device__ __forceinline__ void for_each_acc(ocf_f16v (&acc)[2][2], const TileCt
 }
 
 // ---- optimizer update (Keras 2.0.4 get_updates, float32 op order) ---------------------
-__device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float& p, float& s1, float& s2) {
+// KIND fixed at compile time where a kernel is specialised per optimizer (optim_ws_kernel: a
+// quarter of the code of the runtime switch below, which matters for the instruction cache)
+template <int KIND>
+__device__ __forceinline__ void opt_update_k(const OcfOptParams& o, float g, float& p, float& s1, float& s2) {
   if (o.l2 != 0.f) g = g + 2.0f * o.l2 * p;
+  if constexpr (KIND == OCF_OPT_ADAGRAD) {        // a += g^2 ; p -= lr*g/(sqrt(a)+eps)
+    float a = s1 + g * g;
+    s1 = a;
+    p = p - (o.lr * g) / (sqrtf(a) + o.eps);
+  } else if constexpr (KIND == OCF_OPT_RMSPROP) { // a = rho*a + (1-rho)*g^2
+    float a = o.rho * s1 + (1.0f - o.rho) * (g * g);
+    s1 = a;
+    p = p - (o.lr * g) / (sqrtf(a) + o.eps);
+  } else if constexpr (KIND == OCF_OPT_ADAM) {    // m,v EMAs; p -= lr_t*m/(sqrt(v)+eps)
+    float m = o.rho * s1 + (1.0f - o.rho) * g;
+    float v = o.beta2 * s2 + (1.0f - o.beta2) * (g * g);
+    s1 = m;
+    s2 = v;
+    p = p - (o.lr * m) / (sqrtf(v) + o.eps);
+  } else {
+    (void)s1; (void)s2;
+    p = p - o.lr * g;
+  }
+}
+__device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float& p, float& s1, float& s2) {
   switch (o.kind) {
-    case OCF_OPT_ADAGRAD: {           // a += g^2 ; p -= lr*g/(sqrt(a)+eps)
-      float a = s1 + g * g;
-      s1 = a;
-      p = p - (o.lr * g) / (sqrtf(a) + o.eps);
-    } break;
-    case OCF_OPT_RMSPROP: {           // a = rho*a + (1-rho)*g^2
-      float a = o.rho * s1 + (1.0f - o.rho) * (g * g);
-      s1 = a;
-      p = p - (o.lr * g) / (sqrtf(a) + o.eps);
-    } break;
-    case OCF_OPT_ADAM: {              // m,v EMAs; p -= lr_t*m/(sqrt(v)+eps)
-      float m = o.rho * s1 + (1.0f - o.rho) * g;
-      float v = o.beta2 * s2 + (1.0f - o.beta2) * (g * g);
-      s1 = m;
-      s2 = v;
-      p = p - (o.lr * m) / (sqrtf(v) + o.eps);
-    } break;
-    default:
-      p = p - o.lr * g;
+    case OCF_OPT_ADAGRAD: opt_update_k<OCF_OPT_ADAGRAD>(o, g, p, s1, s2); break;
+    case OCF_OPT_RMSPROP: opt_update_k<OCF_OPT_RMSPROP>(o, g, p, s1, s2); break;
+    case OCF_OPT_ADAM: opt_update_k<OCF_OPT_ADAM>(o, g, p, s1, s2); break;
+    default: opt_update_k<0>(o, g, p, s1, s2);
   }
 }
 

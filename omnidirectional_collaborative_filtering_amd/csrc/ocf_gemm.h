@@ -227,6 +227,8 @@ struct GemmShape {
   int sp_ntiles, sp_krows;   // column tiles per CSR row; batch rows that exist (K beyond is padding)
   float* sp_colsum;          // nullable: out[m] = colsum_scale * sum_k A[k][m] (tile_n == 0 workgroups)
   float colsum_scale;
+  // sparse A bucketed by (column tile, K-step) (ocf_sparse_tiles; optim_ws_kernel)
+  const int32_t* sp_bptr; const int2* sp_ent;
 };
 
 // Fill the A image of one K-step from sparse entries: zero it, then 4 threads per batch row walk the
@@ -258,6 +260,68 @@ __device__ __forceinline__ void sparse_a_fill(const GemmShape& sh, char* img, in
     if (v == 0.f) continue;
     const int m = sh.sp_col[e] - m0;
     *reinterpret_cast<CT*>(img + k * I::STRIDE + m * (int)sizeof(CT)) = CvtT<CT>::to(v);
+  }
+}
+
+// one K-step of the wave's 64x64 sub-tile (2x2 blocks of 32x32) from the LDS operand images
+template <typename CT, bool ACOL, bool BCOL, int RA = GT_BM, int RB = GT_BN>
+__device__ __forceinline__ void mfma_kstep(const char* bufA, const char* bufB, int wm, int wn, int lane,
+                                           ocf_f16v (&acc)[2][2]) {
+  constexpr int BK = KInfo<CT>::BK;
+  if constexpr (sizeof(CT) == 2) {
+#if OCF_FRAG_PREFETCH
+    // all fragments of the K-step first (one LDS latency per step instead of one per 16-deep slice)
+    typename Frag<CT>::T fa[BK / 16][2], fb[BK / 16][2];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[ks][i] = read_frag16<CT, RA, ACOL>(bufA, wm + 32 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[ks][j] = read_frag16<CT, RB, BCOL>(bufB, wn + 32 * j, ks, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (std::is_same<CT, _Float16>::value)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
+        }
+#else
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      typename Frag<CT>::T fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = read_frag16<CT, RA, ACOL>(bufA, wm + 32 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = read_frag16<CT, RB, BCOL>(bufB, wn + 32 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (std::is_same<CT, _Float16>::value)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+    }
+#endif
+  } else {
+    float fa[2][16], fb[2][16];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) read_frag32<RA, ACOL>(bufA, wm + 32 * i, lane, fa[i]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) read_frag32<RB, BCOL>(bufB, wn + 32 * j, lane, fb[j]);
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -324,62 +388,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto compute = [&](const char* bufA) {
-    const char* bufB = bufA + Cfg::ImgA::BYTES;
-    if constexpr (sizeof(CT) == 2) {
-#if OCF_FRAG_PREFETCH
-      // all fragments of the K-step first (one LDS latency per step instead of one per 16-deep slice)
-      typename Frag<CT>::T fa[BK / 16][2], fb[BK / 16][2];
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i) fa[ks][i] = read_frag16<CT, GT_BM, ACOL>(bufA, wm + 32 * i, ks, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[ks][j] = read_frag16<CT, GT_BN, BCOL>(bufB, wn + 32 * j, ks, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            if constexpr (std::is_same<CT, _Float16>::value)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
-            else
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks][i], fb[ks][j], acc[i][j], 0, 0, 0);
-          }
-#else
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        typename Frag<CT>::T fa[2], fb[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) fa[i] = read_frag16<CT, GT_BM, ACOL>(bufA, wm + 32 * i, ks, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = read_frag16<CT, GT_BN, BCOL>(bufB, wn + 32 * j, ks, lane);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            if constexpr (std::is_same<CT, _Float16>::value)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-            else
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-          }
-      }
-#endif
-    } else {
-      float fa[2][16], fb[2][16];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) read_frag32<GT_BM, ACOL>(bufA, wm + 32 * i, lane, fa[i]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) read_frag32<GT_BN, BCOL>(bufB, wn + 32 * j, lane, fb[j]);
-#pragma unroll
-      for (int s = 0; s < 16; ++s)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-    }
+    mfma_kstep<CT, ACOL, BCOL>(bufA, bufA + Cfg::ImgA::BYTES, wm, wn, lane, acc);
   };
   char* buf0 = lds;
   char* buf1 = lds + Cfg::BUF;

@@ -1,10 +1,12 @@
 // ocf_gemm: dispatch of the MFMA GEMM template to the layout / dtype / epilogue combinations the
 // autoencoder step uses ("GEMM inventory").
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
+#include "ocf_optim_ws.h"
 
 using namespace ocf;
 
@@ -39,6 +41,84 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   }
   hipLaunchKernelGGL((gemm_kernel<CT, ACOL, BCOL, CT, BGT, Epi, LDS, SPA>), dim3(ntile, splits), dim3(GT_THREADS), 0, s,
                      sh, ep);
+  OCF_HIP(hipGetLastError());
+}
+
+// tuning switches (ocf_set_tuning); env OCF_OPTIM_WS=0 disables the role-split optimizer kernel
+int g_optim_ws = -1;
+bool optim_ws_on() {
+  if (g_optim_ws < 0) {
+    const char* e = std::getenv("OCF_OPTIM_WS");
+    g_optim_ws = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_optim_ws != 0;
+}
+
+int cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  OCF_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!n[dev]) OCF_HIP(hipDeviceGetAttribute(&n[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return n[dev];
+}
+
+WsJobs ws_jobs(const OcfGemmArgs& g) {
+  WsJobs j{};
+  j.cb_p = g.cb_p; j.cb_s1 = g.cb_s1; j.cb_s2 = g.cb_s2; j.cb_op = g.cb_op;
+  j.jb_part = g.jb_part; j.jb_parts = g.jb_parts; j.jb_n = g.jb_n; j.jb_ld = g.jb_ld; j.jb_p = g.jb_p;
+  j.jb_s1 = g.jb_s1; j.jb_s2 = g.jb_s2; j.jb_op = g.jb_op;
+  j.js_sp = g.js_sp; j.js_rs = g.js_rs; j.js_out = g.js_out; j.js_nparts = g.js_nparts; j.js_ntiles = g.js_ntiles;
+  j.js_M = g.js_M;
+  return j;
+}
+
+// the folded jobs as separate launches (generic kernel path): before / after the GEMM
+void jobs_before(const OcfGemmArgs& g, hipStream_t s) {
+  if (g.jb_part)
+    OCF_CHECK(ocf_bias_opt_from_partials(g.jb_p, g.jb_part, g.jb_parts, g.jb_ld, g.jb_n, g.jb_s1, g.jb_s2, nullptr,
+                                         &g.jb_op, s) == 0, ocf_last_error());
+  if (g.js_sp)
+    OCF_CHECK(ocf_stats_finalize(g.js_sp, g.js_nparts, g.js_rs, g.js_ntiles, g.js_M, g.js_out, s) == 0,
+              ocf_last_error());
+}
+void jobs_after(const OcfGemmArgs& g, hipStream_t s) {
+  if (g.cb_p)
+    OCF_CHECK(ocf_bias_opt_from_partials(g.cb_p, g.sp_colsum, 1, g.M, g.M, g.cb_s1, g.cb_s2, nullptr, &g.cb_op, s) == 0,
+              ocf_last_error());
+}
+
+// EPI_OPTIM on [K][M] x [K][N] operands (the dW GEMMs) through the persistent role-split kernel
+template <typename CT, bool SPA>
+void launch_ws(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
+  OCF_CHECK(g.s1 != nullptr, "ocf_gemm OPTIM: optimizer slot s1 required");
+  GemmShape sh{};
+  sh.A = g.A; sh.B = g.B; sh.lda = g.lda; sh.ldb = g.ldb;
+  sh.M = g.M; sh.N = g.N; sh.K = g.K; sh.kchunk = g.K;
+  sh.b_blk = g.b_blocked != 0;
+  sh.sp_colsum = g.sp_colsum;
+  sh.colsum_scale = g.opt.gscale;
+  if constexpr (SPA) {
+    sh.sp_rows = g.sp_rows; sh.sp_rp = g.sp_rp; sh.sp_tptr = g.sp_tptr; sh.sp_col = g.sp_col;
+    sh.sp_lidx = g.sp_lidx; sh.sp_lboff = g.sp_lboff; sh.sp_vals = g.sp_vals;
+    sh.sp_ntiles = g.sp_ntiles; sh.sp_krows = g.sp_krows;
+    sh.sp_bptr = g.sp_bptr; sh.sp_ent = reinterpret_cast<const int2*>(g.sp_ent);
+  }
+  const int T = (g.M / GT_BM) * (g.N / GT_BN);
+  const int cus = (cu_count() + 7) / 8 * 8;
+  const int G = std::min(cus, (T + 7) / 8 * 8);   // one workgroup per CU (LDS), multiple of 8 (XCDs)
+  const WsJobs jb = ws_jobs(g);
+  switch (g.opt.kind) {
+    case OCF_OPT_ADAGRAD:
+      hipLaunchKernelGGL((optim_ws_kernel<CT, SPA, OCF_OPT_ADAGRAD>), dim3(G), dim3(WS_THREADS), 0, s, sh, ep, jb);
+      break;
+    case OCF_OPT_RMSPROP:
+      hipLaunchKernelGGL((optim_ws_kernel<CT, SPA, OCF_OPT_RMSPROP>), dim3(G), dim3(WS_THREADS), 0, s, sh, ep, jb);
+      break;
+    default:
+      OCF_CHECK(g.opt.kind == OCF_OPT_ADAM && g.s2, "optim_ws: Adagrad, RMSprop or Adam (with both slots)");
+      hipLaunchKernelGGL((optim_ws_kernel<CT, SPA, OCF_OPT_ADAM>), dim3(G), dim3(WS_THREADS), 0, s, sh, ep, jb);
+  }
   OCF_HIP(hipGetLastError());
 }
 
@@ -113,10 +193,22 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
         OCF_CHECK(!g.p_shadow || g.compute_dtype != OCF_F32, "ocf_gemm OPTIM: shadow weights need f16/bf16 compute");
         OCF_CHECK(!g.shadow_blocked || g.ld_out % 64 == 0, "ocf_gemm OPTIM: blocked shadow needs ld_out % 64 == 0");
         if constexpr (ACOL) {
-          if (g.a_sparse) {
-            launch<CT, ACOL, BCOL, CT, EpiOptim, true>(g, p, s);
-            return;
+          if constexpr (sizeof(CT) == 2) {
+            // role-split kernel: slots present (SGD stays generic), row-major B, and for a sparse A
+            // the (column tile, K-step) buckets of ocf_sparse_tiles
+            const bool ws_kind = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
+                                 (g.opt.kind == OCF_OPT_ADAM && g.s2);
+            if (optim_ws_on() && ws_kind && g.s1 && !g.b_blocked && (!g.a_sparse || (g.sp_bptr && g.sp_ent))) {
+              if (g.a_sparse) launch_ws<CT, true>(g, p, s);
+              else launch_ws<CT, false>(g, p, s);
+              return;
+            }
           }
+          jobs_before(g, s);
+          if (g.a_sparse) launch<CT, ACOL, BCOL, CT, EpiOptim, true>(g, p, s);
+          else launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
+          jobs_after(g, s);
+          return;
         }
         launch<CT, ACOL, BCOL, CT, EpiOptim>(g, p, s);
         return;
@@ -166,6 +258,15 @@ void dispatch(const OcfGemmArgs& g, hipStream_t s) {
 
 }  // namespace
 
+extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
+  OCF_TRY_BEGIN
+  const std::string k = key ? key : "";
+  OCF_CHECK(k == "optim_ws", "ocf_set_tuning: unknown key '" + k + "'");
+  if (previous) *previous = optim_ws_on() ? 1 : 0;
+  g_optim_ws = value ? 1 : 0;
+  OCF_TRY_END
+}
+
 extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   OCF_TRY_BEGIN
   const OcfGemmArgs& g = *args;
@@ -185,6 +286,11 @@ extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
                   g.sp_ntiles * GT_BM >= g.M && g.sp_krows <= g.K,
               "ocf_gemm: sparse A descriptor incomplete");
   }
+  OCF_CHECK(!(g.cb_p || g.jb_part || g.js_sp) || (g.epi == OCF_EPI_OPTIM && g.a_col),
+            "ocf_gemm: folded jobs only with OPTIM on [K][M] A");
+  OCF_CHECK(!g.cb_p || g.sp_colsum, "ocf_gemm: cb_p needs sp_colsum");
+  OCF_CHECK(!g.jb_part || g.jb_p, "ocf_gemm: jb_part needs jb_p");
+  OCF_CHECK(!g.js_sp || g.js_out, "ocf_gemm: js_sp needs js_out");
   hipStream_t s = (hipStream_t)stream;
   switch (g.compute_dtype) {
     case OCF_F16: dispatch<_Float16>(g, s); break;

@@ -424,3 +424,119 @@ extern "C" int ocf_colsum(const void* d, int dtype, int64_t ld, int B, int N, fl
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }
+
+// ---------------------------------------------------------------------------------------
+// (M tile, K-step) buckets of a batch's sparse A operand for the persistent dW kernel.
+// Pass 1: one wave per bucket (t, kt), lane = batch row b - 64 kt, counts.  Pass 2: one workgroup
+// per tile writes each lane's tile segment at its wave-prefix offset (rows in order, entries in
+// column order): deterministic, no atomics.
+namespace ocf {
+
+struct TbSeg {
+  int64_t e0;   // first entry of row r's tile-t segment (column-sorted view)
+  int n;        // entries in it
+  int64_t lb;   // value index base of batch row b
+};
+
+__device__ __forceinline__ TbSeg tb_segment(const OcfTileBucketArgs& a, int t, int b) {
+  TbSeg s{0, 0, 0};
+  if (b >= a.krows) return s;
+  const int r = a.rows[b];
+  if (r < 0) return s;
+  const int32_t* tp = a.tptr + (int64_t)r * (a.ntiles + 1) + t;
+  s.e0 = a.rp[r] + tp[0];
+  s.n = tp[1] - tp[0];
+  s.lb = a.lboff[b];
+  return s;
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+__global__ void __launch_bounds__(256) tb_count_kernel(OcfTileBucketArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int id = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (id >= a.gm * a.nk) return;
+  const int t = id / a.nk, kt = id % a.nk;
+  const TbSeg s = tb_segment(a, t, kt * 64 + lane);
+  const int tot = __shfl(wave_incl_scan(s.n, lane), 63, 64);
+  if (lane == 0) a.cnt[id] = tot;
+}
+
+// one workgroup per column tile t: its base = sum of the counts of all earlier buckets (a parallel
+// fixed-order sum, cheap at a few thousand buckets, and no separate scan launch), then one wave per
+// K-step writes its rows' segments at the wave-prefix offsets; the last workgroup writes bptr[total]
+__global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
+  __shared__ int red[256];
+  __shared__ int kt_cnt[64];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nb = a.gm * a.nk, before = t * a.nk;
+  int s = 0;
+  for (int i = tid; i < before; i += 256) s += a.cnt[i];
+  red[tid] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  const int tile_base = red[0];
+  if (t == a.gm - 1 && tid == 0) {
+    int tot = tile_base;
+    for (int i = before; i < nb; ++i) tot += a.cnt[i];
+    a.bptr[nb] = tot;
+  }
+  for (int kt0 = 0; kt0 < a.nk; kt0 += 4) {
+    const int kt = kt0 + w;
+    // bucket offsets of this group of K-steps within the tile
+    if (tid < 4 && kt0 + tid < a.nk) kt_cnt[tid] = a.cnt[before + kt0 + tid];
+    __syncthreads();
+    int koff = tile_base;
+    for (int i = 0; i < kt0; ++i) koff += a.cnt[before + i];
+    for (int i = 0; i < w; ++i) koff += kt_cnt[i];
+    if (kt < a.nk) {
+      const TbSeg sg = tb_segment(a, t, kt * 64 + lane);
+      const int incl = wave_incl_scan(sg.n, lane);
+      if (lane == 0) a.bptr[before + kt] = koff;
+      const int64_t base = (int64_t)koff + incl - sg.n;
+      if (base + sg.n <= a.cap)
+        for (int j = 0; j < sg.n; ++j) {
+          const int64_t e = sg.e0 + j;
+          int2 v;
+          v.x = (int)(sg.lb + a.lidx[e]);
+          v.y = lane | ((a.col[e] - t * 128) << 8);
+          reinterpret_cast<int2*>(a.ent)[base + j] = v;
+        }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace ocf
+
+extern "C" int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfTileBucketArgs& a = *args;
+  OCF_CHECK(a.rows && a.rp && a.tptr && a.col && a.lidx && a.lboff && a.cnt && a.bptr && a.ent,
+            "ocf_sparse_tiles: null pointer");
+  OCF_CHECK(a.gm >= 0 && a.nk >= 0 && a.gm <= a.ntiles && a.krows <= 64 * a.nk,
+            "ocf_sparse_tiles: gm <= ntiles and krows <= 64 * nk required");
+  const int nb = a.gm * a.nk;
+  hipStream_t s = (hipStream_t)stream;
+  if (nb > 0) {
+    hipLaunchKernelGGL(tb_count_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a);
+    OCF_HIP(hipGetLastError());
+  }
+  if (nb > 0) {
+    hipLaunchKernelGGL(tb_fill_kernel, dim3(a.gm), dim3(256), 0, s, a);
+    OCF_HIP(hipGetLastError());
+  } else {
+    OCF_HIP(hipMemsetAsync(a.bptr, 0, sizeof(int32_t), s));
+  }
+  OCF_TRY_END
+}

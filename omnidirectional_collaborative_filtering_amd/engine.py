@@ -235,6 +235,10 @@ class Engine:
         # index loads per K-step, so it wins only for short K loops: ML-20M, 1 GPU (K = 256): 0.774 vs
         # 0.811 ms/step; 8-way feature parallel (K = 2,048 global rows): 0.538 vs 0.389 ms/step.
         self.sparse_dw = Bp <= 256
+        self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
+        self.tb = None
+        self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
+        self._stats_pending = None
         self._gbuf = {}
         HpL = self.Hp[-1]
         self.db_rows = torch.zeros(Bp, HpL, device=d, dtype=torch.float32)      # hidden-bias grad rows
@@ -400,8 +404,26 @@ class Engine:
                 self._xin_clean = True
             a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
+            self.tb = self._tile_buckets() if (self.gt is not None and self.sparse_dw and self.dw_buckets) else None
         self._xin_prev = (type(a).from_buffer_copy(a), owner) if self.sparse_clear else None
         self._xin_clean = False
+
+    def _tile_buckets(self):
+        """the batch's entries bucketed by (user tile, K-step) for the persistent weight-gradient
+        kernel (ocf_sparse_tiles); shared by dW_out (deltas) and dW_in (inputs): same entries"""
+        t = self.tseg
+        gm, nk = self.Np // TILE, self.Bp // 64
+        a = _lib.OcfTileBucketArgs()
+        p = lambda v: ptr(v) if torch.is_tensor(v) else v
+        a.rows, a.rp, a.tptr, a.col, a.lidx, a.lboff = (p(t[k]) for k in ("t_rows", "t_rp", "t_tptr", "t_col", "t_lidx",
+                                                                          "t_lboff"))
+        a.krows, a.ntiles, a.gm, a.nk = self.B, t["t_ntiles"], gm, nk
+        cnt = self._buf("tb_cnt", gm * nk, torch.int32)
+        bptr = self._buf("tb_ptr", gm * nk + 1, torch.int32)
+        ent = self._buf("tb_ent", 2 * self.gt["E"], torch.int32)
+        a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
+        call("ocf_sparse_tiles", a, cur_stream())
+        return dict(sp_bptr=bptr, sp_ent=ent)
 
     def load_dense(self, inputs, out_mask, targets):
         """API path: dense arrays (torch/numpy) in the model.py input order."""
@@ -425,6 +447,7 @@ class Engine:
              self.Bp, s)
         self._xin_prev, self._xin_clean = None, False      # xin written densely
         self._grow_buckets(B * N)
+        self.tb = None
         self.tseg = None
         call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
              ptr(self.bk_ptr), ptr(self.bk_cur), ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m), s)
@@ -574,13 +597,28 @@ class Engine:
                 sp, n_sp, rs, n_rs = self.stats_part, self.n_tiles * (self.Bp // TILE), self.row_sse_part, self.n_tiles
         self._grow_stats(self.n_stats + 1)
         dst = self.stats_hist[self.n_stats]
-        if self.side is not None:
+        if with_grad and self._folds():
+            # finalized by the output-layer weight-gradient launch (OcfGemmArgs js_*)
+            self._stats_pending = (sp, n_sp, rs, n_rs, self.Bp, dst)
+        elif self.side is not None:
             self._fork()
             with torch.cuda.stream(self.side):
                 call("ocf_stats_finalize", ptr(sp), n_sp, ptr(rs), n_rs, self.Bp, ptr(dst), cur_stream())
         else:
             call("ocf_stats_finalize", ptr(sp), n_sp, ptr(rs), n_rs, self.Bp, ptr(dst), cur_stream())
         self.n_stats += 1
+
+    def _folds(self):
+        """single-GPU row-gather step with the fused optimizer: the stats finalisation and both
+        bias updates ride in the output-layer dW launch instead of side-stream kernels"""
+        return (self.fold_jobs and self.gt is not None and self.comm is None and len(self.H) == 1
+                and self.sparse_dw and self.tb is not None and self.trainable[1])
+
+    def _flush_stats(self):
+        if self._stats_pending is not None:
+            call("ocf_stats_finalize", *[ptr(x) if torch.is_tensor(x) else x for x in self._stats_pending],
+                 cur_stream())
+            self._stats_pending = None
 
     def _gemm_mse(self, L, gscale, with_grad):
         tg = self.tseg if self.tseg is not None else dict(bk_ptr=self.bk_ptr, bk_rc=self.bk_rc, bk_t=self.bk_t,
@@ -672,7 +710,7 @@ class Engine:
         if fused:
             self.opt.iterations += 1
 
-    def _weight_update_sparse(self, i, vals, Bm, ldb, N, gscale, grads_out, op, colsum=None):
+    def _weight_update_sparse(self, i, vals, Bm, ldb, N, gscale, grads_out, op, colsum=None, jobs=None):
         """EPI_OPTIM / EPI_GRAD for a first/last layer whose A operand (the batch entries: deltas or
         inputs, [B][N] transposed) is built in LDS from the target CSR's column-sorted view"""
         if grads_out is None and not self.trainable[i]:
@@ -682,7 +720,7 @@ class Engine:
             t = self.tseg
             sp = dict(a_sparse=1, sp_rows=t["t_rows"], sp_rp=t["t_rp"], sp_tptr=t["t_tptr"], sp_col=t["t_col"],
                       sp_lidx=t["t_lidx"], sp_lboff=t["t_lboff"], sp_vals=vals, sp_ntiles=t["t_ntiles"],
-                      sp_krows=self.B, sp_colsum=colsum)
+                      sp_krows=self.B, sp_colsum=colsum, **(self.tb or {}))
             A = Bm                    # not read (sparse A); any valid pointer
         else:                         # dense operand: the decoder's delta or the scattered layer-0 input
             sp = dict(sp_colsum=colsum)
@@ -691,7 +729,7 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp)
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
         else:
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
                        opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), **sp)
@@ -714,6 +752,29 @@ class Engine:
             db_last, parts_last = self.db_rows, Bp
         delta = self._buf("delta_e", self.gt["E"]) if self.sparse_dw else None
         xval = self.gt["xval"]
+        if fused and self._folds():
+            # dW_out also: output-bias gradient (column sums of the deltas) and its update, the
+            # hidden-bias update from the decoder's row partials, the step's stats
+            jobs = {}
+            if self.trainable[1]:
+                sb = self.slots[1][1]
+                jobs.update(cb_p=self.b[1], cb_s1=sb[0], cb_s2=sb[1], cb_op=self._bias_op)
+            if self.trainable[0]:
+                sb = self.slots[0][1]
+                jobs.update(jb_part=db_last, jb_parts=parts_last, jb_ld=HpL, jb_n=HpL, jb_p=self.b[0], jb_s1=sb[0],
+                            jb_s2=sb[1], jb_op=self._bias_op)
+            if self._stats_pending is not None:
+                sp, n_sp, rs, n_rs, M, dst = self._stats_pending
+                jobs.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
+                self._stats_pending = None
+            with self.phase("dW_out"):
+                self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
+                                           jobs=jobs)
+            with self.phase("dW_in"):
+                self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
+            self.opt.iterations += 1
+            return
+        self._flush_stats()
         if fused and L == 1 and self.comm is None and self.side is not None:
             self._fork()
             with torch.cuda.stream(self.side):
@@ -807,6 +868,7 @@ class Engine:
 
     def take_stats(self):
         """host copy of the per-step stats recorded since the last call: [steps, 4 + Bp]."""
+        self._flush_stats()
         st = self.stats_hist[: self.n_stats]
         if self.comm is not None and self.n_stats:
             st = st.clone()

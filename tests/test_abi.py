@@ -51,7 +51,9 @@ STRUCTS = {
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
                                        "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part", "t_rows", "t_lboff", "t_ntiles",
                                        "t_aux", "p_shadow", "b_nt", "shadow_blocked", "a_sparse",
-                                       "sp_lboff", "sp_krows", "sp_colsum"]),
+                                       "sp_lboff", "sp_krows", "sp_colsum", "sp_bptr", "sp_ent", "cb_op", "jb_part",
+                                       "jb_ld", "jb_op", "js_sp", "js_M"]),
+    "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap"]),
 }
 
 
