@@ -219,11 +219,15 @@ def main():
     # weight operands: the compute-dtype shadow (2 B) written by the optimizer epilogue, fp32 in fp32 mode
     w_b = 4 if args.dtype == "float32" else 2
     sh_b = 0 if args.dtype == "float32" else 2
+    # batch operand of the weight-gradient GEMMs: dense [B][N] (2 B per element) or, on the sparse
+    # path, the batch's entries (4-B value + 4-B packed index each)
+    sparse_a = bool(eng.use_sparse and eng.sparse_ok and eng.sparse_dw)
+    a_bytes = (8.0 * nnz / args.steps / max(world, 1)) if sparse_a else Bg * Nl * 2
     alg = {
         # bytes per launch, algorithmic (real, unpadded sizes of this rank): optimizer state r/w (+ shadow
         # write) + streamed operands
-        "dW_in": P * (opt_b + sh_b) + Bg * Nl * 2 + Bg * H * 2,
-        "dW_out": P * (opt_b + sh_b) + Bg * Nl * 2 + Bg * H * 2,
+        "dW_in": P * (opt_b + sh_b) + a_bytes + Bg * H * 2,
+        "dW_out": P * (opt_b + sh_b) + a_bytes + Bg * H * 2,
         "enc_gemm": P * w_b + Bg * Nl * 2,
         "dec_gemm_mse": P * w_b + Bg * H * 2 + Bg * Nl * 2,
         "dec_bwd_gemm": P * w_b + Bg * Nl * 2,

@@ -278,6 +278,8 @@ int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on
  *               [K][M] x [K][N] operands with 16-bit compute run on the persistent role-split kernel
  *               (ocf_optim_ws.h); 0 = the generic tile kernel.  Bit-identical results.
+ *   "optim_ws_max_k": largest K (batch rows) sent to that kernel (default 256; beyond it the K-loop
+ *               outgrows the optimizer stream it hides under and the generic kernel is faster).
  * previous (nullable) receives the old value. */
 int ocf_set_tuning(const char* key, int value, int* previous);
 

@@ -44,8 +44,13 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   OCF_HIP(hipGetLastError());
 }
 
-// tuning switches (ocf_set_tuning); env OCF_OPTIM_WS=0 disables the role-split optimizer kernel
+// tuning switches (ocf_set_tuning); env OCF_OPTIM_WS=0 disables the role-split optimizer kernel.
+// The role split pays off while the MFMA role's K-loop fits under the stream of a tile: at K = 256
+// (ML-20M, one GPU) 238-251 us vs 290-316 us for the generic kernel; at K = 2,048 (8-way feature
+// parallel global batch) the K-loop dominates and the generic kernel's two workgroups per CU win
+// (dW 132 / 111 us vs 175 / 137 us).
 int g_optim_ws = -1;
+int g_optim_ws_max_k = 256;
 bool optim_ws_on() {
   if (g_optim_ws < 0) {
     const char* e = std::getenv("OCF_OPTIM_WS");
@@ -198,7 +203,8 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
             // the (column tile, K-step) buckets of ocf_sparse_tiles
             const bool ws_kind = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
                                  (g.opt.kind == OCF_OPT_ADAM && g.s2);
-            if (optim_ws_on() && ws_kind && g.s1 && !g.b_blocked && (!g.a_sparse || (g.sp_bptr && g.sp_ent))) {
+            if (optim_ws_on() && g.K <= g_optim_ws_max_k && ws_kind && g.s1 && !g.b_blocked &&
+                (!g.a_sparse || (g.sp_bptr && g.sp_ent))) {
               if (g.a_sparse) launch_ws<CT, true>(g, p, s);
               else launch_ws<CT, false>(g, p, s);
               return;
@@ -261,9 +267,15 @@ void dispatch(const OcfGemmArgs& g, hipStream_t s) {
 extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   OCF_TRY_BEGIN
   const std::string k = key ? key : "";
-  OCF_CHECK(k == "optim_ws", "ocf_set_tuning: unknown key '" + k + "'");
-  if (previous) *previous = optim_ws_on() ? 1 : 0;
-  g_optim_ws = value ? 1 : 0;
+  if (k == "optim_ws") {
+    if (previous) *previous = optim_ws_on() ? 1 : 0;
+    g_optim_ws = value ? 1 : 0;
+  } else if (k == "optim_ws_max_k") {
+    if (previous) *previous = g_optim_ws_max_k;
+    g_optim_ws_max_k = value;
+  } else {
+    throw std::runtime_error("ocf_set_tuning: unknown key '" + k + "'");
+  }
   OCF_TRY_END
 }
 

@@ -16,10 +16,19 @@ OPTS = {
 }
 
 
-def set_ws(on):
+def _tune(key, value):
     prev = _lib.I32(0)
-    _lib.call("ocf_set_tuning", b"optim_ws", int(on), prev)
+    _lib.call("ocf_set_tuning", key, int(value), prev)
     return prev.value
+
+
+def set_ws(on):
+    """route EPI_OPTIM to the role-split kernel (at every K, so all shapes here exercise it) or to
+    the generic kernel; returns the previous setting for set_ws(prev)"""
+    if isinstance(on, tuple):
+        _tune(b"optim_ws_max_k", on[1])
+        return (_tune(b"optim_ws", on[0]), None)
+    return (_tune(b"optim_ws", on), _tune(b"optim_ws_max_k", 1 << 30))
 
 
 def _sparse_batch(M, K, krows, seed):
@@ -194,8 +203,11 @@ def test_ws_matches_torch_reference(gpu):
     cd = _lib.DT_F16
     A, Bm, state = _operands(cd, M, N, K, seed=9)
     gs = 1e-3
-    set_ws(1)
-    P, S1, _, cs = _run(cd, M, N, K, OPTS["adagrad"](gs), A, Bm, state, colsum=True)
+    prev = set_ws(1)
+    try:
+        P, S1, _, cs = _run(cd, M, N, K, OPTS["adagrad"](gs), A, Bm, state, colsum=True)
+    finally:
+        set_ws(prev)
     G = (A.double().t() @ Bm.double()) * gs
     a = state[1].double() + G * G
     p = state[0].double() - 0.01 * G / (a.sqrt() + 1e-8)

@@ -44,6 +44,8 @@ def phase_of(name, seen):
         return ("dW_out", "dW_in")[k % 2]
     if "scatter_flat" in name:
         return "scatter"
+    if "tb_count" in name or "tb_fill" in name:
+        return "tile_buckets"
     return None
 
 
