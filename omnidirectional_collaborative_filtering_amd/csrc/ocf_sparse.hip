@@ -23,7 +23,6 @@
 namespace ocf {
 
 constexpr int RG_THREADS = 256;
-constexpr int RG_GROUPS = RG_THREADS / 16;
 constexpr int RG_MAX_H = 512;
 #ifndef OCF_RG_U
 #define OCF_RG_U 4
@@ -129,9 +128,10 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   float acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
-  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
-    float x[RG_U];
-    int n[RG_U];
+  // entry indices one iteration ahead of the weight-row loads that depend on them
+  float x[RG_U];
+  int n[RG_U];
+  auto idx = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
@@ -139,12 +139,19 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
       x[u] = ok ? a.xval[lb + ju] : 0.f;
       n[u] = ok ? a.col[s + ju] : 0;
     }
+  };
+  idx(j0 + grp);
+  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
     uint4 w[RG_U][PPL];
+    float xc[RG_U];
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u)
+    for (int u = 0; u < RG_U; ++u) {
+      xc[u] = x[u];
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
         w[u][i] = x[u] != 0.f ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+    }
+    idx(j + NG * RG_U);
 #pragma unroll
     for (int u = 0; u < RG_U; ++u)
 #pragma unroll
@@ -152,7 +159,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
         float f[E];
         unpack_piece<WT>(w[u][i], f);
 #pragma unroll
-        for (int k = 0; k < E; ++k) acc[i * E + k] += x[u] * f[k];
+        for (int k = 0; k < E; ++k) acc[i * E + k] += xc[u] * f[k];
       }
   }
   reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l);
@@ -185,10 +192,11 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
   float sse = 0.f, sae = 0.f, cnt = 0.f;
-  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
-    bool live[RG_U];
-    int n[RG_U];
-    float t[RG_U];
+  // entry indices one iteration ahead; the bias of each entry's column loads with its weight row
+  bool live[RG_U];
+  int n[RG_U];
+  float t[RG_U];
+  auto idx = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
@@ -197,13 +205,25 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
       n[u] = ok ? a.col[s + ju] : 0;
       t[u] = ok ? a.val[s + ju] : 0.f;
     }
+  };
+  idx(j0 + grp);
+  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
     uint4 w[RG_U][PPL];
-    float dot[RG_U];
+    bool lv[RG_U];
+    int nc[RG_U];
+    float tc[RG_U], bn[RG_U];
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u)
+    for (int u = 0; u < RG_U; ++u) {
+      lv[u] = live[u];
+      nc[u] = n[u];
+      tc[u] = t[u];
+      bn[u] = live[u] ? a.bias[n[u]] : 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
         w[u][i] = live[u] ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+    }
+    idx(j + NG * RG_U);
+    float dot[RG_U];
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       float d0 = 0.f;
@@ -225,15 +245,15 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
       const int ju = j + u * NG;
       if (ju >= j1) break;
       float d = 0.f;
-      if (live[u]) {
-        const float yh = m * (dot[u] + a.bias[n[u]]);
-        const float err = yh - t[u];
+      if (lv[u]) {
+        const float yh = m * (dot[u] + bn[u]);
+        const float err = yh - tc[u];
         d = err * m;
         if (l == 0) {
           sse += err * err;
           sae += fabsf(err);
-          cnt += (t[u] + yh != 0.f) ? 1.f : 0.f;
-          if (a.d_out) store_ct(a.d_out, a.d_dtype, (int64_t)b * a.ld_d + n[u], d);
+          cnt += (tc[u] + yh != 0.f) ? 1.f : 0.f;
+          if (a.d_out) store_ct(a.d_out, a.d_dtype, (int64_t)b * a.ld_d + nc[u], d);
         }
       }
       if (l == 0 && a.delta_e) a.delta_e[lb + ju] = d;

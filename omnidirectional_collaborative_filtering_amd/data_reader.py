@@ -18,6 +18,8 @@ deliberate:
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -26,7 +28,7 @@ from .dataset import FixedSplit, load_reference_json
 from .engine import TILE, cur_stream, ptr, ru
 
 AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
-GATHER_CHUNK = 256     # entries per row-gather work unit (ocf_gather_*)
+GATHER_CHUNK = int(os.environ.get("OCF_GATHER_CHUNK", 256))   # entries per row-gather work unit (ocf_gather_*)
 
 
 class _DeviceCSR:
