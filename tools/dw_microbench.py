@@ -15,11 +15,10 @@ from omnidirectional_collaborative_filtering_amd import _lib  # noqa: E402
 from omnidirectional_collaborative_filtering_amd.engine import cur_stream  # noqa: E402
 from tools.gemm_microbench import gemm, timeit  # noqa: E402
 
-Bp, Np, Hp = 256, 138496, 512
 F16 = _lib.DT_F16
 
 
-def main():
+def main(Bp=256, Np=138496, Hp=512):
     torch.manual_seed(0)
     X = (torch.randn(Bp, Np, device="cuda") * (torch.rand(Bp, Np, device="cuda") < 0.05)).half()
     dh = torch.randn(Bp, Hp, device="cuda").half()
@@ -46,8 +45,12 @@ def main():
     us = timeit(lambda: C.copy_(P))
     res["copy_us"] = round(us, 1)
     res["copy_TBs"] = round(n * 8 / us / 1e6, 3)
-    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), **res}), flush=True)
+    print(json.dumps({"lib": os.path.basename(_lib.LIB_PATH), "shape": [Np, Hp], **res}), flush=True)
 
 
 if __name__ == "__main__":
-    main()
+    import sys as _s
+    if len(_s.argv) > 2:
+        main(Np=int(_s.argv[1]), Hp=int(_s.argv[2]))
+    else:
+        main()
