@@ -17,6 +17,8 @@
 // owns one entry at a time and each lane holds PPL 16-byte pieces of the row (pieces l, l+16, ...:
 // every load instruction of a group reads 256 contiguous bytes).  Chunk partials are reduced in a
 // fixed order per row by ocf_rows_reduce, which also applies the layer epilogue.
+#include <cstdlib>
+
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
 
@@ -317,6 +319,19 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(OcfRowsReduceArgs a) {
 // lanes) that the row's 16-byte pieces fill
 template <typename WT> bool gather_shape(int H, int& G, int& ppl) {
   const int pieces = H / EPc<WT>::v;
+  // group width cap: 32 lanes x 2 pieces per entry beat 64 x 1 at H = 512 (ML-20M step: decoder
+  // 72 -> 55 us, encoder 57 -> 50 us): twice the entries in flight per workgroup and one shuffle
+  // step less per dot product.  OCF_RG_GMAX overrides (diagnostics).
+  static const int gmax = [] {
+    const char* e = std::getenv("OCF_RG_GMAX");
+    return e ? std::atoi(e) : 32;
+  }();
+  for (int g : {64, 32, 16})
+    if (g <= gmax && pieces % g == 0 && pieces / g <= 4) {
+      G = g;
+      ppl = pieces / g;
+      return true;
+    }
   for (int g : {64, 32, 16})
     if (pieces % g == 0) {
       G = g;
@@ -331,6 +346,8 @@ void by_shape(int G, int ppl, const OcfGatherArgs& a, hipStream_t s) {
   if (G == 64 && ppl == 1) L<64, 1>::go(a, s);
   else if (G == 64 && ppl == 2) L<64, 2>::go(a, s);
   else if (G == 32 && ppl == 1) L<32, 1>::go(a, s);
+  else if (G == 32 && ppl == 2) L<32, 2>::go(a, s);
+  else if (G == 16 && ppl == 4) L<16, 4>::go(a, s);
   else if (G == 32 && ppl == 3) L<32, 3>::go(a, s);
   else if (G == 16 && ppl == 1) L<16, 1>::go(a, s);
   else if (G == 16 && ppl == 3) L<16, 3>::go(a, s);
