@@ -99,6 +99,9 @@ typedef struct OcfScatterArgs {
   /* per batch-local source-1 entry: its rating if it is a live input (the value X keeps after
    * duplicate resolution), else 0 -- the row-gather encoder's input (nullable) */
   float* xval1;
+  /* (nullable) per-(128-column tile, 64-row K-step) entry counts of source 1 for ocf_sparse_tiles
+   * (tb_cnt[(col >> 7) * tb_nk + (b >> 6)] += 1 per entry; the caller zeroes them beforehand) */
+  int32_t* tb_cnt; int tb_nk;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
@@ -271,6 +274,9 @@ typedef struct OcfTileBucketArgs {
   int krows, ntiles, gm, nk;
   int32_t* cnt; int32_t* bptr; int32_t* ent;
   int64_t cap;
+  /* counted = 1: cnt already holds the counts (ocf_scatter_batch tb_cnt), the count pass is skipped;
+   * cnt_clear (nullable): [gm*nk] counts zeroed by the fill pass (the next batch's counters) */
+  int counted; int32_t* cnt_clear;
 } OcfTileBucketArgs;
 int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
 

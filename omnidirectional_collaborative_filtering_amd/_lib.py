@@ -40,7 +40,7 @@ class OcfScatterArgs(ctypes.Structure):
         ("tile_cnt", P), ("bk_ptr", P), ("bk_cur", P), ("bk_rc", P), ("bk_t", P), ("bk_m", P), ("n_tiles", I32),
         ("pos1", P),
         ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
-        ("xin_clean", I32), ("xval1", P),
+        ("xin_clean", I32), ("xval1", P), ("tb_cnt", P), ("tb_nk", I32),
     ]
 
 
@@ -96,7 +96,7 @@ class OcfTileBucketArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
         ("krows", I32), ("ntiles", I32), ("gm", I32), ("nk", I32),
-        ("cnt", P), ("bptr", P), ("ent", P), ("cap", I64),
+        ("cnt", P), ("bptr", P), ("ent", P), ("cap", I64), ("counted", I32), ("cnt_clear", P),
     ]
 
 

@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a,
       if (a.xin && a.feed == 1) store_val(a.xin, a.xin_dtype, ox + xb, aux);
     }
     if (a.xval1) a.xval1[e] = ((role & 1) && !later_in) ? v : 0.f;
+    if (a.tb_cnt) atomicAdd(&a.tb_cnt[(c >> 7) * a.tb_nk + (b >> 6)], 1);   // ocf_sparse_tiles counts
     const bool live_tg = (role & 2) && !later_tg;
     if (role & 2) {
       if (a.Mout) a.Mout[o] = aux;

@@ -523,6 +523,8 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
     __syncthreads();
   }
   const int tile_base = red[0];
+  if (a.cnt_clear)   // the next batch's counters (ocf_scatter_batch tb_cnt), zeroed for it
+    for (int i = tid; i < a.nk; i += 256) a.cnt_clear[before + i] = 0;
   if (t == a.gm - 1 && tid == 0) {
     int tot = tile_base;
     for (int i = before; i < nb; ++i) tot += a.cnt[i];
@@ -565,7 +567,8 @@ extern "C" int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream) {
             "ocf_sparse_tiles: gm <= ntiles and krows <= 64 * nk required");
   const int nb = a.gm * a.nk;
   hipStream_t s = (hipStream_t)stream;
-  if (nb > 0) {
+  OCF_CHECK(a.cnt_clear != a.cnt, "ocf_sparse_tiles: cnt_clear must not alias cnt");
+  if (nb > 0 && !a.counted) {
     hipLaunchKernelGGL(tb_count_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a);
     OCF_HIP(hipGetLastError());
   }

@@ -238,6 +238,7 @@ class Engine:
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
+        self._tb_par = 0
         self._stats_pending = None
         self._gbuf = {}
         HpL = self.Hp[-1]
@@ -392,9 +393,16 @@ class Engine:
         seg["t_flag"] = self.tflag
         self.tseg = seg
         self.gt = None
+        a.tb_cnt, a.tb_nk = None, 0
         if gather is not None and self.sparse_ok and self.use_sparse:
             xval = self._buf("xval", int(a.E1))
             a.xval1 = ptr(xval)
+            if self.sparse_dw and self.dw_buckets and targets["flag"] == 1:   # train split: inputs = targets
+                # tile-bucket counts from the scatter (ocf_sparse_tiles then skips its count pass);
+                # two counter sets alternate so the fill pass can zero the next batch's
+                gm, nk = self.Np // TILE, self.Bp // 64
+                self._tb_par ^= 1
+                a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
             if self.sparse_dw:
                 a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
             self.gt = dict(gather, xval=xval, aux=float(targets["t_aux"]), E=int(targets["E"]))
@@ -404,7 +412,7 @@ class Engine:
                 self._xin_clean = True
             a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
-            self.tb = self._tile_buckets() if (self.gt is not None and self.sparse_dw and self.dw_buckets) else None
+            self.tb = self._tile_buckets() if a.tb_cnt else None
         self._xin_prev = (type(a).from_buffer_copy(a), owner) if self.sparse_clear else None
         self._xin_clean = False
 
@@ -418,10 +426,12 @@ class Engine:
         a.rows, a.rp, a.tptr, a.col, a.lidx, a.lboff = (p(t[k]) for k in ("t_rows", "t_rp", "t_tptr", "t_col", "t_lidx",
                                                                           "t_lboff"))
         a.krows, a.ntiles, a.gm, a.nk = self.B, t["t_ntiles"], gm, nk
-        cnt = self._buf("tb_cnt", gm * nk, torch.int32)
+        cnt = self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)        # counted by the scatter
+        nxt = self._buf("tb_cnt%d" % (self._tb_par ^ 1), gm * nk, torch.int32)
         bptr = self._buf("tb_ptr", gm * nk + 1, torch.int32)
         ent = self._buf("tb_ent", 2 * self.gt["E"], torch.int32)
         a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
+        a.counted, a.cnt_clear = 1, ptr(nxt)
         call("ocf_sparse_tiles", a, cur_stream())
         return dict(sp_bptr=bptr, sp_ent=ent)
 
