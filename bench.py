@@ -63,6 +63,9 @@ def parse():
                     help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
     ap.add_argument("--nt-operands", type=int, default=0,
                     help="non-temporal loads for GEMM operands at their last use in the step")
+    ap.add_argument("--row-skip", type=int, default=1,
+                    help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
+                         "gradient, identity update; bit-identical)")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient all-reduce)")
@@ -151,6 +154,7 @@ def main():
     if args.sparse_dw >= 0:
         eng.sparse_dw = bool(args.sparse_dw)
     eng.use_sparse = bool(args.gather)
+    eng.row_skip = bool(args.row_skip)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)
@@ -198,6 +202,7 @@ def main():
     host_ms = (t_issued - t_start) / args.steps * 1e3    # host time to issue one step (diagnostic)
     dom_timed = eng.phase_times_ms().get(dom) if dom else None
     eng.timers = None
+    row_skip_used = eng._rtag_live          # (the eval batches below reset it)
     tot = torch.tensor([elapsed, float(nnz)], device=dev, dtype=torch.float64)
     if world > 1:
         tmax = tot[:1].clone()
@@ -222,6 +227,19 @@ def main():
     # roofline of the dominant kernel: fused weight-gradient GEMM + optimizer update (per rank)
     Nl = data.num_cols
     P = Nl * H
+    # row skipping: only the weight rows of columns holding a batch entry carry optimizer traffic
+    # (pass-through training with data_sparsity [1,1]: every entry is a live input and a live target,
+    # so both weight matrices have the batch's distinct columns as live rows)
+    live = 1.0
+    if row_skip_used and args.optimizer == "adagrad":
+        tr = data.train
+        fr = []
+        for i in range(args.steps):
+            rows = np.asarray(gen.rows_host[batches[(args.warmup + i) % len(batches)]])
+            rows = rows[rows >= 0]
+            cols = np.concatenate([tr.col[tr.row_ptr[r]:tr.row_ptr[r + 1]] for r in rows])
+            fr.append(len(np.unique(cols)) / Nl)
+        live = float(np.mean(fr))
     opt_b = OPT_STATE_BYTES[args.optimizer]
     # weight operands: the compute-dtype shadow (2 B) written by the optimizer epilogue, fp32 in fp32 mode
     w_b = 4 if args.dtype == "float32" else 2
@@ -233,8 +251,8 @@ def main():
     alg = {
         # bytes per launch, algorithmic (real, unpadded sizes of this rank): optimizer state r/w (+ shadow
         # write) + streamed operands
-        "dW_in": P * (opt_b + sh_b) + a_bytes + Bg * H * 2,
-        "dW_out": P * (opt_b + sh_b) + a_bytes + Bg * H * 2,
+        "dW_in": P * live * (opt_b + sh_b) + a_bytes + Bg * H * 2,
+        "dW_out": P * live * (opt_b + sh_b) + a_bytes + Bg * H * 2,
         "enc_gemm": P * w_b + Bg * Nl * 2,
         "dec_gemm_mse": P * w_b + Bg * H * 2 + Bg * Nl * 2,
         "dec_bwd_gemm": P * w_b + Bg * Nl * 2,
@@ -248,7 +266,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
                 "kernel_mean_us": round(ms * 1e3, 1), "kernel_samples": dom_timed["n"],
-                "alg_bytes_per_launch": int(alg[dom])}
+                "alg_bytes_per_launch": int(alg[dom]), "live_row_frac": round(live, 4)}
         # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
         pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
         if pmcs and world == 1:
@@ -259,7 +277,9 @@ def main():
                 roof["traffic_source"] = os.path.relpath(pmcs[-1], ROOT)
     ms_step = elapsed / args.steps * 1e3
     step_flops = 10.0 * Bg * Nl * H
-    step_bytes = P * 2 * (opt_b + 4) + 2 * (3 * Nl * H) + 8 * (nnz / args.steps / max(world, 1))
+    # SURVEY §8(d) step bytes; with row skipping the optimizer term covers the live rows only
+    step_bytes_dense = P * 2 * (opt_b + 4) + 2 * (3 * Nl * H) + 8 * (nnz / args.steps / max(world, 1))
+    step_bytes = step_bytes_dense - P * 2 * (opt_b + 4) * (1.0 - live)
     line = {
         "metric": METRIC, "value": round(nnz / elapsed, 1), "unit": "ratings/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
@@ -272,7 +292,8 @@ def main():
                    "parallelism": ("feature%d" % world) if fp else ("dp%d" % world)},
         "masked_rmse": rmse,
         "roofline": roof,
-        "step_roofline": {"alg_bytes": int(step_bytes), "alg_flops": int(step_flops),
+        "step_roofline": {"alg_bytes": int(step_bytes), "alg_bytes_dense_update": int(step_bytes_dense),
+                          "live_row_frac": round(live, 4), "alg_flops": int(step_flops),
                           "hbm_bound_ms": round(step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 4),
                           "mfma_bound_ms": round(step_flops / (MFMA_F16_PEAK_TFS * 1e12) * 1e3, 4),
                           "frac_of_binding_roof": round(max(step_bytes / (HBM_PEAK_GBS * 1e9),

@@ -102,6 +102,11 @@ typedef struct OcfScatterArgs {
   /* (nullable) per-(128-column tile, 64-row K-step) entry counts of source 1 for ocf_sparse_tiles
    * (tb_cnt[(col >> 7) * tb_nk + (b >> 6)] += 1 per entry; the caller zeroes them beforehand) */
   int32_t* tb_cnt; int tb_nk;
+  /* (nullable) per-column row tags: rtag_in[c] = rtag for every column c holding a live input of
+   * the batch, rtag_out[c] = rtag for every column holding a live target (source 1, mode 0).  The
+   * columns so tagged are a superset of the weight rows with a nonzero gradient this step
+   * (OcfGemmArgs row_tag); the caller cycles rtag through 1..255 so no clearing pass is needed */
+  uint8_t* rtag_in; uint8_t* rtag_out; int rtag;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
@@ -234,6 +239,12 @@ typedef struct OcfGemmArgs {
   const float* jb_part; int jb_parts, jb_n; int64_t jb_ld; float* jb_p; float* jb_s1; float* jb_s2;
   OcfOptParams jb_op;
   const float* js_sp; const float* js_rs; float* js_out; int js_nparts, js_ntiles, js_M;
+  /* OPTIM with Adagrad and l2 == 0 (nullable): rows m with row_tag[m] != row_tag_value have an
+   * all-zero gradient (caller's guarantee, e.g. OcfScatterArgs rtag_*).  For them Keras' Adagrad
+   * update (a += 0; p -= lr * 0 / (sqrt(a) + eps)) is the identity, so the kernel skips their
+   * parameter / slot / shadow traffic; results are bit-identical to the full update.  Ignored by
+   * kernels that do not use it; rejected with any other optimizer or l2 != 0. */
+  const uint8_t* row_tag; int row_tag_value;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

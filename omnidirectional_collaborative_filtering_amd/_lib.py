@@ -41,6 +41,7 @@ class OcfScatterArgs(ctypes.Structure):
         ("pos1", P),
         ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
         ("xin_clean", I32), ("xval1", P), ("tb_cnt", P), ("tb_nk", I32),
+        ("rtag_in", P), ("rtag_out", P), ("rtag", I32),
     ]
 
 
@@ -89,6 +90,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("jb_part", P), ("jb_parts", I32), ("jb_n", I32), ("jb_ld", I64), ("jb_p", P), ("jb_s1", P), ("jb_s2", P),
         ("jb_op", OcfOptParams),
         ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
+        ("row_tag", P), ("row_tag_value", I32),
     ]
 
 

@@ -70,7 +70,16 @@ template <typename CT> struct WaveStager {
 template <int KIND> struct WsSet {
   static constexpr int U = WsCfg<KIND>::U;
   float4 p[U], a[U], b[WsCfg<KIND>::NS == 2 ? U : 1];
+  uint64_t live;   // live-row bits of the tile this set holds (WsStream::live_rows)
 };
+
+// Row skipping (EpiOptim::Params row_tag): a stream thread's chunk j = g*U+u of a tile lies in
+// tile row 2*sw + (lane >> 5) + 8*j (sw = stream wave 0..3).  Each lane reads the tags of rows
+// 2*lane and 2*lane+1 (one u16), two ballots give the even- and odd-row live bits of the tile, and
+// a lane keeps its parity's mask shifted by sw, so chunk j is live iff bit 4*j is set.  Dead rows
+// get an out-of-range buffer offset: the load returns zeros without touching memory and the
+// stores are dropped.
+constexpr uint32_t WS_OOB = 0x80000000u;   // >= num_records (0x7FFFFFFF) of wt_rsrc
 
 template <int KIND> struct WsStream {
   static constexpr int U = WsCfg<KIND>::U;
@@ -86,11 +95,24 @@ template <int KIND> struct WsStream {
     c4 = (ch & 31) * 4;
     return (int64_t)(m0 + ml) * ep.ld + n0 + c4;
   }
-  __device__ __forceinline__ void load(int m0, int n0, int g, WsSet<KIND>& s) const {
+  // tag of this lane's row pair in tile m0 (issued early; consumed by live_rows)
+  __device__ __forceinline__ uint32_t tag_load(int m0) const {
+    if (!ep.row_tag) return 0;
+    return *reinterpret_cast<const uint16_t*>(ep.row_tag + m0 + 2 * (stid & 63));
+  }
+  __device__ __forceinline__ uint64_t live_rows(uint32_t t2) const {
+    if (!ep.row_tag) return ~0ull;
+    const uint32_t tv = (uint32_t)ep.row_tag_value;
+    const uint64_t ev = __ballot((t2 & 0xffu) == tv), od = __ballot((t2 >> 8) == tv);
+    return (((stid >> 5) & 1) ? od : ev) >> (stid >> 6);
+  }
+  __device__ __forceinline__ void load(int m0, int n0, int g, WsSet<KIND>& s, uint64_t live) const {
+    s.live = live;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       int ml, c4;
-      const uint32_t o = (uint32_t)(off(m0, n0, g, u, ml, c4) * 4);
+      const bool lv = (live >> (4 * (g * U + u))) & 1;
+      const uint32_t o = (uint32_t)(off(m0, n0, g, u, ml, c4) * 4) | (lv ? 0u : WS_OOB);
       s.p[u] = ld_pol16<OCF_OPT_LD_POL>(rp, ep.p, o);
       s.a[u] = ld_pol16<OCF_OPT_LD_POL>(r1, ep.s1, o);
       if constexpr (NS == 2) s.b[u] = ld_pol16<OCF_OPT_LD_POL>(r2, ep.s2, o);
@@ -112,9 +134,10 @@ template <int KIND> struct WsStream {
       opt_update_k<KIND>(o, gv.y * o.gscale, pv.y, av.y, bv.y);
       opt_update_k<KIND>(o, gv.z * o.gscale, pv.z, av.z, bv.z);
       opt_update_k<KIND>(o, gv.w * o.gscale, pv.w, av.w, bv.w);
-      const uint32_t ob = (uint32_t)(of * 4);
+      const bool lv = (s.live >> (4 * (g * U + u))) & 1;
+      const uint32_t ob = (uint32_t)(of * 4) | (lv ? 0u : WS_OOB);
       st_pol16<OCF_OPT_ST_POL>(rp, ep.p, ob, pv);
-      if (ep.shadow) EpiOptim::store_shadow(ep, m0 + ml, n0 + c4, pv);
+      if (ep.shadow && lv) EpiOptim::store_shadow(ep, m0 + ml, n0 + c4, pv);
       st_pol16<OCF_OPT_ST_POL>(r1, ep.s1, ob, av);
       if constexpr (NS == 2) st_pol16<OCF_OPT_ST_POL>(r2, ep.s2, ob, bv);
     }
@@ -394,24 +417,33 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
     };
     // one tile from Y: groups alternate register sets; the last group prefetches group 0 of the
     // next tile into set 0
+    // live-row bits: of the tile being streamed (cur) and of the next one, whose tags are loaded at
+    // the top of run_tile and turned into bits just before its first group is prefetched
+    uint64_t cur = ~0ull;
     auto run_tile = [&](int i) {
       int m0, n0, pm0 = 0, pn0 = 0;
       origin(i, m0, n0);
       const bool pre = i + 1 < sc.count;
       if (pre) origin(i + 1, pm0, pn0);
+      const uint32_t t2 = pre ? st.tag_load(pm0) : 0u;
 #pragma unroll
       for (int g = 0; g < NG; g += 2) {
-        st.load(m0, n0, g + 1, s1);
+        st.load(m0, n0, g + 1, s1, cur);
         st.apply(m0, n0, g, s0);
-        if (g + 2 < NG) st.load(m0, n0, g + 2, s0);
-        else if (pre) st.load(pm0, pn0, 0, s0);
+        if (g + 2 < NG) {
+          st.load(m0, n0, g + 2, s0, cur);
+        } else if (pre) {
+          cur = st.live_rows(t2);
+          st.load(pm0, pn0, 0, s0, cur);
+        }
         st.apply(m0, n0, g + 1, s1);
       }
     };
     {
       int m0, n0;
       origin(0, m0, n0);
-      st.load(m0, n0, 0, s0);
+      cur = st.live_rows(st.tag_load(m0));
+      st.load(m0, n0, 0, s0, cur);
     }
     {  // folded small jobs, one per stream wave, while the MFMA role runs the first K-loop; taken
        // from the last workgroups first (the last slots of each XCD range hold one tile less)

@@ -114,6 +114,9 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a,
       if (live_tg && a.tile_cnt) atomicAdd(&a.tile_cnt[c >> 7], 1);
     }
     if (a.tflag1) a.tflag1[e] = live_tg ? 1 : 0;
+    // row tags (ocf.h OcfScatterArgs rtag_*): same-value byte stores, no ordering needed
+    if (a.rtag_in && (role & 1) && !later_in) a.rtag_in[c] = (uint8_t)a.rtag;
+    if (a.rtag_out && live_tg) a.rtag_out[c] = (uint8_t)a.rtag;
     if (a.Mmiss) a.Mmiss[o] = aux;
     if (a.xin) {
       if (a.feed == 2) store_val(a.xin, a.xin_dtype, ox + xb, aux);
@@ -284,6 +287,8 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   OCF_CHECK(a.E1 >= 0 && a.E2 >= 0, "ocf_scatter_batch: negative entry counts");
   OCF_CHECK(a.E2 == 0 || (a.rows2 && a.lboff2), "ocf_scatter_batch: source 2 needs rows2 / lboff2");
   OCF_CHECK(a.E1 == 0 || (a.rows1 && (a.lboff1 || a.boff1)), "ocf_scatter_batch: source 1 needs rows1 / offsets");
+  OCF_CHECK(!(a.rtag_in || a.rtag_out) || (a.rtag >= 1 && a.rtag <= 255),
+            "ocf_scatter_batch: row tags need 1 <= rtag <= 255");
   // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks)
   float* dense[5] = {a.X, a.Min, a.Mout, a.T, a.Mmiss};
   for (float* d : dense)

@@ -238,6 +238,14 @@ class Engine:
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
+        # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
+        # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
+        # role-split dW kernels skip the parameter / slot / shadow traffic of the untagged rows, whose
+        # update is the identity (zero gradient).  Bit-identical to the full update.
+        self.row_skip = True
+        self.rtag = [torch.zeros(self.Np, device=d, dtype=torch.uint8) for _ in range(2)]   # inputs, targets
+        self._rtag_val = 0
+        self._rtag_live = False
         self._tb_par = 0
         self._stats_pending = None
         self._gbuf = {}
@@ -394,6 +402,8 @@ class Engine:
         self.tseg = seg
         self.gt = None
         a.tb_cnt, a.tb_nk = None, 0
+        a.rtag_in = a.rtag_out = None
+        self._rtag_live = False
         if gather is not None and self.sparse_ok and self.use_sparse:
             xval = self._buf("xval", int(a.E1))
             a.xval1 = ptr(xval)
@@ -403,6 +413,10 @@ class Engine:
                 gm, nk = self.Np // TILE, self.Bp // 64
                 self._tb_par ^= 1
                 a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
+                if self.row_skip:
+                    self._rtag_val = self._rtag_val % 255 + 1
+                    a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
+                    self._rtag_live = True
             if self.sparse_dw:
                 a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
             self.gt = dict(gather, xval=xval, aux=float(targets["t_aux"]), E=int(targets["E"]))
@@ -738,6 +752,8 @@ class Engine:
         if grads_out is None:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
+            if self._rtag_live and self.sparse_dw and op.kind == _lib.OPT_ADAGRAD and op.l2 == 0:
+                sp.update(row_tag=self.rtag[0 if i == 0 else 1], row_tag_value=self._rtag_val)
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
                        ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
         else:

@@ -31,7 +31,7 @@ def set_ws(on):
     return (_tune(b"optim_ws", on), _tune(b"optim_ws_max_k", 1 << 30))
 
 
-def _sparse_batch(M, K, krows, seed):
+def _sparse_batch(M, K, krows, seed, col_frac=None):
     """a CSR over M columns, a batch of `krows` of its rows (some batch slots empty) and per-entry
     values in list order; returns the descriptor tensors and the dense [K][M] equivalent"""
     from omnidirectional_collaborative_filtering_amd.dataset import RatingsCSR
@@ -41,7 +41,13 @@ def _sparse_batch(M, K, krows, seed):
     lens[rng.rand(R) < 0.1] = 0
     rp = np.zeros(R + 1, np.int64)
     np.cumsum(lens, out=rp[1:])
-    col = np.concatenate([rng.choice(M, size=n, replace=False) for n in lens]).astype(np.int32)
+    if col_frac is None:
+        col = np.concatenate([rng.choice(M, size=n, replace=False) for n in lens]).astype(np.int32)
+    else:                                           # columns from a random subset only
+        pool = np.sort(rng.choice(M, size=int(M * col_frac), replace=False))
+        lens = np.minimum(lens, len(pool))
+        rp[1:] = np.cumsum(lens)
+        col = np.concatenate([rng.choice(pool, size=n, replace=False) for n in lens]).astype(np.int32)
     csr = RatingsCSR(rp, col, np.ones(len(col), np.float32))
     col_s, _, lidx_s, tptr = csr.tile_index(M)
     rows = rng.choice(R, size=krows, replace=False).astype(np.int32)
@@ -80,9 +86,11 @@ def _buckets(sp, M, K):
     return bptr, ent
 
 
-def _run(cd, M, N, K, opt, A, Bm, state, sparse=None, shadow_blocked=None, colsum=False):
+def _run(cd, M, N, K, opt, A, Bm, state, sparse=None, shadow_blocked=None, colsum=False, extra=None):
     P, S1, S2 = (t.clone() for t in state)
-    Sh = torch.zeros(M, N, device="cuda", dtype=torch.float16 if cd == _lib.DT_F16 else torch.bfloat16) \
+    sdt = torch.float16 if cd == _lib.DT_F16 else torch.bfloat16
+    # shadow starts as the rounded copy of P (row-major layout), as the engine keeps it
+    Sh = (P.to(sdt) if shadow_blocked == 0 else torch.zeros(M, N, device="cuda", dtype=sdt)) \
         if shadow_blocked is not None else None
     cs = torch.full((M,), -7.0, device="cuda") if colsum else None
     a = _lib.OcfGemmArgs()
@@ -102,6 +110,8 @@ def _run(cd, M, N, K, opt, A, Bm, state, sparse=None, shadow_blocked=None, colsu
         a.a_sparse = 1
         for k, v in sparse.items():
             setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
+    for k, v in (extra or {}).items():
+        setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
     _lib.call("ocf_gemm", a, cur_stream())
     torch.cuda.synchronize()
     return [P, S1, S2] + ([Sh] if Sh is not None else []) + ([cs] if cs is not None else [])
@@ -269,3 +279,87 @@ def test_folded_jobs_match_separate_kernels(gpu, opt):
     for i, (r, x) in enumerate(zip(ref, got)):
         assert torch.equal(r, x), i
     assert not torch.equal(ref[5], bias0[0]) and not torch.equal(ref[8], hb0[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1280, 512, 256, 256), (2560, 512, 128, 100), (512, 256, 320, 300)])
+@pytest.mark.parametrize("cd", [_lib.DT_F16, _lib.DT_BF16])
+def test_ws_row_tags_bit_identical(gpu, shape, cd):
+    """Row skipping (ocf.h OcfGemmArgs row_tag): with Adagrad and l2 = 0, rows whose tag differs from
+    row_tag_value (no batch entry in that column: zero gradient) are neither read nor written.  The
+    result -- parameters, slot, shadow, column sums -- equals the full update bit for bit; tagged
+    rows include every column with an entry plus random extra rows (a superset is allowed)."""
+    M, N, K, krows = shape
+    sp, dense = _sparse_batch(M, K, krows, seed=K + 1, col_frac=0.6)
+    bptr, ent = _buckets(sp, M, K)
+    _, Bm, state = _operands(cd, M, N, K, seed=9)
+    Ad = torch.from_numpy(dense).to(torch.float16 if cd == _lib.DT_F16 else torch.bfloat16).cuda()
+    rng = np.random.RandomState(M)
+    TAG = 7
+    tags = rng.randint(0, 256, size=M).astype(np.uint8)
+    tags[tags == TAG] = 0
+    used = (dense != 0).any(0)
+    tags[used] = TAG
+    tags[rng.rand(M) < 0.1] = TAG
+    assert (tags != TAG).sum() > M // 10          # there is something to skip
+    rt = torch.from_numpy(tags).cuda()
+    opt = OPTS["adagrad"](2e-3)
+    spb = dict(sp, sp_bptr=bptr, sp_ent=ent)
+    prev = set_ws(1)
+    try:
+        full = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True)
+        skip = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True,
+                    extra=dict(row_tag=rt, row_tag_value=TAG))
+    finally:
+        set_ws(prev)
+    for r, x in zip(full, skip):
+        assert torch.equal(r, x)
+    dead = torch.from_numpy(tags != TAG).cuda()
+    assert torch.equal(skip[0][dead], state[0][dead])      # untagged rows untouched
+    assert not torch.equal(skip[0][~dead], state[0][~dead])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["rmsprop", "adam", "adagrad_l2"])
+def test_ws_row_tags_rejected_unless_identity(gpu, opt):
+    """row tags are only valid where a zero gradient is an identity update (Adagrad, l2 = 0)"""
+    M, N, K = 256, 128, 64
+    A, Bm, state = _operands(_lib.DT_F16, M, N, K, seed=3)
+    rt = torch.ones(M, dtype=torch.uint8, device="cuda")
+    with pytest.raises(_lib.OcfError, match="row_tag"):
+        _run(_lib.DT_F16, M, N, K, OPTS[opt](1e-3), A, Bm, state, shadow_blocked=0,
+             extra=dict(row_tag=rt, row_tag_value=1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float16", "bfloat16"])
+def test_engine_row_skip_bit_identical(gpu, cd):
+    """Generator training steps with and without row skipping (Engine.row_skip): identical weights,
+    Adagrad slots and weight shadows after several steps on a wide, sparse dataset where most
+    columns of a batch hold no rating."""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B = 900, 4000, 30000, 128
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=3)
+    data = split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(3))
+    out = []
+    for skip in (False, True):
+        np.random.seed(5)
+        rd = data_reader(cols, rows, dataset=data, eval_mode="fixed_split")
+        om = om_ = omni_model(1, 200, cols, B, dense_activation="sigmoid", use_causal_info=False,
+                              compute_dtype=cd, seed=4)
+        eng = om.engine
+        eng.row_skip = skip
+        m = om.model
+        m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+        m.fit_generator(gen, 5, epochs=1, verbose=0)
+        assert eng._rtag_live == skip
+        torch.cuda.synchronize()
+        out.append([t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                   [s for sw, sb in eng.slots for s in sw + sb if s is not None] + [t.clone() for t in eng.Wsh])
+        del om_
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
