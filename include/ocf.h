@@ -239,12 +239,13 @@ typedef struct OcfGemmArgs {
   const float* jb_part; int jb_parts, jb_n; int64_t jb_ld; float* jb_p; float* jb_s1; float* jb_s2;
   OcfOptParams jb_op;
   const float* js_sp; const float* js_rs; float* js_out; int js_nparts, js_ntiles, js_M;
-  /* OPTIM with Adagrad and l2 == 0 (nullable): rows m with row_tag[m] != row_tag_value have an
-   * all-zero gradient (caller's guarantee, e.g. OcfScatterArgs rtag_*).  For them Keras' Adagrad
-   * update (a += 0; p -= lr * 0 / (sqrt(a) + eps)) is the identity, so the kernel skips their
-   * parameter / slot / shadow traffic; results are bit-identical to the full update.  Ignored by
-   * kernels that do not use it; rejected with any other optimizer or l2 != 0. */
-  const uint8_t* row_tag; int row_tag_value;
+  /* OPTIM with Adagrad and l2 == 0 (nullable): live-row records of M's 128-row tiles (layout:
+   * OCF_LIVE_REC below, built by ocf_sparse_tiles from the scatter's row tags).  Rows not listed
+   * have an all-zero gradient (caller's guarantee); for them Keras' Adagrad update (a += 0;
+   * p -= lr * 0 / (sqrt(a) + eps)) is the identity, so the kernel streams the parameter / slot /
+   * shadow traffic of the listed rows only; results are bit-identical to the full update.  Used by
+   * the role-split kernel, ignored by the generic one; rejected with any other optimizer or l2 != 0. */
+  const uint8_t* row_live;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
@@ -279,6 +280,11 @@ int ocf_stats_finalize(const float* stats_part, int n_parts, const float* row_ss
  * [gm*nk + 1]; ent: [cap][2] with cap >= the batch's entries in tiles < gm.  Built once per batch
  * and shared by both weight-gradient GEMMs (train split: inputs and targets share the descriptor).
  * Extension (no reference counterpart): feeds the persistent dW kernel. */
+/* live-row record of one 128-row tile (OCF_LIVE_REC bytes): int32 L = number of live rows at byte 0,
+ * then at byte 16 + (k % 8) * 16 + k / 8 the tile-local index of its k-th live row (ascending), k < L
+ * (the 16 row slots one stream thread of the dW kernel owns are contiguous: one 16-B load). */
+#define OCF_LIVE_REC 144
+
 typedef struct OcfTileBucketArgs {
   const int32_t* rows; const int64_t* rp; const int32_t* tptr; const int32_t* col; const int32_t* lidx;
   const int64_t* lboff;
@@ -288,6 +294,10 @@ typedef struct OcfTileBucketArgs {
   /* counted = 1: cnt already holds the counts (ocf_scatter_batch tb_cnt), the count pass is skipped;
    * cnt_clear (nullable): [gm*nk] counts zeroed by the fill pass (the next batch's counters) */
   int counted; int32_t* cnt_clear;
+  /* (nullable) live-row records (OCF_LIVE_REC bytes per tile, gm tiles) of the rows m < 128 gm whose
+   * tag equals rtag: live_in from rtag_in, live_out from rtag_out (OcfScatterArgs row tags) */
+  const uint8_t* rtag_in; const uint8_t* rtag_out; int rtag;
+  uint8_t* live_in; uint8_t* live_out;
 } OcfTileBucketArgs;
 int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
 

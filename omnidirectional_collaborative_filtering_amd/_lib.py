@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("OCF_LIB_PATH") or os.path.join(_HERE, "libocf.so")   
 DT_F32, DT_F16, DT_BF16 = 0, 1, 2
 ACT = {"linear": 0, None: 0, "sigmoid": 1, "tanh": 2, "relu": 3}
 OPT_SGD, OPT_ADAGRAD, OPT_RMSPROP, OPT_ADAM = 0, 1, 2, 3
+LIVE_REC = 144                 # ocf.h OCF_LIVE_REC
 EPI_SLAB, EPI_BIAS_ACT, EPI_GRAD_ACT, EPI_GRAD, EPI_OPTIM, EPI_PREDICT, EPI_MASKED_MSE = range(7)
 
 P = ctypes.c_void_p
@@ -90,7 +91,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("jb_part", P), ("jb_parts", I32), ("jb_n", I32), ("jb_ld", I64), ("jb_p", P), ("jb_s1", P), ("jb_s2", P),
         ("jb_op", OcfOptParams),
         ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
-        ("row_tag", P), ("row_tag_value", I32),
+        ("row_live", P),
     ]
 
 
@@ -99,6 +100,7 @@ class OcfTileBucketArgs(ctypes.Structure):
         ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
         ("krows", I32), ("ntiles", I32), ("gm", I32), ("nk", I32),
         ("cnt", P), ("bptr", P), ("ent", P), ("cap", I64), ("counted", I32), ("cnt_clear", P),
+        ("rtag_in", P), ("rtag_out", P), ("rtag", I32), ("live_in", P), ("live_out", P),
     ]
 
 

@@ -257,10 +257,9 @@ struct EpiOptim {
     void* shadow;      // compute-dtype copy of the updated weights (nullable)
     int shadow_dtype;
     bool shadow_blocked;  // shadow in the 64x64-blocked layout (else the layout of p)
-    // (optim_ws_kernel only) rows m with row_tag[m] != row_tag_value have a zero gradient and an
-    // identity update (Adagrad, l2 = 0; ocf.h OcfGemmArgs row_tag): their traffic is skipped
-    const uint8_t* row_tag = nullptr;
-    int row_tag_value = 0;
+    // (optim_ws_kernel only) live-row records (ocf.h OcfGemmArgs row_live, OCF_LIVE_REC): rows not
+    // listed have a zero gradient and an identity update (Adagrad, l2 = 0); their traffic is skipped
+    const uint8_t* row_live = nullptr;
   };
   // the parameter / slot values of the first chunk group do not depend on the product: with
   // OCF_OPT_PRE they are loaded before the K-loop

@@ -197,11 +197,9 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
         OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm OPTIM: parameter block over 2 GiB");
         OCF_CHECK(!g.p_shadow || g.compute_dtype != OCF_F32, "ocf_gemm OPTIM: shadow weights need f16/bf16 compute");
         OCF_CHECK(!g.shadow_blocked || g.ld_out % 64 == 0, "ocf_gemm OPTIM: blocked shadow needs ld_out % 64 == 0");
-        OCF_CHECK(!g.row_tag || (g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f && g.row_tag_value >= 1 &&
-                                 g.row_tag_value <= 255),
-                  "ocf_gemm OPTIM: row_tag needs Adagrad, l2 == 0 and 1 <= row_tag_value <= 255");
-        p.row_tag = g.row_tag;   // used by the role-split kernel; the generic kernel updates every row
-        p.row_tag_value = g.row_tag_value;
+        OCF_CHECK(!g.row_live || (g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f),
+                  "ocf_gemm OPTIM: row_live records need Adagrad with l2 == 0 (zero gradient = identity update)");
+        p.row_live = g.row_live;   // used by the role-split kernel; the generic kernel updates every row
         if constexpr (ACOL) {
           if constexpr (sizeof(CT) == 2) {
             // role-split kernel: slots present (SGD stays generic), row-major B, and for a sparse A

@@ -29,6 +29,9 @@ constexpr int WS_THREADS = 512;
 #ifndef OCF_WS_U
 #define OCF_WS_U 4
 #endif
+#ifndef OCF_WS_LOOP
+#define OCF_WS_LOOP 1   // stream groups of a tile: 1 run-time loop over the live groups; 0 all (dead slots OOB), 2 unrolled + skip (both measured 1-3 % slower)
+#endif
 constexpr int WS_YS = GT_BN;                              // Y row stride (floats), unpadded
 constexpr int WS_HALF = 64;                               // rows of a wave's operand half
 // chunks per group and groups per tile (16 float4 chunks per stream thread per tile)
@@ -70,61 +73,81 @@ template <typename CT> struct WaveStager {
 template <int KIND> struct WsSet {
   static constexpr int U = WsCfg<KIND>::U;
   float4 p[U], a[U], b[WsCfg<KIND>::NS == 2 ? U : 1];
-  uint64_t live;   // live-row bits of the tile this set holds (WsStream::live_rows)
 };
 
-// Row skipping (EpiOptim::Params row_tag): a stream thread's chunk j = g*U+u of a tile lies in
-// tile row 2*sw + (lane >> 5) + 8*j (sw = stream wave 0..3).  Each lane reads the tags of rows
-// 2*lane and 2*lane+1 (one u16), two ballots give the even- and odd-row live bits of the tile, and
-// a lane keeps its parity's mask shifted by sw, so chunk j is live iff bit 4*j is set.  Dead rows
-// get an out-of-range buffer offset: the load returns zeros without touching memory and the
-// stores are dropped.
+// Live rows (EpiOptim::Params row_live, ocf.h OCF_LIVE_REC): a stream thread's chunk slot j of a
+// tile is the live row of rank r0 + 8 j (r0 = stid / 32, columns (stid % 32) * 4 .. + 3), so the
+// live rows are streamed densely: group g (slots gU .. gU+U-1) exists iff 32 g < L for U = 4.  Slots
+// past L get an out-of-range buffer offset (the load returns zeros without touching memory, the
+// stores are dropped).  Without records every row is live and slot j is row r0 + 8 j.
 constexpr uint32_t WS_OOB = 0x80000000u;   // >= num_records (0x7FFFFFFF) of wt_rsrc
+struct WsRows {
+  int L;      // live rows of the tile (wave-uniform)
+  uint4 r;    // this thread's 16 row slots (tile-local row indices, one byte each)
+};
 
 template <int KIND> struct WsStream {
   static constexpr int U = WsCfg<KIND>::U;
   static constexpr int NS = WsCfg<KIND>::NS;
+  static constexpr int SLOTS = GT_BM * (GT_BN / 4) / GT_THREADS;   // 16 chunk slots per thread per tile
   EpiOptim::Params ep;
   __amdgpu_buffer_rsrc_t rp, r1, r2;
   const float* Y;
   int stid;
 
-  __device__ __forceinline__ int64_t off(int m0, int n0, int g, int u, int& ml, int& c4) const {
-    const int ch = stid + (g * U + u) * GT_THREADS;
-    ml = ch >> 5;
-    c4 = (ch & 31) * 4;
-    return (int64_t)(m0 + ml) * ep.ld + n0 + c4;
+  __device__ __forceinline__ WsRows rows_load(int m0) const {
+    WsRows q;
+    q.r = make_uint4(0, 0, 0, 0);
+    if (!ep.row_live) {
+      q.L = GT_BM;
+      return q;
+    }
+    const uint8_t* rec = ep.row_live + (int64_t)(m0 / GT_BM) * OCF_LIVE_REC;
+    q.L = *reinterpret_cast<const int*>(rec);
+    q.r = *reinterpret_cast<const uint4*>(rec + 16 + (stid >> 5) * 16);
+    return q;
   }
-  // tag of this lane's row pair in tile m0 (issued early; consumed by live_rows)
-  __device__ __forceinline__ uint32_t tag_load(int m0) const {
-    if (!ep.row_tag) return 0;
-    return *reinterpret_cast<const uint16_t*>(ep.row_tag + m0 + 2 * (stid & 63));
+  // groups of a tile (wave-uniform)
+  __device__ __forceinline__ int groups(const WsRows& q) const {
+    const int L = __builtin_amdgcn_readfirstlane(q.L);
+    const int ng = (L * (GT_BN / 4) + GT_THREADS * U - 1) / (GT_THREADS * U);
+    return ng < 1 ? 1 : ng;
   }
-  __device__ __forceinline__ uint64_t live_rows(uint32_t t2) const {
-    if (!ep.row_tag) return ~0ull;
-    const uint32_t tv = (uint32_t)ep.row_tag_value;
-    const uint64_t ev = __ballot((t2 & 0xffu) == tv), od = __ballot((t2 >> 8) == tv);
-    return (((stid >> 5) & 1) ? od : ev) >> (stid >> 6);
+  // chunk slot j: tile row ml, column c4; false = dead slot
+  __device__ __forceinline__ bool slot(const WsRows& q, int j, int& ml, int& c4) const {
+    const int k = (stid >> 5) + (GT_THREADS / 32) * j;
+    c4 = (stid & 31) * 4;
+    if (!ep.row_live) {
+      ml = k;
+      return true;
+    }
+    // word j / 4 of the slots by masks (a select chain on a run-time index becomes a stack array)
+    const uint32_t w = (uint32_t)(j >> 2);
+    const uint32_t word = (q.r.x & (0u - (uint32_t)(w == 0))) | (q.r.y & (0u - (uint32_t)(w == 1))) |
+                          (q.r.z & (0u - (uint32_t)(w == 2))) | (q.r.w & (0u - (uint32_t)(w == 3)));
+    const bool lv = k < q.L;
+    ml = lv ? (int)((word >> (8 * (j & 3))) & 0xff) : 0;
+    return lv;
   }
-  __device__ __forceinline__ void load(int m0, int n0, int g, WsSet<KIND>& s, uint64_t live) const {
-    s.live = live;
+  __device__ __forceinline__ void load(int m0, int n0, int g, WsSet<KIND>& s, const WsRows& q) const {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       int ml, c4;
-      const bool lv = (live >> (4 * (g * U + u))) & 1;
-      const uint32_t o = (uint32_t)(off(m0, n0, g, u, ml, c4) * 4) | (lv ? 0u : WS_OOB);
+      const bool lv = slot(q, g * U + u, ml, c4);
+      const uint32_t o = (uint32_t)(((int64_t)(m0 + ml) * ep.ld + n0 + c4) * 4) | (lv ? 0u : WS_OOB);
       s.p[u] = ld_pol16<OCF_OPT_LD_POL>(rp, ep.p, o);
       s.a[u] = ld_pol16<OCF_OPT_LD_POL>(r1, ep.s1, o);
       if constexpr (NS == 2) s.b[u] = ld_pol16<OCF_OPT_LD_POL>(r2, ep.s2, o);
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the prefetch above the consumer of the other set
   }
-  __device__ __forceinline__ void apply(int m0, int n0, int g, WsSet<KIND>& s) const {
+  __device__ __forceinline__ void apply(int m0, int n0, int g, WsSet<KIND>& s, const WsRows& q) const {
     const OcfOptParams o = ep.op;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       int ml, c4;
-      const int64_t of = off(m0, n0, g, u, ml, c4);
+      const bool lv = slot(q, g * U + u, ml, c4);
+      const int64_t of = (int64_t)(m0 + ml) * ep.ld + n0 + c4;
       const float4 gv = *reinterpret_cast<const float4*>(Y + ml * WS_YS + c4);
       float4 pv = s.p[u];
       float4 av = s.a[u];
@@ -134,7 +157,6 @@ template <int KIND> struct WsStream {
       opt_update_k<KIND>(o, gv.y * o.gscale, pv.y, av.y, bv.y);
       opt_update_k<KIND>(o, gv.z * o.gscale, pv.z, av.z, bv.z);
       opt_update_k<KIND>(o, gv.w * o.gscale, pv.w, av.w, bv.w);
-      const bool lv = (s.live >> (4 * (g * U + u))) & 1;
       const uint32_t ob = (uint32_t)(of * 4) | (lv ? 0u : WS_OOB);
       st_pol16<OCF_OPT_ST_POL>(rp, ep.p, ob, pv);
       if (ep.shadow && lv) EpiOptim::store_shadow(ep, m0 + ml, n0 + c4, pv);
@@ -409,7 +431,6 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
     // ------------------------------------------------------------------ stream role
     const WsStream<KIND> st{ep, wt_rsrc(ep.p), wt_rsrc(ep.s1), wt_rsrc(ep.s2), Y, tid - 256};
     WsSet<KIND> s0, s1;
-    constexpr int NG = WsCfg<KIND>::NG;
     auto origin = [&](int i, int& m0, int& n0) {
       const int t = sc.tile(i);
       m0 = (t / gn) * GT_BM;
@@ -417,33 +438,47 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
     };
     // one tile from Y: groups alternate register sets; the last group prefetches group 0 of the
     // next tile into set 0
-    // live-row bits: of the tile being streamed (cur) and of the next one, whose tags are loaded at
-    // the top of run_tile and turned into bits just before its first group is prefetched
-    uint64_t cur = ~0ull;
+    // live-row records: of the tile being streamed (qc) and of the next one, loaded at the top of
+    // run_tile and first used when its first group is prefetched
+    WsRows qc;
     auto run_tile = [&](int i) {
       int m0, n0, pm0 = 0, pn0 = 0;
       origin(i, m0, n0);
       const bool pre = i + 1 < sc.count;
       if (pre) origin(i + 1, pm0, pn0);
-      const uint32_t t2 = pre ? st.tag_load(pm0) : 0u;
-#pragma unroll
-      for (int g = 0; g < NG; g += 2) {
-        st.load(m0, n0, g + 1, s1, cur);
-        st.apply(m0, n0, g, s0);
-        if (g + 2 < NG) {
-          st.load(m0, n0, g + 2, s0, cur);
-        } else if (pre) {
-          cur = st.live_rows(t2);
-          st.load(pm0, pn0, 0, s0, cur);
+      const WsRows qn = pre ? st.rows_load(pm0) : qc;
+      const int ng = st.groups(qc);
+      if constexpr (OCF_WS_LOOP == 1) {     // run-time loop over the live groups
+        for (int g = 0; g < ng; g += 2) {
+          const bool two = g + 1 < ng;
+          if (two) st.load(m0, n0, g + 1, s1, qc);
+          st.apply(m0, n0, g, s0, qc);
+          if (g + 2 < ng) st.load(m0, n0, g + 2, s0, qc);
+          else if (pre) st.load(pm0, pn0, 0, s0, qn);
+          if (two) st.apply(m0, n0, g + 1, s1, qc);
         }
-        st.apply(m0, n0, g + 1, s1);
+      } else {                             // unrolled; 2: wave-uniform skip of dead groups, 0: none
+        constexpr int NG = WsCfg<KIND>::NG;
+        const int ne = OCF_WS_LOOP == 2 ? ng : NG;
+#pragma unroll
+        for (int g = 0; g < NG; g += 2) {
+          if (g < ne) {
+            const bool two = g + 1 < ne;
+            if (two) st.load(m0, n0, g + 1, s1, qc);
+            st.apply(m0, n0, g, s0, qc);
+            if (g + 2 < ne) st.load(m0, n0, g + 2, s0, qc);
+            else if (pre) st.load(pm0, pn0, 0, s0, qn);
+            if (two) st.apply(m0, n0, g + 1, s1, qc);
+          }
+        }
       }
+      qc = qn;
     };
     {
       int m0, n0;
       origin(0, m0, n0);
-      cur = st.live_rows(st.tag_load(m0));
-      st.load(m0, n0, 0, s0, cur);
+      qc = st.rows_load(m0);
+      st.load(m0, n0, 0, s0, qc);
     }
     {  // folded small jobs, one per stream wave, while the MFMA role runs the first K-loop; taken
        // from the last workgroups first (the last slots of each XCD range hold one tile less)

@@ -514,6 +514,19 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
   __shared__ int kt_cnt[64];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nb = a.gm * a.nk, before = t * a.nk;
+  // live-row records of tile t (ocf.h OCF_LIVE_REC): wave 0 from the input tags, wave 1 from the
+  // target tags; rank k of a live row = live rows before it in the tile
+  if (w < 2 && (w == 0 ? a.live_in : a.live_out)) {
+    const uint8_t* tg = (w == 0 ? a.rtag_in : a.rtag_out) + (int64_t)t * 128;
+    uint8_t* rec = (w == 0 ? a.live_in : a.live_out) + (int64_t)t * OCF_LIVE_REC;
+    const bool l0 = tg[lane] == (uint8_t)a.rtag, l1 = tg[64 + lane] == (uint8_t)a.rtag;
+    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1), below = (1ull << lane) - 1;
+    const int n0 = __popcll(b0);
+    const int k0 = __popcll(b0 & below), k1 = n0 + __popcll(b1 & below);
+    if (l0) rec[16 + (k0 & 7) * 16 + (k0 >> 3)] = (uint8_t)lane;
+    if (l1) rec[16 + (k1 & 7) * 16 + (k1 >> 3)] = (uint8_t)(64 + lane);
+    if (lane == 0) *reinterpret_cast<int*>(rec) = n0 + __popcll(b1);
+  }
   int s = 0;
   for (int i = tid; i < before; i += 256) s += a.cnt[i];
   red[tid] = s;
@@ -568,6 +581,8 @@ extern "C" int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream) {
   const int nb = a.gm * a.nk;
   hipStream_t s = (hipStream_t)stream;
   OCF_CHECK(a.cnt_clear != a.cnt, "ocf_sparse_tiles: cnt_clear must not alias cnt");
+  OCF_CHECK((!a.live_in || a.rtag_in) && (!a.live_out || a.rtag_out), "ocf_sparse_tiles: live records need row tags");
+  OCF_CHECK(!(a.live_in || a.live_out) || (a.rtag >= 1 && a.rtag <= 255), "ocf_sparse_tiles: 1 <= rtag <= 255");
   if (nb > 0 && !a.counted) {
     hipLaunchKernelGGL(tb_count_kernel, dim3((nb + 3) / 4), dim3(256), 0, s, a);
     OCF_HIP(hipGetLastError());

@@ -244,6 +244,8 @@ class Engine:
         # update is the identity (zero gradient).  Bit-identical to the full update.
         self.row_skip = True
         self.rtag = [torch.zeros(self.Np, device=d, dtype=torch.uint8) for _ in range(2)]   # inputs, targets
+        # per 128-row tile: the live rows (ocf.h OCF_LIVE_REC), built by ocf_sparse_tiles from the tags
+        self.live_rec = [torch.zeros(self.Np // TILE * _lib.LIVE_REC, device=d, dtype=torch.uint8) for _ in range(2)]
         self._rtag_val = 0
         self._rtag_live = False
         self._tb_par = 0
@@ -446,6 +448,9 @@ class Engine:
         ent = self._buf("tb_ent", 2 * self.gt["E"], torch.int32)
         a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
         a.counted, a.cnt_clear = 1, ptr(nxt)
+        if self._rtag_live:
+            a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
+            a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
         call("ocf_sparse_tiles", a, cur_stream())
         return dict(sp_bptr=bptr, sp_ent=ent)
 
@@ -753,7 +758,7 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             if self._rtag_live and self.sparse_dw and op.kind == _lib.OPT_ADAGRAD and op.l2 == 0:
-                sp.update(row_tag=self.rtag[0 if i == 0 else 1], row_tag_value=self._rtag_val)
+                sp.update(row_live=self.live_rec[0 if i == 0 else 1])
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
                        ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
         else:

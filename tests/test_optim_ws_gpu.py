@@ -44,7 +44,8 @@ def _sparse_batch(M, K, krows, seed, col_frac=None):
     if col_frac is None:
         col = np.concatenate([rng.choice(M, size=n, replace=False) for n in lens]).astype(np.int32)
     else:                                           # columns from a random subset only
-        pool = np.sort(rng.choice(M, size=int(M * col_frac), replace=False))
+        cand = np.setdiff1d(np.arange(M), np.arange(128, 256)) if M >= 384 else np.arange(M)   # tile 1 empty
+        pool = np.sort(rng.choice(cand, size=int(len(cand) * col_frac), replace=False))
         lens = np.minimum(lens, len(pool))
         rp[1:] = np.cumsum(lens)
         col = np.concatenate([rng.choice(pool, size=n, replace=False) for n in lens]).astype(np.int32)
@@ -69,7 +70,7 @@ def _sparse_batch(M, K, krows, seed, col_frac=None):
     return d, dense
 
 
-def _buckets(sp, M, K):
+def _buckets(sp, M, K, extra=None):
     """ocf_sparse_tiles on a sparse descriptor: (bptr, ent) device tensors"""
     gm, nk = M // 128, K // 64
     cap = max(1, int(sp["sp_lboff"][-1].item()) + 4 * M)
@@ -81,6 +82,8 @@ def _buckets(sp, M, K):
     a.col, a.lidx, a.lboff = sp["sp_col"].data_ptr(), sp["sp_lidx"].data_ptr(), sp["sp_lboff"].data_ptr()
     a.krows, a.ntiles, a.gm, a.nk = sp["sp_krows"], sp["sp_ntiles"], gm, nk
     a.cnt, a.bptr, a.ent, a.cap = cnt.data_ptr(), bptr.data_ptr(), ent.data_ptr(), cap
+    for k, v in (extra or {}).items():
+        setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
     _lib.call("ocf_sparse_tiles", a, cur_stream())
     torch.cuda.synchronize()
     return bptr, ent
@@ -281,17 +284,40 @@ def test_folded_jobs_match_separate_kernels(gpu, opt):
     assert not torch.equal(ref[5], bias0[0]) and not torch.equal(ref[8], hb0[0])
 
 
+def live_records(live):
+    """NumPy restatement of ocf.h OCF_LIVE_REC for a boolean live-row vector (len a multiple of 128)"""
+    gm = len(live) // 128
+    rec = np.zeros((gm, _lib.LIVE_REC), np.uint8)
+    for t in range(gm):
+        rows = np.nonzero(live[128 * t: 128 * t + 128])[0]
+        rec[t, :4] = np.frombuffer(np.int32(len(rows)).tobytes(), np.uint8)
+        for k, r in enumerate(rows):
+            rec[t, 16 + (k % 8) * 16 + k // 8] = r
+    return rec.reshape(-1)
+
+
+def _rec_valid(rec):
+    """(L per tile, the bytes of ranks < L) of a record array"""
+    rec = rec.reshape(-1, _lib.LIVE_REC)
+    L = rec[:, :4].copy().view(np.int32)[:, 0]
+    out = []
+    for t, n in enumerate(L):
+        out.append([rec[t, 16 + (k % 8) * 16 + k // 8] for k in range(n)])
+    return L, out
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(1280, 512, 256, 256), (2560, 512, 128, 100), (512, 256, 320, 300)])
 @pytest.mark.parametrize("cd", [_lib.DT_F16, _lib.DT_BF16])
-def test_ws_row_tags_bit_identical(gpu, shape, cd):
-    """Row skipping (ocf.h OcfGemmArgs row_tag): with Adagrad and l2 = 0, rows whose tag differs from
-    row_tag_value (no batch entry in that column: zero gradient) are neither read nor written.  The
-    result -- parameters, slot, shadow, column sums -- equals the full update bit for bit; tagged
-    rows include every column with an entry plus random extra rows (a superset is allowed)."""
+def test_ws_live_rows_bit_identical(gpu, shape, cd):
+    """Row skipping (ocf.h OcfGemmArgs row_live): with Adagrad and l2 = 0 only the listed rows of each
+    tile are streamed (densely, by rank); rows not listed (no batch entry in that column: zero
+    gradient) are neither read nor written.  The result -- parameters, slot, shadow, column sums --
+    equals the full update bit for bit; listed rows include every column with an entry plus random
+    extra rows (a superset is allowed).  The records come from ocf_sparse_tiles (checked against the
+    NumPy restatement)."""
     M, N, K, krows = shape
     sp, dense = _sparse_batch(M, K, krows, seed=K + 1, col_frac=0.6)
-    bptr, ent = _buckets(sp, M, K)
     _, Bm, state = _operands(cd, M, N, K, seed=9)
     Ad = torch.from_numpy(dense).to(torch.float16 if cd == _lib.DT_F16 else torch.bfloat16).cuda()
     rng = np.random.RandomState(M)
@@ -301,34 +327,48 @@ def test_ws_row_tags_bit_identical(gpu, shape, cd):
     used = (dense != 0).any(0)
     tags[used] = TAG
     tags[rng.rand(M) < 0.1] = TAG
-    assert (tags != TAG).sum() > M // 10          # there is something to skip
+    tags[:128][(rng.rand(128) < 0.5) & ~used[:128]] = TAG + 1     # tile 0: only the used rows live
+    if M >= 384:
+        assert not (dense[:, 128:256] != 0).any()
+        tags[128:256] = 0                           # tile 1: no live row at all
+    live = tags == TAG
+    assert (~live).sum() > M // 10                  # there is something to skip
+    # records through ocf_sparse_tiles (both record arrays; targets tagged with the inputs' tags)
+    gm, nk = M // 128, K // 64
     rt = torch.from_numpy(tags).cuda()
+    rec_in = torch.full((gm * _lib.LIVE_REC,), 0xEE, dtype=torch.uint8, device="cuda")
+    rec_out = torch.full_like(rec_in, 0xEE)
+    bptr, ent = _buckets(sp, M, K, extra=dict(rtag_in=rt, rtag_out=rt, rtag=TAG, live_in=rec_in, live_out=rec_out))
+    want_L, want = _rec_valid(live_records(live))
+    for rec in (rec_in, rec_out):
+        got_L, got = _rec_valid(rec.cpu().numpy())
+        np.testing.assert_array_equal(got_L, want_L)
+        assert got == want
     opt = OPTS["adagrad"](2e-3)
     spb = dict(sp, sp_bptr=bptr, sp_ent=ent)
     prev = set_ws(1)
     try:
         full = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True)
         skip = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True,
-                    extra=dict(row_tag=rt, row_tag_value=TAG))
+                    extra=dict(row_live=rec_in))
     finally:
         set_ws(prev)
     for r, x in zip(full, skip):
         assert torch.equal(r, x)
-    dead = torch.from_numpy(tags != TAG).cuda()
-    assert torch.equal(skip[0][dead], state[0][dead])      # untagged rows untouched
+    dead = torch.from_numpy(~live).cuda()
+    assert torch.equal(skip[0][dead], state[0][dead])      # rows not listed untouched
     assert not torch.equal(skip[0][~dead], state[0][~dead])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("opt", ["rmsprop", "adam", "adagrad_l2"])
-def test_ws_row_tags_rejected_unless_identity(gpu, opt):
-    """row tags are only valid where a zero gradient is an identity update (Adagrad, l2 = 0)"""
+def test_ws_live_rows_rejected_unless_identity(gpu, opt):
+    """live-row records are only valid where a zero gradient is an identity update (Adagrad, l2 = 0)"""
     M, N, K = 256, 128, 64
     A, Bm, state = _operands(_lib.DT_F16, M, N, K, seed=3)
-    rt = torch.ones(M, dtype=torch.uint8, device="cuda")
-    with pytest.raises(_lib.OcfError, match="row_tag"):
-        _run(_lib.DT_F16, M, N, K, OPTS[opt](1e-3), A, Bm, state, shadow_blocked=0,
-             extra=dict(row_tag=rt, row_tag_value=1))
+    rec = torch.from_numpy(live_records(np.ones(M, bool))).cuda()
+    with pytest.raises(_lib.OcfError, match="row_live"):
+        _run(_lib.DT_F16, M, N, K, OPTS[opt](1e-3), A, Bm, state, shadow_blocked=0, extra=dict(row_live=rec))
 
 
 @pytest.mark.gpu
