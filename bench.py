@@ -63,6 +63,10 @@ def parse():
                     help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
     ap.add_argument("--nt-operands", type=int, default=0,
                     help="non-temporal loads for GEMM operands at their last use in the step")
+    ap.add_argument("--ws-max-k", type=int, default=0,
+                    help="largest batch K routed to the role-split dW kernel (0: library default)")
+    ap.add_argument("--fold-jobs", type=int, default=1,
+                    help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -155,6 +159,10 @@ def main():
         eng.sparse_dw = bool(args.sparse_dw)
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
+    eng.fold_jobs = bool(args.fold_jobs)
+    if args.ws_max_k:
+        from omnidirectional_collaborative_filtering_amd import _lib
+        _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)

@@ -264,6 +264,22 @@ __device__ __forceinline__ void sparse_a_fill(const GemmShape& sh, char* img, in
 }
 
 // one K-step of the wave's 64x64 sub-tile (2x2 blocks of 32x32) from the LDS operand images
+// column c of a [K][M] LDS image summed over its BK rows in k order (the output-bias gradient):
+// loads batched 16 at a time so the fixed-order add chain does not wait on each LDS read
+template <typename CT, int BK>
+__device__ __forceinline__ float colsum_kstep(const char* img, int stride, int c) {
+  float s0 = 0.f;
+#pragma unroll
+  for (int k0 = 0; k0 < BK; k0 += 16) {
+    CT v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = *reinterpret_cast<const CT*>(img + (k0 + j) * stride + c * (int)sizeof(CT));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s0 += (float)v[j];
+  }
+  return s0;
+}
+
 template <typename CT, bool ACOL, bool BCOL, int RA = GT_BM, int RB = GT_BN>
 __device__ __forceinline__ void mfma_kstep(const char* bufA, const char* bufB, int wm, int wn, int lane,
                                            ocf_f16v (&acc)[2][2]) {
@@ -470,10 +486,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     auto sum_a = [&](const char* img) {      // column sums of the A image (fixed k order), [K][M] A only
       if constexpr (ACOL) {
         if (colsum && tid < GT_BM) {
-          using I = Img<CT, GT_BM, true>;
-          float s0 = 0.f;
-          for (int k = 0; k < BK; ++k) s0 += (float)*reinterpret_cast<const CT*>(img + k * I::STRIDE + tid * (int)sizeof(CT));
-          csum += s0;
+          csum += colsum_kstep<CT, BK>(img, Img<CT, GT_BM, true>::STRIDE, tid);
         }
       }
     };

@@ -181,6 +181,19 @@ struct WsSched {
   __device__ __forceinline__ int tile(int i) const { return first + i * stride; }
 };
 
+// tile t -> origin: panel m = t / gn; its gn column tiles are rotated by m / 8, so a workgroup
+// (which takes every (G/8)-th tile, G/8 a multiple of gn) cycles through the column tiles instead of
+// always drawing the same one -- the n0 == 0 tiles carry the output-bias column sums and would
+// otherwise all land on a quarter of the workgroups
+__device__ __forceinline__ void ws_tile_origin(int t, int gn, int& m0, int& n0) {
+  const int m = t / gn;
+  m0 = m * GT_BM;
+#ifndef OCF_WS_ROTATE
+#define OCF_WS_ROTATE 1
+#endif
+  n0 = ((t % gn + (OCF_WS_ROTATE ? (m >> 3) : 0)) % gn) * GT_BN;
+}
+
 // small jobs of the step folded into the launch (ocf.h OcfGemmArgs cb_* / jb_* / js_*), done by the
 // stream role while it waits for the first tile and by the colsum waves.  Each reproduces the
 // arithmetic and summation order of the kernel it replaces (bias_opt_partials_kernel,
@@ -262,11 +275,19 @@ struct WsJobs {
     else if (j == nbj) stats_totals(lane);
     else stats_row(j - nbj - 1, lane);
   }
-  // output-layer bias from its column sum (bias_opt_partials_kernel with one partial)
+  // output-layer bias from its column sum (bias_opt_partials_kernel with one partial); the bias and
+  // its slots are loaded when the tile starts (colsum_pre) so the update does not stall the MFMA
+  // role at the tile hand-off
+  struct BiasPre {
+    float w, a, b;
+  };
+  __device__ __forceinline__ BiasPre colsum_pre(int m) const {
+    return BiasPre{cb_p[m], cb_s1 ? cb_s1[m] : 0.f, cb_s2 ? cb_s2[m] : 0.f};
+  }
   template <int KIND>
-  __device__ __forceinline__ void colsum_bias(int m, float v) const {
+  __device__ __forceinline__ void colsum_bias(int m, float v, BiasPre q) const {
     const float g = (v + 0.f) + (0.f + 0.f);
-    float w = cb_p[m], a = cb_s1 ? cb_s1[m] : 0.f, b = cb_s2 ? cb_s2[m] : 0.f;
+    float w = q.w, a = q.a, b = q.b;
     opt_update_k<KIND>(cb_op, g, w, a, b);
     cb_p[m] = w;
     if (cb_s1) cb_s1[m] = a;
@@ -318,8 +339,7 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
     const int total = sc.count * nk;                      // K-steps over all of this WG's tiles
     auto tile_of = [&](int q, int& m0, int& n0) {
       const int t = sc.tile(q / nk);
-      m0 = (t / gn) * GT_BM;
-      n0 = (t % gn) * GT_BN;
+      ws_tile_origin(t, gn, m0, n0);
     };
     // sparse A: bucket of step q = (column tile m0/128, K-step q % nk)
     auto bucket_issue = [&](int q, WsBucket& bk) {
@@ -358,31 +378,46 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
     };
     // colsum (output-bias gradient): the wn == 0 waves sum their 64 A columns over k, in order
     float csum = 0.f;
-    auto sum_a = [&]() {
-      float s0 = 0.f;
-      for (int k = 0; k < BK; ++k) s0 += (float)*reinterpret_cast<const CT*>(imgA + k * I::STRIDE + lane * 2);
-      csum += s0;
-    };
+    auto sum_a = [&]() { csum += colsum_kstep<CT, BK>(imgA, I::STRIDE, lane); };
 
-    // prologue: step 0 staged; sparse: entries of step 1 in flight
-    WsBucket b_next{}, b_next2{};
-    issue(0);
+    // prologue: step 0 staged; sparse: entries of step 1 and B of step 1 in flight
+    auto issue_b = [&](int q, WaveStager<CT>& st) {
+      int m0, n0;
+      tile_of(q, m0, n0);
+      st.load(tile_rsrc(Bg + n0 + wn), sh.ldb, (q % nk) * stb, lane);
+    };
+    // sparse A pipeline: bucket entries three K-steps ahead, their values two ahead (each load of the
+    // index -> value chain has a whole K-step of slack)
+    WsBucket b_next{}, b_next2{}, b_next3{};
+    float v_next = 0.f;
     if constexpr (SPA) {
+      issue_b(0, sb);
       WsBucket b0;
       bucket_issue(0, b0);
       if (total > 1) bucket_issue(1, b_next);
-      fill(b0, val_of(b0));
+      if (total > 2) bucket_issue(2, b_next2);
+      const float v0 = val_of(b0);
+      if (total > 1) v_next = val_of(b_next);
+      fill(b0, v0);
     } else {
+      issue(0);
       sa.store(imgA, lane);
     }
     sb.store(imgB, lane);
 
     ocf_f16v acc[2][2];
-    for (int q = 0; q < total; ++q) {
+    WsJobs::BiasPre bpre{0.f, 0.f, 0.f};
+    // K-step q: operands of step q+1 in flight during its MFMAs (measured: a second B stage for long
+    // K loops gains nothing and costs 32 VGPRs)
+    auto body = [&](int q) {
       const int kt = q % nk;
       int m0, n0;
       tile_of(q, m0, n0);
+#ifdef OCF_WS_DIAG_NOCOLSUM
+      const bool colsum = false;   // diagnostics only (wrong bias gradient): the cost of the column sums
+#else
       const bool colsum = sh.sp_colsum && n0 == 0 && wn == 0;
+#endif
       if (kt == 0) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)
@@ -391,30 +426,36 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
         csum = 0.f;
+        if (colsum && jobs.cb_p) bpre = jobs.colsum_pre(m0 + wm + lane);
       }
       if (colsum) sum_a();
       const bool more = q + 1 < total;
-      float vnext = 0.f;
+      float v_next2 = 0.f;
       if constexpr (SPA) {
-        if (q + 2 < total) bucket_issue(q + 2, b_next2);
-        if (more) vnext = val_of(b_next);
+        if (q + 3 < total) bucket_issue(q + 3, b_next3);
+        if (q + 2 < total) v_next2 = val_of(b_next2);
+        if (more) issue_b(q + 1, sb);
+      } else {
+        if (more) issue(q + 1);
       }
-      if (more) issue(q + 1);
       mfma_kstep<CT, true, true, WS_HALF, WS_HALF>(imgA, imgB, 0, 0, lane, acc);
       if (more) {
         if constexpr (SPA) {
-          fill(b_next, vnext);
+          fill(b_next, v_next);
           b_next = b_next2;
+          b_next2 = b_next3;
+          v_next = v_next2;
+          sb.store(imgB, lane);
         } else {
           sa.store(imgA, lane);
+          sb.store(imgB, lane);
         }
-        sb.store(imgB, lane);
       }
       if (kt == nk - 1) {
         if (colsum) {
           const float v = csum * sh.colsum_scale;
           sh.sp_colsum[m0 + wm + lane] = v;
-          if (jobs.cb_p) jobs.colsum_bias<KIND>(m0 + wm + lane, v);
+          if (jobs.cb_p) jobs.colsum_bias<KIND>(m0 + wm + lane, v, bpre);
         }
         lds_barrier();   // A: product of this tile ready; the stream role is done with Y
 #pragma unroll
@@ -426,15 +467,15 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
               Y[(wm + acc_row(bi, r, lane)) * WS_YS + wn + acc_col(bj, lane)] = acc[bi][bj][r];
         lds_barrier();   // B: Y holds this tile
       }
-    }
+    };
+    for (int q = 0; q < total; ++q) body(q);
   } else {
     // ------------------------------------------------------------------ stream role
     const WsStream<KIND> st{ep, wt_rsrc(ep.p), wt_rsrc(ep.s1), wt_rsrc(ep.s2), Y, tid - 256};
     WsSet<KIND> s0, s1;
     auto origin = [&](int i, int& m0, int& n0) {
       const int t = sc.tile(i);
-      m0 = (t / gn) * GT_BM;
-      n0 = (t % gn) * GT_BN;
+      ws_tile_origin(t, gn, m0, n0);
     };
     // one tile from Y: groups alternate register sets; the last group prefetches group 0 of the
     // next tile into set 0
