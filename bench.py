@@ -67,6 +67,8 @@ def parse():
                     help="largest batch K routed to the role-split dW kernel (0: library default)")
     ap.add_argument("--fold-jobs", type=int, default=1,
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
+    ap.add_argument("--shadow-blocked", type=int, default=-1,
+                    help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -160,6 +162,9 @@ def main():
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
+    if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
+        eng.shadow_blocked = bool(args.shadow_blocked)
+        eng._refresh_shadows()
     if args.ws_max_k:
         from omnidirectional_collaborative_filtering_amd import _lib
         _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)

@@ -50,7 +50,7 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
 // parallel global batch) the K-loop dominates and the generic kernel's two workgroups per CU win
 // (dW 132 / 111 us vs 175 / 137 us).
 int g_optim_ws = -1;
-int g_optim_ws_max_k = 256;
+int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
 bool optim_ws_on() {
   if (g_optim_ws < 0) {
     const char* e = std::getenv("OCF_OPTIM_WS");

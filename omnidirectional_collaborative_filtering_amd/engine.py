@@ -107,8 +107,10 @@ class Engine:
         # optimizer epilogue gives bit-identical products at half the bytes
         self.Wsh = [None] * len(self.W)
         # shadows stored 64x64-blocked: a GEMM K-step reads two contiguous 8 KB blocks instead of 64-128
-        # strided row pieces (tools/probes/hbm_pattern.hip: 5.0 vs 3.7-4.0 TB/s from HBM)
-        self.shadow_blocked = True
+        # strided row pieces (tools/probes/hbm_pattern.hip: 5.0 vs 3.7-4.0 TB/s from HBM).  Models that
+        # take the row-gather path (one 1-block input layer, H <= 512) read the shadows by whole rows
+        # instead (one contiguous 1 KB row per entry): row-major there (ML-20M step 0.512 -> 0.506 ms)
+        self.shadow_blocked = not (self.k == 1 and self.Hp[0] <= 512 and self.Hp[-1] <= 512)
         if self.cdt != _lib.DT_F32:
             for i in sorted({0, len(self.W) - 1}):
                 self.Wsh[i] = torch.zeros(self.W[i].shape, device=self.dev, dtype=self.tdt)
@@ -233,8 +235,9 @@ class Engine:
         # dW_out / dW_in operand A: built in LDS from the entries (sparse A, ocf.h a_sparse; no dense
         # [B][N] arrays, no memsets) or the dense d_out / xin.  The sparse fill pays a chain of dependent
         # index loads per K-step, so it wins only for short K loops: ML-20M, 1 GPU (K = 256): 0.774 vs
-        # 0.811 ms/step; 8-way feature parallel (K = 2,048 global rows): 0.538 vs 0.389 ms/step.
-        self.sparse_dw = Bp <= 256
+        # 0.811 ms/step; with the bucketed role-split kernel, rank 0 of a feature-parallel job: 2-way
+        # (K = 512) 0.453 vs 0.509, 4-way (K = 1,024) 0.42 vs 0.38, 8-way (K = 2,048) 0.46 vs 0.375.
+        self.sparse_dw = Bp <= 512
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
