@@ -351,23 +351,41 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
       bk.e = lane < bk.n ? sh.sp_ent[bk.lo + lane] : make_int2(0, -1);
     };
     auto val_of = [&](const WsBucket& bk) { return bk.e.y >= 0 ? sh.sp_vals[bk.e.x] : 0.f; };
-    auto fill = [&](const WsBucket& bk, float v0) {
-      // zero this wave's A half, then scatter the bucket's entries that fall in it
+    // The A half is zeroed once; afterwards each fill first clears only the previous K-step's entries
+    // (one 2-B store per lane instead of 8 KB of zeros per wave and K-step), unless that bucket
+    // overflowed 64 entries (rare: then the whole half is zeroed again)
+    auto zero_a = [&]() {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int c = lane + 64 * i;
         *reinterpret_cast<uint4*>(imgA + (c >> 3) * I::STRIDE + (c & 7) * 16) = make_uint4(0, 0, 0, 0);
       }
+    };
+    int2 e_prev = make_int2(0, -1);
+    int n_prev = 0;
+    auto fill = [&](const WsBucket& bk, float v0) {
+      auto at = [&](int2 e, int& k, int& m) {
+        k = e.y & 255;
+        m = (e.y >> 8) - wm;
+        return e.y >= 0 && (unsigned)m < 64u;
+      };
+      if (__builtin_amdgcn_readfirstlane(n_prev) > 64) {
+        zero_a();
+      } else {
+        int k, m;
+        if (at(e_prev, k, m)) *reinterpret_cast<CT*>(imgA + k * I::STRIDE + m * 2) = CvtT<CT>::to(0.f);
+      }
       auto put = [&](int2 e, float v) {
-        const int k = e.y & 255, m = (e.y >> 8) - wm;
-        if (e.y >= 0 && (unsigned)m < 64u && v != 0.f)
-          *reinterpret_cast<CT*>(imgA + k * I::STRIDE + m * 2) = CvtT<CT>::to(v);
+        int k, m;
+        if (at(e, k, m) && v != 0.f) *reinterpret_cast<CT*>(imgA + k * I::STRIDE + m * 2) = CvtT<CT>::to(v);
       };
       put(bk.e, v0);
       for (int j = 64 + lane; j < bk.n; j += 64) {        // buckets beyond 64 entries (rare)
         const int2 e = sh.sp_ent[bk.lo + j];
         put(e, sh.sp_vals[e.x]);
       }
+      e_prev = bk.e;
+      n_prev = bk.n;
     };
     auto issue = [&](int q) {                              // operand loads of step q into registers
       int m0, n0;
@@ -398,6 +416,7 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
       if (total > 2) bucket_issue(2, b_next2);
       const float v0 = val_of(b0);
       if (total > 1) v_next = val_of(b_next);
+      zero_a();
       fill(b0, v0);
     } else {
       issue(0);
