@@ -69,6 +69,8 @@ def parse():
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
                     help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
+    ap.add_argument("--dw-rows", type=int, default=-1,
+                    help="weight gradients row by row from the entries (1) or by the MFMA role-split kernel (0)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -162,6 +164,8 @@ def main():
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
+    if args.dw_rows >= 0:
+        eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
         eng.shadow_blocked = bool(args.shadow_blocked)
         eng._refresh_shadows()

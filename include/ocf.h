@@ -246,6 +246,12 @@ typedef struct OcfGemmArgs {
    * shadow traffic of the listed rows only; results are bit-identical to the full update.  Used by
    * the role-split kernel, ignored by the generic one; rejected with any other optimizer or l2 != 0. */
   const uint8_t* row_live;
+  /* OPTIM / a_col = 1, a_sparse (nullable): the same sparse A as row lists (OcfTileBucketArgs row_ptr /
+   * row_ent; values sp_vals).  With them the weight gradient is computed row by row from the entries
+   * (g[m][:] = sum over the entries (v, k) of column m, in k order, of v * B[k][:], fp32) and updated
+   * in place by one wave per row -- no MFMA over the mostly-zero A; with Adagrad and l2 == 0 rows
+   * without entries are skipped (identity update).  Requires N % 128 == 0, N <= 512. */
+  const int32_t* sp_rowptr; const int32_t* sp_rowent;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
@@ -298,6 +304,10 @@ typedef struct OcfTileBucketArgs {
    * tag equals rtag: live_in from rtag_in, live_out from rtag_out (OcfScatterArgs row tags) */
   const uint8_t* rtag_in; const uint8_t* rtag_out; int rtag;
   uint8_t* live_in; uint8_t* live_out;
+  /* (nullable) row lists, the transpose of the buckets: for row m < 128 gm, the entries of column m
+   * ordered by batch row, as pairs (value index, k) at row_ent[row_ptr[m] .. row_ptr[m+1]) (row_ent:
+   * [cap][2]; row_ptr: [128 gm + 1]).  Deterministic (no atomics in the ordering). */
+  int32_t* row_ptr; int32_t* row_ent;
 } OcfTileBucketArgs;
 int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
 

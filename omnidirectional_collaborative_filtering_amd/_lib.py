@@ -91,7 +91,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("jb_part", P), ("jb_parts", I32), ("jb_n", I32), ("jb_ld", I64), ("jb_p", P), ("jb_s1", P), ("jb_s2", P),
         ("jb_op", OcfOptParams),
         ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
-        ("row_live", P),
+        ("row_live", P), ("sp_rowptr", P), ("sp_rowent", P),
     ]
 
 
@@ -101,6 +101,7 @@ class OcfTileBucketArgs(ctypes.Structure):
         ("krows", I32), ("ntiles", I32), ("gm", I32), ("nk", I32),
         ("cnt", P), ("bptr", P), ("ent", P), ("cap", I64), ("counted", I32), ("cnt_clear", P),
         ("rtag_in", P), ("rtag_out", P), ("rtag", I32), ("live_in", P), ("live_out", P),
+        ("row_ptr", P), ("row_ent", P),
     ]
 
 

@@ -7,6 +7,7 @@
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
 #include "ocf_optim_ws.h"
+#include "ocf_rows_dw.h"
 
 using namespace ocf;
 
@@ -49,6 +50,7 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
 // (ML-20M, one GPU) 238-251 us vs 290-316 us for the generic kernel; at K = 2,048 (8-way feature
 // parallel global batch) the K-loop dominates and the generic kernel's two workgroups per CU win
 // (dW 132 / 111 us vs 175 / 137 us).
+int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (ocf_set_tuning "optim_rows")
 int g_optim_ws = -1;
 int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
 bool optim_ws_on() {
@@ -91,6 +93,48 @@ void jobs_after(const OcfGemmArgs& g, hipStream_t s) {
   if (g.cb_p)
     OCF_CHECK(ocf_bias_opt_from_partials(g.cb_p, g.sp_colsum, 1, g.M, g.M, g.cb_s1, g.cb_s2, nullptr, &g.cb_op, s) == 0,
               ocf_last_error());
+}
+
+// EPI_OPTIM over a sparse batch operand given as row lists: one wave per weight row (ocf_rows_dw.h)
+template <typename CT>
+bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
+  const int cpl = g.N / 64;
+  if (!(g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N)) return false;
+  if (ep.shadow && ep.shadow_blocked && cpl % 4 != 0) return false;
+  RowsDwArgs ra{};
+  ra.p = g.p; ra.s1 = g.s1; ra.s2 = g.s2; ra.ld = g.ld_out; ra.M = g.M; ra.N = g.N;
+  ra.B = g.B; ra.ldb = g.ldb;
+  ra.rowptr = g.sp_rowptr; ra.rowent = reinterpret_cast<const int2*>(g.sp_rowent); ra.vals = g.sp_vals;
+  ra.op = g.opt;
+  ra.shadow = ep.shadow; ra.shadow_dtype = ep.shadow_dtype; ra.shadow_blocked = ep.shadow_blocked;
+  ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
+  ra.skip_empty = g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f;
+  const WsJobs jb = ws_jobs(g);
+  const int waves = (g.M + RW_BLOCK - 1) / RW_BLOCK;
+  const int grid = std::max(1, (std::max(waves, jb.count()) + 3) / 4);
+  auto go = [&](auto kind_tag, auto cpl_tag) {
+    constexpr int KIND = decltype(kind_tag)::value, CPL = decltype(cpl_tag)::value;
+    hipLaunchKernelGGL((optim_rows_kernel<CT, KIND, CPL>), dim3(grid), dim3(RW_THREADS), 0, s, ra, jb);
+  };
+  auto by_cpl = [&](auto kind_tag) {
+    switch (cpl) {
+      case 2: go(kind_tag, std::integral_constant<int, 2>{}); break;
+      case 4: go(kind_tag, std::integral_constant<int, 4>{}); break;
+      case 6: go(kind_tag, std::integral_constant<int, 6>{}); break;
+      default: go(kind_tag, std::integral_constant<int, 8>{});
+    }
+  };
+  switch (g.opt.kind) {
+    case OCF_OPT_ADAGRAD: by_cpl(std::integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
+    case OCF_OPT_RMSPROP: by_cpl(std::integral_constant<int, OCF_OPT_RMSPROP>{}); break;
+    case OCF_OPT_ADAM:
+      OCF_CHECK(g.s2, "ocf_gemm OPTIM: Adam needs both slots");
+      by_cpl(std::integral_constant<int, OCF_OPT_ADAM>{});
+      break;
+    default: by_cpl(std::integral_constant<int, 0>{});
+  }
+  OCF_HIP(hipGetLastError());
+  return true;
 }
 
 // EPI_OPTIM on [K][M] x [K][N] operands (the dW GEMMs) through the persistent role-split kernel
@@ -201,6 +245,8 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
                   "ocf_gemm OPTIM: row_live records need Adagrad with l2 == 0 (zero gradient = identity update)");
         p.row_live = g.row_live;   // used by the role-split kernel; the generic kernel updates every row
         if constexpr (ACOL) {
+          // row lists of a sparse batch operand: one wave per weight row, no MFMA over the zeros
+          if (g.a_sparse && g.sp_rowptr && g.sp_rowent && g.sp_vals && g_optim_rows && launch_rows<CT>(g, p, s)) return;
           if constexpr (sizeof(CT) == 2) {
             // role-split kernel: slots present (SGD stays generic), row-major B, and for a sparse A
             // the (column tile, K-step) buckets of ocf_sparse_tiles
@@ -270,7 +316,10 @@ void dispatch(const OcfGemmArgs& g, hipStream_t s) {
 extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   OCF_TRY_BEGIN
   const std::string k = key ? key : "";
-  if (k == "optim_ws") {
+  if (k == "optim_rows") {
+    if (previous) *previous = g_optim_rows;
+    g_optim_rows = value ? 1 : 0;
+  } else if (k == "optim_ws") {
     if (previous) *previous = optim_ws_on() ? 1 : 0;
     g_optim_ws = value ? 1 : 0;
   } else if (k == "optim_ws_max_k") {

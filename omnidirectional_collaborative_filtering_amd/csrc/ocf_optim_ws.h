@@ -204,7 +204,7 @@ struct WsJobs {
   OcfOptParams jb_op;
   const float* js_sp; const float* js_rs; float* js_out; int js_nparts, js_ntiles, js_M;
 
-  __device__ __forceinline__ int count() const {
+  __host__ __device__ __forceinline__ int count() const {
     int n = jb_part ? (jb_n + 63) / 64 : 0;
     if (js_sp) n += 1 + (js_rs ? js_M : 0);
     return n;
@@ -214,8 +214,9 @@ struct WsJobs {
   __device__ __forceinline__ void bias_block(int blk, int lane) const {
     const int i = blk * 64 + lane;
     if (i >= jb_n) return;
-    // 64 loads in flight per batch (group k & 3 of row k), added per group in row order
-    constexpr int NB = 64;
+    // 16 loads in flight per batch (group k & 3 of row k), added per group in row order (the sums are
+    // those of any batch size that is a multiple of 4; 16 keeps the jobs' register footprint small)
+    constexpr int NB = 16;
     float p[4] = {0.f, 0.f, 0.f, 0.f};
     for (int k0 = 0; k0 < jb_parts; k0 += NB) {
       float x[NB];

@@ -506,6 +506,67 @@ __global__ void __launch_bounds__(256) tb_count_kernel(OcfTileBucketArgs a) {
   if (lane == 0) a.cnt[id] = tot;
 }
 
+// Row lists of tile t (ocf.h OcfTileBucketArgs row_ptr / row_ent), from the tile's buckets just
+// written by this workgroup (entries in (K-step, batch row, column) order): a counting sort by column
+// whose rank inside a column is the number of earlier same-column entries (chunks of 256 in order,
+// an LDS scan inside a chunk), so every column's list is in batch-row order without atomics deciding
+// the order.
+__device__ void tb_rows(const OcfTileBucketArgs& a, int t, int tile_base) {
+  __shared__ int cnt_m[128], base_m[128], kofs[65];
+  __shared__ uint8_t mch[256];
+  const int tid = threadIdx.x;
+  const int nk = a.nk, before = t * nk;
+  if (tid < 128) cnt_m[tid] = 0;
+  if (tid <= nk) kofs[tid] = 0;
+  __syncthreads();
+  if (tid < 64) {                       // bucket offsets of the tile, relative to its first entry
+    const int v = tid < nk ? a.cnt[before + tid] : 0;
+    const int incl = wave_incl_scan(v, tid);
+    if (tid < nk) kofs[tid] = incl - v;
+    if (tid == nk - 1) kofs[nk] = incl;
+  }
+  __syncthreads();
+  const int n = kofs[nk];
+  const int2* ent = reinterpret_cast<const int2*>(a.ent) + tile_base;
+  const bool fits = (int64_t)tile_base + n <= a.cap;
+  if (fits)
+    for (int i = tid; i < n; i += 256) atomicAdd(&cnt_m[ent[i].y >> 8], 1);   // counts only: order-free
+  __syncthreads();
+  if (tid < 64) {                       // exclusive scan of the column counts, two columns per lane
+    const int c0 = fits ? cnt_m[2 * tid] : 0, c1 = fits ? cnt_m[2 * tid + 1] : 0;
+    const int incl = wave_incl_scan(c0 + c1, tid), ex = incl - c0 - c1;
+    base_m[2 * tid] = ex;
+    base_m[2 * tid + 1] = ex + c0;
+    a.row_ptr[t * 128 + 2 * tid] = tile_base + ex;
+    a.row_ptr[t * 128 + 2 * tid + 1] = tile_base + ex + c0;
+    if (t == a.gm - 1 && tid == 63) a.row_ptr[a.gm * 128] = tile_base + incl;
+  }
+  __syncthreads();
+  if (!fits) return;
+  int2* rent = reinterpret_cast<int2*>(a.row_ent) + tile_base;
+  for (int c0 = 0; c0 < n; c0 += 256) {
+    const int i = c0 + tid;
+    int2 e = make_int2(0, 0);
+    int m = -1;
+    if (i < n) {
+      e = ent[i];
+      m = e.y >> 8;
+      mch[tid] = (uint8_t)m;
+    }
+    __syncthreads();
+    if (i < n) {
+      int r = 0;
+      for (int j = 0; j < tid; ++j) r += mch[j] == m;
+      int kt = 0;                         // the entry's K-step: the bucket holding position i
+      while (kt + 1 < nk && kofs[kt + 1] <= i) ++kt;
+      rent[base_m[m] + r] = make_int2(e.x, kt * 64 + (e.y & 255));
+    }
+    __syncthreads();
+    if (i < n) atomicAdd(&base_m[m], 1);   // the chunk's entries of m precede the next chunk's
+    __syncthreads();
+  }
+}
+
 // one workgroup per column tile t: its base = sum of the counts of all earlier buckets (a parallel
 // fixed-order sum, cheap at a few thousand buckets, and no separate scan launch), then one wave per
 // K-step writes its rows' segments at the wave-prefix offsets; the last workgroup writes bptr[total]
@@ -567,6 +628,7 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
     }
     __syncthreads();
   }
+  if (a.row_ptr) tb_rows(a, t, tile_base);
 }
 
 }  // namespace ocf
@@ -578,6 +640,7 @@ extern "C" int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream) {
             "ocf_sparse_tiles: null pointer");
   OCF_CHECK(a.gm >= 0 && a.nk >= 0 && a.gm <= a.ntiles && a.krows <= 64 * a.nk,
             "ocf_sparse_tiles: gm <= ntiles and krows <= 64 * nk required");
+  OCF_CHECK(!a.row_ptr || (a.row_ent && a.nk <= 64), "ocf_sparse_tiles: row lists need row_ent and nk <= 64");
   const int nb = a.gm * a.nk;
   hipStream_t s = (hipStream_t)stream;
   OCF_CHECK(a.cnt_clear != a.cnt, "ocf_sparse_tiles: cnt_clear must not alias cnt");

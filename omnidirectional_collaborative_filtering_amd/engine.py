@@ -239,6 +239,11 @@ class Engine:
         # (K = 512) 0.453 vs 0.509, 4-way (K = 1,024) 0.42 vs 0.38, 8-way (K = 2,048) 0.46 vs 0.375.
         self.sparse_dw = Bp <= 512
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
+        # ... or as row lists (the buckets' transpose): the weight gradient row by row from the entries,
+        # one wave per weight row, no MFMA over the mostly-zero batch operand (ocf_rows_dw.h).  Measured
+        # slower than the role-split MFMA kernel (ML-20M step 0.534 vs 0.508 ms; 8-way feature-parallel
+        # rank step 0.411 vs 0.374 on the generic kernel): each row pays a dependent entry -> B chain.
+        self.dw_rows = False
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
@@ -451,11 +456,17 @@ class Engine:
         ent = self._buf("tb_ent", 2 * self.gt["E"], torch.int32)
         a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
         a.counted, a.cnt_clear = 1, ptr(nxt)
+        out = dict(sp_bptr=bptr, sp_ent=ent)
+        if self.dw_rows:
+            rptr = self._buf("tb_rowptr", self.Np + 1, torch.int32)
+            rent = self._buf("tb_rowent", 2 * self.gt["E"], torch.int32)
+            a.row_ptr, a.row_ent = ptr(rptr), ptr(rent)
+            out.update(sp_rowptr=rptr, sp_rowent=rent)
         if self._rtag_live:
             a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
             a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
         call("ocf_sparse_tiles", a, cur_stream())
-        return dict(sp_bptr=bptr, sp_ent=ent)
+        return out
 
     def load_dense(self, inputs, out_mask, targets):
         """API path: dense arrays (torch/numpy) in the model.py input order."""

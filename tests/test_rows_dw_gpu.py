@@ -1,0 +1,159 @@
+"""Row-list weight-gradient kernel (ocf_rows_dw.h, OcfGemmArgs sp_rowptr / sp_rowent): the row lists
+built by ocf_sparse_tiles against a NumPy restatement, the fused update against a plain PyTorch fp32
+reference (g = A^T B from the same entries, Keras' optimizer formulas), rows without entries skipped
+only where that is the identity (Adagrad, l2 = 0), the output-bias column sums and their update."""
+import numpy as np
+import pytest
+import torch
+
+from omnidirectional_collaborative_filtering_amd import _lib
+from omnidirectional_collaborative_filtering_amd.engine import cur_stream
+from tests.test_optim_ws_gpu import OPTS, _buckets, _sparse_batch
+
+
+def _row_lists(sp, M, K):
+    rptr = torch.full((M + 1,), -5, dtype=torch.int32, device="cuda")
+    cap = max(1, int(sp["sp_lboff"][-1].item()) + 4 * M)
+    rent = torch.full((cap, 2), -9, dtype=torch.int32, device="cuda")
+    bptr, ent = _buckets(sp, M, K, extra=dict(row_ptr=rptr, row_ent=rent))
+    return bptr, ent, rptr, rent
+
+
+def _dense_entries(sp, M):
+    """per column m: [(value index, k)] in k order (NumPy restatement of the row lists)"""
+    h = {k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in sp.items()}
+    cols = [[] for _ in range(M)]
+    for b in range(h["sp_krows"]):
+        r = h["sp_rows"][b]
+        if r < 0:
+            continue
+        for e in range(h["sp_rp"][r], h["sp_rp"][r + 1]):
+            cols[h["sp_col"][e]].append((h["sp_lboff"][b] + h["sp_lidx"][e], b))
+    return cols
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(256, 64, 40), (1280, 256, 256), (512, 320, 300), (640, 2048, 900)])
+def test_row_lists_match_numpy(gpu, shape):
+    M, K, krows = shape
+    sp, _ = _sparse_batch(M, K, krows, seed=K + 3)
+    _, _, rptr, rent = _row_lists(sp, M, K)
+    cols = _dense_entries(sp, M)
+    want_ptr = np.concatenate([[0], np.cumsum([len(c) for c in cols])])
+    got_ptr = rptr.cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(got_ptr - got_ptr[0], want_ptr)
+    ent = rent.cpu().numpy()
+    for m in range(M):
+        got = [tuple(x) for x in ent[got_ptr[m]:got_ptr[m + 1]]]
+        assert got == cols[m], m
+
+
+def _run_rows(cd, M, N, K, opt, Bm, state, sp, rows=True, colsum=False, jobs=None):
+    P, S1, S2 = (t.clone() for t in state)
+    sdt = {_lib.DT_F16: torch.float16, _lib.DT_BF16: torch.bfloat16}.get(cd)
+    Sh = P.to(sdt) if sdt is not None else None
+    cs = torch.full((M,), -7.0, device="cuda") if colsum else None
+    a = _lib.OcfGemmArgs()
+    a.compute_dtype = cd
+    a.A, a.a_dtype, a.a_col, a.lda = Bm.data_ptr(), cd, 1, M
+    a.B, a.b_dtype, a.b_col, a.ldb = Bm.data_ptr(), cd, 1, N
+    a.M, a.N, a.K, a.splits, a.epi = M, N, K, 1, _lib.EPI_OPTIM
+    a.p, a.ld_out, a.s1 = P.data_ptr(), N, S1.data_ptr()
+    a.s2 = S2.data_ptr() if opt.kind == _lib.OPT_ADAM else None
+    a.opt = opt
+    if Sh is not None:
+        a.p_shadow, a.shadow_blocked = Sh.data_ptr(), 0
+    if cs is not None:
+        a.sp_colsum = cs.data_ptr()
+    a.a_sparse = 1
+    for k, v in sp.items():
+        if not rows and k in ("sp_rowptr", "sp_rowent"):
+            continue
+        setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
+    for k, v in (jobs or {}).items():
+        setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
+    _lib.call("ocf_gemm", a, cur_stream())
+    torch.cuda.synchronize()
+    return P, S1, S2, Sh, cs
+
+
+def _torch_update(opt, g, p, s1, s2):
+    g = g.double()
+    p, s1, s2 = p.double(), s1.double(), s2.double()
+    if opt.l2:
+        g = g + 2.0 * opt.l2 * p
+    if opt.kind == _lib.OPT_ADAGRAD:
+        s1 = s1 + g * g
+        p = p - opt.lr * g / (s1.sqrt() + opt.eps)
+    elif opt.kind == _lib.OPT_RMSPROP:
+        s1 = opt.rho * s1 + (1 - opt.rho) * g * g
+        p = p - opt.lr * g / (s1.sqrt() + opt.eps)
+    else:
+        s1 = opt.rho * s1 + (1 - opt.rho) * g
+        s2 = opt.beta2 * s2 + (1 - opt.beta2) * g * g
+        p = p - opt.lr * s1 / (s2.sqrt() + opt.eps)
+    return p.float(), s1.float(), s2.float()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", [_lib.DT_F16, _lib.DT_BF16, _lib.DT_F32])
+@pytest.mark.parametrize("opt_name", ["adagrad", "rmsprop", "adam", "adagrad_l2"])
+@pytest.mark.parametrize("shape", [(1280, 512, 256, 256), (768, 256, 2048, 900), (384, 128, 64, 40)])
+def test_rows_kernel_vs_torch(gpu, cd, opt_name, shape):
+    M, N, K, krows = shape
+    sp, dense = _sparse_batch(M, K, krows, seed=M + K, col_frac=0.6)
+    bptr, ent, rptr, rent = _row_lists(sp, M, K)
+    spr = dict(sp, sp_bptr=bptr, sp_ent=ent, sp_rowptr=rptr, sp_rowent=rent)
+    g = torch.Generator().manual_seed(K)
+    td = {_lib.DT_F16: torch.float16, _lib.DT_BF16: torch.bfloat16, _lib.DT_F32: torch.float32}[cd]
+    Bm = torch.randn(K, N, generator=g).to(td).cuda()
+    state = ((torch.randn(M, N, generator=g) * 0.05).cuda(), torch.rand(M, N, generator=g).cuda(),
+             torch.rand(M, N, generator=g).cuda())
+    gscale = 3e-3
+    opt = OPTS[opt_name](gscale)
+    P, S1, S2, Sh, cs = _run_rows(cd, M, N, K, opt, Bm, state, spr, colsum=True)
+    # reference: the same entries (fp32 values, B as stored) in fp64
+    A = torch.from_numpy(dense).double().cuda()
+    grad = (A.t() @ Bm.double()) * gscale
+    rp, r1, r2 = _torch_update(opt, grad, *state)
+    torch.testing.assert_close(P, rp, rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(S1, r1, rtol=1e-5, atol=2e-6)
+    if opt.kind == _lib.OPT_ADAM:
+        torch.testing.assert_close(S2, r2, rtol=1e-5, atol=2e-6)
+    if Sh is not None:
+        assert torch.equal(Sh, P.to(Sh.dtype))        # shadow = the updated weights, rounded once
+    torch.testing.assert_close(cs.double(), A.sum(0) * gscale, rtol=1e-5, atol=1e-7)
+    empty = torch.from_numpy(~(dense != 0).any(0)).cuda()
+    if opt_name == "adagrad":                          # identity on rows without entries: untouched
+        assert torch.equal(P[empty], state[0][empty]) and torch.equal(S1[empty], state[1][empty])
+    elif opt_name == "rmsprop":                        # a decays even with g = 0: every row updated
+        assert not torch.equal(S1[empty], state[1][empty])
+
+
+@pytest.mark.gpu
+def test_rows_kernel_matches_mfma_kernels_and_bias_job(gpu):
+    """same update as the role-split MFMA kernel up to the operand rounding (f16 A values there), and
+    the folded output-bias update (cb_*) equals ocf_bias_opt_from_partials on the column sums"""
+    M, N, K, krows = 1280, 512, 256, 256
+    cd = _lib.DT_F16
+    sp, dense = _sparse_batch(M, K, krows, seed=11, col_frac=0.6)
+    bptr, ent, rptr, rent = _row_lists(sp, M, K)
+    spr = dict(sp, sp_bptr=bptr, sp_ent=ent, sp_rowptr=rptr, sp_rowent=rent)
+    g = torch.Generator().manual_seed(1)
+    Bm = torch.randn(K, N, generator=g).half().cuda()
+    state = ((torch.randn(M, N, generator=g) * 0.05).cuda(), torch.rand(M, N, generator=g).cuda(),
+             torch.rand(M, N, generator=g).cuda())
+    opt = OPTS["adagrad"](2e-3)
+    bias = torch.randn(M, generator=g).cuda()
+    bacc = torch.rand(M, generator=g).cuda()
+    b1, a1 = bias.clone(), bacc.clone()
+    rows = _run_rows(cd, M, N, K, opt, Bm, state, spr, colsum=True,
+                     jobs=dict(cb_p=b1, cb_s1=a1, cb_op=OPTS["adagrad"](1.0)))
+    ws = _run_rows(cd, M, N, K, opt, Bm, state, spr, rows=False, colsum=True)
+    torch.testing.assert_close(rows[0], ws[0], rtol=0, atol=2e-5)
+    b2, a2 = bias.clone(), bacc.clone()
+    o = OPTS["adagrad"](1.0)
+    _lib.call("ocf_bias_opt_from_partials", b2.data_ptr(), rows[4].data_ptr(), 1, M, M, a2.data_ptr(), None, None, o,
+              cur_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(b1, b2) and torch.equal(a1, a2)
