@@ -786,17 +786,31 @@ class Engine:
         L, Bp = len(self.H), self.Bp
         HpL = self.Hp[L - 1]
         fused = grads_out is None
+        delta = self._buf("delta_e", self.gt["E"]) if self.sparse_dw else None
+        xval = self.gt["xval"]
+        out_done = False
         if self.comm is not None:
-            with self.phase("allreduce_bwd"):
-                self.comm(self.dhpre)
+            start = getattr(self.comm, "start", None)
+            if start is not None:
+                # the output layer's update needs only the deltas and h, not the summed dh: it runs
+                # while the all-reduce of the dh partials is in flight on the collective's stream
+                work = start(self.dhpre)
+                with self.phase("dW_out"):
+                    self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
+                                               self.db_out_col)
+                self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+                out_done = True
+                with self.phase("allreduce_bwd"):
+                    work.wait()
+            else:
+                with self.phase("allreduce_bwd"):
+                    self.comm(self.dhpre)
             call("ocf_splitk_grad_act", ptr(self.dhpre), 1, Bp * HpL, Bp, HpL, HpL, ptr(self.a[L - 1]),
                  ptr(self.mask[L - 1]), self.keep, self.act, ptr(self.dh[L - 1]), self.cdt, ptr(self.db_h[L - 1][0]),
                  gscale, self.B, self.H[L - 1], s)
             db_last, parts_last = self.db_h[L - 1], Bp // 4
         else:
             db_last, parts_last = self.db_rows, Bp
-        delta = self._buf("delta_e", self.gt["E"]) if self.sparse_dw else None
-        xval = self.gt["xval"]
         if fused and self._folds():
             # dW_out also: output-bias gradient (column sums of the deltas) and its update, the
             # hidden-bias update from the decoder's row partials, the step's stats
@@ -833,9 +847,11 @@ class Engine:
                 self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
             self.opt.iterations += 1
             return
-        with self.phase("dW_out"):
-            self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op, self.db_out_col)
-        self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+        if not out_done:
+            with self.phase("dW_out"):
+                self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
+                                           self.db_out_col)
+            self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
         for i in range(L - 1, 0, -1):
             self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
                        self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,

@@ -100,4 +100,9 @@ def make_comm(world):
 
     def comm(t):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
+
+    def start(t):
+        """asynchronous form: returns the work handle; wait() orders the caller's stream after it"""
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+    comm.start = start
     return comm

@@ -43,7 +43,7 @@ STRUCTS = {
     "OcfOptParams": (_lib.OcfOptParams, ["kind", "lr", "gscale"]),
     "OcfScatterArgs": (_lib.OcfScatterArgs, ["keep1", "s0", "seed", "mode", "rows2", "aux", "ld", "xin_dtype",
                                              "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean",
-                                             "xval1", "tb_cnt", "tb_nk"]),
+                                             "xval1", "tb_cnt", "tb_nk", "rtag_in", "rtag_out", "rtag"]),
     "OcfGatherArgs": (_lib.OcfGatherArgs, ["rows", "n_chunks", "ldw", "w_blocked", "H", "part", "aux", "delta_e",
                                            "ld_d"]),
     "OcfRowsReduceArgs": (_lib.OcfRowsReduceArgs, ["mode", "out", "keep", "seed", "stream", "n_real", "gscale",
@@ -52,9 +52,11 @@ STRUCTS = {
                                        "ld_db", "n_real", "opt", "ld_pmask", "row_sse_part", "t_rows", "t_lboff", "t_ntiles",
                                        "t_aux", "p_shadow", "b_nt", "shadow_blocked", "a_sparse",
                                        "sp_lboff", "sp_krows", "sp_colsum", "sp_bptr", "sp_ent", "cb_op", "jb_part",
-                                       "jb_ld", "jb_op", "js_sp", "js_M"]),
+                                       "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
+                                       "sp_rowent"]),
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
-                                                       "cnt_clear"]),
+                                                       "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",
+                                                       "row_ptr", "row_ent"]),
 }
 
 
