@@ -414,6 +414,15 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   // about to be written to LDS); only for 16-bit operands, where two sets fit the register budget
   // of two workgroups per CU.
   constexpr bool DEEP = !SPA && Epi::DEEP_PIPE && sizeof(CT) == 2 && sizeof(AGT) == 2 && sizeof(BGT) == 2;
+  // output-column sums of a [K][M] A for the tile_n == 0 workgroups (the output-bias gradient), in
+  // fixed k order, from each K-step's A image once it is in LDS
+  const bool colsum = ACOL && sh.sp_colsum && tile_n == 0;
+  float csum = 0.f;
+  auto sum_a = [&](const char* img) {
+    if constexpr (ACOL) {
+      if (colsum && tid < GT_BM) csum += colsum_kstep<CT, BK>(img, Img<CT, GT_BM, true>::STRIDE, tid);
+    }
+  };
   if constexpr (DEEP) {
     Stager<AGT, CT, GT_BM, ACOL> sa0, sa1;
     Stager<BGT, CT, GT_BN, BCOL> sb0, sb1;
@@ -437,6 +446,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
       if (nk > 1) ld1(1);
       st0(buf0);
       __syncthreads();
+      sum_a(buf0);
       int kt = 0;
       // steady state: buf0 holds step kt, set 1 carries step kt+1
       for (; kt + 3 < nk; kt += 2) {
@@ -444,10 +454,12 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
         compute(buf0);
         st1(buf1);
         __syncthreads();
+        sum_a(buf1);
         ld1(kt + 3);
         compute(buf1);
         st0(buf0);
         __syncthreads();
+        sum_a(buf0);
       }
       const int rem = nk - kt;   // 1, 2 or 3 steps left
       if (rem == 3) {
@@ -455,14 +467,17 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
         compute(buf0);
         st1(buf1);
         __syncthreads();
+        sum_a(buf1);
         compute(buf1);
         st0(buf0);
         __syncthreads();
+        sum_a(buf0);
         compute(buf0);
       } else if (rem == 2) {
         compute(buf0);
         st1(buf1);
         __syncthreads();
+        sum_a(buf1);
         compute(buf1);
       } else {
         compute(buf0);
@@ -473,21 +488,11 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
     Stager<AGT, CT, GT_BM, ACOL> sa;
     Stager<BGT, CT, GT_BN, BCOL> sb;
     const uint32_t sta = decltype(sa)::step_bytes(sh.lda, false), stb = decltype(sb)::step_bytes(sh.ldb, bblk);
-    // sparse A: output-column sums of A for the tile_n == 0 workgroups (bias gradient)
-    const bool colsum = ACOL && sh.sp_colsum && tile_n == 0;
-    float csum = 0.f;
     auto fill_a = [&](char* img, int kt) {   // SPA: zero + scatter the A image of K-step kt
       if constexpr (SPA) {
         sparse_a_zero<CT, GT_BM, BK>(img, tid);
         __syncthreads();
         sparse_a_fill<CT, GT_BM, BK>(sh, img, k_begin + kt * BK, m0, tid);
-      }
-    };
-    auto sum_a = [&](const char* img) {      // column sums of the A image (fixed k order), [K][M] A only
-      if constexpr (ACOL) {
-        if (colsum && tid < GT_BM) {
-          csum += colsum_kstep<CT, BK>(img, Img<CT, GT_BM, true>::STRIDE, tid);
-        }
       }
     };
     if (nk > 0) {
@@ -518,8 +523,8 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
       __syncthreads();
       if (more) sum_a(((kt + 1) & 1) ? buf1 : buf0);
     }
-    if (colsum && tid < GT_BM) sh.sp_colsum[m0 + tid] = csum * sh.colsum_scale;
   }
+  if (colsum && tid < GT_BM) sh.sp_colsum[m0 + tid] = csum * sh.colsum_scale;
 
   TileCtx c;
   c.m0 = m0; c.n0 = n0; c.wm = wm; c.wn = wn; c.lane = lane; c.tid = tid;

@@ -24,7 +24,10 @@
 
 namespace ocf {
 
-constexpr int RG_THREADS = 256;
+#ifndef OCF_RG_THREADS
+#define OCF_RG_THREADS 256
+#endif
+constexpr int RG_THREADS = OCF_RG_THREADS;   // threads per row-gather workgroup (one chunk of <= 256 entries)
 constexpr int RG_MAX_H = 512;
 #ifndef OCF_RG_U
 #define OCF_RG_U 4
