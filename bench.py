@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="diagnostic: run rank 0 of a G-way feature-parallel job alone (collectives skipped, "
                          "numerics of a partial model); not a bench line")
+    ap.add_argument("--emulate-comm", type=int, default=1,
+                    help="with --emulate-shards: run the rank's collective code path with no-op collectives")
     ap.add_argument("--sparse-clear", type=int, default=0,
                     help="clear the previous batch's layer-0 entries instead of a dense memset")
     ap.add_argument("--sparse-dw", type=int, default=-1,
@@ -71,6 +73,8 @@ def parse():
                     help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
     ap.add_argument("--dw-rows", type=int, default=-1,
                     help="weight gradients row by row from the entries (1) or by the MFMA role-split kernel (0)")
+    ap.add_argument("--split-dw", type=int, default=1,
+                    help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -78,6 +82,21 @@ def parse():
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient all-reduce)")
     return ap.parse_args()
+
+
+class _NoComm:
+    """--emulate-shards with --emulate-comm: the feature-parallel rank step with its collectives replaced by
+    no-ops (same kernels, streams and ordering as a real rank; the all-reduce time itself is missing)"""
+
+    class _Work:
+        def wait(self):
+            pass
+
+    def __call__(self, t):
+        pass
+
+    def start(self, t):
+        return self._Work()
 
 
 def optim(name, lr):
@@ -138,7 +157,7 @@ def main():
         G = args.emulate_shards
         c0, c1 = feature_shard_range(N, 0, G)
         data = data_full.column_shard(c0, c1)
-        Bg, shard, comm = B * G, (c0, c1, N), None
+        Bg, shard, comm = B * G, (c0, c1, N), _NoComm() if args.emulate_comm else None
         fp = True
     elif fp:
         # weak scaling: 256 rows per GPU -> global batch 256*G, each rank owns N/G users
@@ -164,6 +183,7 @@ def main():
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
+    eng.split_dw_streams = bool(args.split_dw)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):

@@ -246,6 +246,8 @@ class Engine:
         self.dw_rows = False
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
+        # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
+        self.split_dw_streams = True
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
         # role-split dW kernels skip the parameter / slot / shadow traffic of the untagged rows, whose
@@ -795,10 +797,20 @@ class Engine:
                 # the output layer's update needs only the deltas and h, not the summed dh: it runs
                 # while the all-reduce of the dh partials is in flight on the collective's stream
                 work = start(self.dhpre)
-                with self.phase("dW_out"):
-                    self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
-                                               self.db_out_col)
-                self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+                if self.side is not None and self.split_dw_streams:
+                    # ... on the side stream, so the input layer's update (main stream, after the
+                    # all-reduce) fills the CUs the output layer's last tiles leave idle
+                    self._fork()
+                    with torch.cuda.stream(self.side):
+                        with self.phase("dW_out"):
+                            self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
+                                                       self.db_out_col)
+                        self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+                else:
+                    with self.phase("dW_out"):
+                        self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
+                                                   self.db_out_col)
+                    self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
                 out_done = True
                 with self.phase("allreduce_bwd"):
                     work.wait()
