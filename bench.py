@@ -75,6 +75,8 @@ def parse():
                     help="weight gradients row by row from the entries (1) or by the MFMA role-split kernel (0)")
     ap.add_argument("--split-dw", type=int, default=1,
                     help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
+    ap.add_argument("--split-dw-1gpu", type=int, default=0,
+                    help="single GPU: the two persistent dW kernels on two streams")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -184,6 +186,7 @@ def main():
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
     eng.split_dw_streams = bool(args.split_dw)
+    eng.split_dw_streams_1gpu = bool(args.split_dw_1gpu)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):

@@ -248,6 +248,7 @@ class Engine:
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
         self.split_dw_streams = True
+        self.split_dw_streams_1gpu = False   # the same for the single-GPU persistent dW kernels (A/B switch)
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
         # role-split dW kernels skip the parameter / slot / shadow traffic of the untagged rows, whose
@@ -838,9 +839,18 @@ class Engine:
                 sp, n_sp, rs, n_rs, M, dst = self._stats_pending
                 jobs.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
                 self._stats_pending = None
-            with self.phase("dW_out"):
-                self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
-                                           jobs=jobs)
+            if self.side is not None and self.split_dw_streams_1gpu:
+                # the two persistent dW kernels on two streams: the second one's workgroups take the CUs
+                # the first one's last tiles leave idle
+                self._fork()
+                with torch.cuda.stream(self.side):
+                    with self.phase("dW_out"):
+                        self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op,
+                                                   self.db_out_col, jobs=jobs)
+            else:
+                with self.phase("dW_out"):
+                    self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
+                                               jobs=jobs)
             with self.phase("dW_in"):
                 self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
             self.opt.iterations += 1
