@@ -77,6 +77,9 @@ def parse():
                     help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
     ap.add_argument("--split-dw-1gpu", type=int, default=0,
                     help="single GPU: the two persistent dW kernels on two streams")
+    ap.add_argument("--fuse-enc", type=int, default=1,
+                    help="single GPU, one hidden layer: the decoder gather applies the hidden layer's bias / "
+                         "activation / dropout to the encoder partials itself (0: separate row-reduce launch)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -187,6 +190,7 @@ def main():
     eng.fold_jobs = bool(args.fold_jobs)
     eng.split_dw_streams = bool(args.split_dw)
     eng.split_dw_streams_1gpu = bool(args.split_dw_1gpu)
+    eng.fuse_enc_epilogue = bool(args.fuse_enc)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):

@@ -140,6 +140,12 @@ typedef struct OcfGatherArgs {
   float* delta_e;            /* per batch-local entry delta err*m (nullable)                      */
   float* chunk_stats;        /* [n_chunks][4]: SSE, SAE, count_nonzero(T + yhat), 0               */
   void* d_out; int d_dtype; int64_t ld_d;     /* optional dense delta (zero elsewhere)            */
+  /* decoder, optional (enc_part != NULL, one hidden layer): the hidden layer's bias / activation /
+   * dropout applied here instead of by ocf_rows_reduce(OCF_REDUCE_BIAS_ACT) -- h[b] = dropout(act(the
+   * encoder chunk partials enc_part[enc_cptr[b] .. enc_cptr[b+1]) summed in order + bias_h)), the same
+   * arithmetic; the first chunk of each batch row also stores a_out, mask_out and h (h is then written) */
+  const float* enc_part; const int32_t* enc_cptr; const float* bias_h; int act; float keep;
+  uint64_t seed, stream; float* a_out; uint8_t* mask_out; int m_real, n_real;
 } OcfGatherArgs;
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);

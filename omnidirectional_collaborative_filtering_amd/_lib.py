@@ -53,6 +53,8 @@ class OcfGatherArgs(ctypes.Structure):
         ("W", P), ("w_dtype", I32), ("ldw", I64), ("w_blocked", I32), ("H", I32), ("part", P),
         ("h", P), ("h_dtype", I32), ("bias", P), ("aux", F32), ("delta_e", P), ("chunk_stats", P),
         ("d_out", P), ("d_dtype", I32), ("ld_d", I64),
+        ("enc_part", P), ("enc_cptr", P), ("bias_h", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64),
+        ("a_out", P), ("mask_out", P), ("m_real", I32), ("n_real", I32),
     ]
 
 

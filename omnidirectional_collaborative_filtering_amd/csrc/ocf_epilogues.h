@@ -106,7 +106,8 @@ struct BiasActParams {
   int m_real, n_real;
 };
 
-__device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, int n, float v) {
+// a = act(v + bias), h = dropout(a); stores a / mask / h where the pointers are set; returns h
+__device__ __forceinline__ float bias_act_value(const BiasActParams& p, int m, int n, float v) {
   int64_t idx = (int64_t)m * p.ld + n;
   bool live = m < p.m_real && n < p.n_real;
   float a = live ? act_apply(p.act, v + p.bias[n]) : 0.f;
@@ -124,6 +125,10 @@ __device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, in
     else if (p.h_dtype == OCF_F16) reinterpret_cast<_Float16*>(p.h_out)[idx] = (_Float16)h;
     else reinterpret_cast<__bf16*>(p.h_out)[idx] = (__bf16)h;
   }
+  return h;
+}
+__device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, int n, float v) {
+  (void)bias_act_value(p, m, n, v);
 }
 
 struct EpiBiasAct {

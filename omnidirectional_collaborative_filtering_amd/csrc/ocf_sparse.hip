@@ -186,12 +186,36 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
   float hv[V];
+  if (a.enc_part) {
+    // the hidden layer's epilogue from the encoder partials (rows_reduce_kernel BIAS_ACT arithmetic); the
+    // row's first chunk stores a / h / mask for the backward pass
+    // once per workgroup, coalesced over the row, staged through LDS for the groups
+    BiasActParams p;
+    const bool first = j0 == 0;
+    p.bias = a.bias_h; p.act = a.act; p.keep = a.keep; p.seed = a.seed; p.stream = a.stream; p.mask_in = nullptr;
+    p.mask_out = first ? a.mask_out : nullptr; p.a_out = first ? a.a_out : nullptr;
+    p.h_out = first ? const_cast<void*>(a.h) : nullptr; p.h_dtype = a.h_dtype; p.ld = a.H;
+    p.m_real = a.m_real; p.n_real = a.n_real;
+    const int e0 = a.enc_cptr[b], e1 = a.enc_cptr[b + 1];
+    for (int x = threadIdx.x; x < a.H; x += RG_THREADS) {
+      float v = 0.f;
+      for (int c = e0; c < e1; ++c) v += a.enc_part[(int64_t)c * a.H + x];
+      red[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, v));
+    }
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < PPL; ++i) {
-    float t[E];
-    load_act_piece<HT, E>(a.h, a.H, b, l + G * i, t);
+    for (int i = 0; i < PPL; ++i)
 #pragma unroll
-    for (int k = 0; k < E; ++k) hv[i * E + k] = t[k];
+      for (int k = 0; k < E; ++k) hv[i * E + k] = red[(l + G * i) * E + k];
+    __syncthreads();   // red is reused by the group reduction at the end
+  } else {
+#pragma unroll
+    for (int i = 0; i < PPL; ++i) {
+      float t[E];
+      load_act_piece<HT, E>(a.h, a.H, b, l + G * i, t);
+#pragma unroll
+      for (int k = 0; k < E; ++k) hv[i * E + k] = t[k];
+    }
   }
   float acc[V];
 #pragma unroll
@@ -410,6 +434,8 @@ extern "C" int ocf_gather_decoder(const OcfGatherArgs* args, void* stream) {
   check_gather(a, "ocf_gather_decoder");
   OCF_CHECK(a.flag && a.val && a.h && a.bias && a.chunk_stats, "ocf_gather_decoder: flag/val/h/bias/chunk_stats required");
   OCF_CHECK(a.h_dtype == a.w_dtype, "ocf_gather_decoder: h and W must share the compute dtype");
+  OCF_CHECK(!a.enc_part || (a.enc_cptr && a.bias_h && (a.keep >= 1.f || a.mask_out) && a.a_out),
+            "ocf_gather_decoder: enc_part needs enc_cptr, bias_h, a_out and (with dropout) mask_out");
   if (a.n_chunks == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   int G, ppl;

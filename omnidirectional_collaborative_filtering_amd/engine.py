@@ -249,6 +249,10 @@ class Engine:
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
         self.split_dw_streams = True
         self.split_dw_streams_1gpu = False   # the same for the single-GPU persistent dW kernels (A/B switch)
+        # one hidden layer, one GPU: the decoder gather applies the hidden layer's epilogue to the encoder's
+        # chunk partials (no separate row-reduce launch between the two gathers)
+        self.fuse_enc_epilogue = True
+        self._enc_fused = None
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
         # role-split dW kernels skip the parameter / slot / shadow traffic of the untagged rows, whose
@@ -414,6 +418,8 @@ class Engine:
         seg["t_flag"] = self.tflag
         self.tseg = seg
         self.gt = None
+        self._enc_fused = None
+        self._enc_fused = None
         a.tb_cnt, a.tb_nk = None, 0
         a.rtag_in = a.rtag_out = None
         self._rtag_live = False
@@ -495,6 +501,8 @@ class Engine:
         self._grow_buckets(B * N)
         self.tb = None
         self.tseg = None
+        self.gt = None                 # dense batch: the GEMM path, never a previous batch's gather tables
+        self._enc_fused = None
         call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
              ptr(self.bk_ptr), ptr(self.bk_cur), ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m), s)
 
@@ -589,6 +597,10 @@ class Engine:
             g = self._gather_args(tab, 0, part, Hp0)
             g.xval = ptr(self.gt["xval"])
             call("ocf_gather_encoder", g, cur_stream())
+            if self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue:
+                # the decoder gather applies bias / activation / dropout to these partials itself
+                self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id)
+                return
             if self.comm is not None:            # partial over this rank's columns -> all-reduce
                 r = self._reduce_args(tab, part, Hp0, _lib.REDUCE_RAW)
                 r.out = ptr(self.hpre)
@@ -611,6 +623,12 @@ class Engine:
         g.flag = ptr(self.tflag)
         g.h, g.h_dtype, g.bias, g.aux = ptr(self.h[L - 1]), self.cdt, ptr(self.b[L]), self.gt["aux"]
         g.chunk_stats = ptr(cst)
+        ef, self._enc_fused = self._enc_fused, None
+        if ef is not None:
+            g.enc_part, g.enc_cptr, g.keep, g.stream = ef["enc_part"], ef["enc_cptr"], ef["keep"], ef["stream"]
+            g.bias_h, g.act, g.seed = ptr(self.b[0]), self.act, self.seed
+            g.a_out, g.mask_out = ptr(self.a[0]), ptr(self.mask[0]) if ef["keep"] < 1 else None
+            g.m_real, g.n_real = self.B, self.H[0]
         if with_grad and self.sparse_dw:
             g.delta_e = ptr(self._buf("delta_e", self.gt["E"]))
         elif with_grad:               # dense delta for the output-layer weight-gradient GEMM

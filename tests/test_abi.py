@@ -45,7 +45,8 @@ STRUCTS = {
                                              "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean",
                                              "xval1", "tb_cnt", "tb_nk", "rtag_in", "rtag_out", "rtag"]),
     "OcfGatherArgs": (_lib.OcfGatherArgs, ["rows", "n_chunks", "ldw", "w_blocked", "H", "part", "aux", "delta_e",
-                                           "ld_d"]),
+                                           "ld_d", "enc_part", "enc_cptr", "bias_h", "act", "keep", "seed",
+                                           "stream", "a_out", "mask_out", "m_real", "n_real"]),
     "OcfRowsReduceArgs": (_lib.OcfRowsReduceArgs, ["mode", "out", "keep", "seed", "stream", "n_real", "gscale",
                                                    "row_sse"]),
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",

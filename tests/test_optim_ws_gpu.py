@@ -403,3 +403,40 @@ def test_engine_row_skip_bit_identical(gpu, cd):
         del om_
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+def test_engine_fused_encoder_epilogue_bit_identical(gpu, cd):
+    """The hidden layer's bias / sigmoid / dropout applied inside the decoder gather (Engine.fuse_enc_epilogue)
+    against the separate row-reduce launch: identical losses, weights, slots, shadows and test SSE."""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B = 900, 4000, 60000, 128
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=8)
+    data = split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(8))
+    out = []
+    for fuse in (False, True):
+        np.random.seed(6)
+        rd = data_reader(cols, rows, dataset=data, eval_mode="fixed_split")
+        om = om_ = omni_model(1, 200, cols, B, dense_activation="sigmoid", use_causal_info=False,
+                              dropout_probability=0.2, compute_dtype=cd, seed=4)
+        eng = om.engine
+        eng.fuse_enc_epilogue = fuse
+        m = om.model
+        m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+        loss = m.fit_generator(gen, 5, epochs=1, verbose=0).history["loss"][0]
+        np.random.seed(9)
+        tg = rd.data_gen(B, None, "test", True, None, -1, return_target_count=True)
+        sse, cnt = m.evaluate_sse(tg, rd.test_set_size // B)
+        torch.cuda.synchronize()
+        out.append(([loss, sse, cnt], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                    [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                    [t.clone() for t in eng.Wsh if t is not None]))
+        del om_
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
