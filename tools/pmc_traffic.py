@@ -6,7 +6,7 @@ Correction (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE reports half
 coalesced streaming read, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-B streaming
 stores.  Both counters are in KiB.  Kernels that run twice per step share a symbol, so phases are
 assigned by launch order within the step: SLAB GEMMs alternate enc_gemm / dec_bwd_gemm (dense path),
-row reductions alternate enc_reduce / dec_reduce (row-gather path), OPTIM GEMMs alternate
+row reductions belong to the gather launched before them (row-gather path), OPTIM GEMMs alternate
 dW_out / dW_in.  Row-gather path: gather_encoder -> enc_gemm, gather_decoder -> dec_gemm_mse (the
 phase names the engine's timers use).  Values are mean bytes per launch over the profiled steps
 (warm-up launches included; they move the same bytes)."""
@@ -28,12 +28,13 @@ def per_dispatch(path, counter):
 
 def phase_of(name, seen):
     if "gather_encoder" in name:
+        seen["gather"] = "enc"
         return "enc_gemm"
     if "gather_decoder" in name:
+        seen["gather"] = "dec"
         return "dec_gemm_mse"
-    if "rows_reduce" in name:
-        k = seen["red"] = seen.get("red", -1) + 1
-        return ("enc_reduce", "dec_reduce")[k % 2]
+    if "rows_reduce" in name:             # belongs to the gather it follows (the decoder gather may
+        return seen.get("gather", "enc") + "_reduce"   # apply the encoder's epilogue itself)
     if "EpiMaskedMSE" in name:
         return "dec_gemm_mse"
     if "EpiSlab" in name:
