@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--fuse-enc", type=int, default=1,
                     help="single GPU, one hidden layer: the decoder gather applies the hidden layer's bias / "
                          "activation / dropout to the encoder partials itself (0: separate row-reduce launch)")
+    ap.add_argument("--async-tb", type=int, default=0,
+                    help="per-batch tile buckets on the side stream, overlapping the row gathers (0: main stream)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -191,6 +193,7 @@ def main():
     eng.split_dw_streams = bool(args.split_dw)
     eng.split_dw_streams_1gpu = bool(args.split_dw_1gpu)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
+    eng.async_tile_buckets = bool(args.async_tb)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
