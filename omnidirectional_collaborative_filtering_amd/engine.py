@@ -256,6 +256,7 @@ class Engine:
         # measured neutral (ML-20M step 0.5052 vs 0.5056 ms, 4 interleaved runs; the fork/join events
         # cost what the overlap saves), so off
         self.async_tile_buckets = False
+        self._tb_forked = False
         self._enc_fused = None
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
@@ -452,6 +453,7 @@ class Engine:
             if a.tb_cnt and self.side is not None and self.async_tile_buckets:
                 # only the weight-gradient kernels read the buckets: build them beside the gathers
                 self._fork()
+                self._tb_forked = True
                 with torch.cuda.stream(self.side):
                     self.tb = self._tile_buckets()
             else:
@@ -814,7 +816,9 @@ class Engine:
         """backward after the row-gather decoder: the last hidden delta already exists (single GPU) or
         its partial sum does (feature parallel: all-reduce, then activation/dropout)"""
         s = cur_stream()
-        self._join()                  # the tile buckets, when built on the side stream
+        if self._tb_forked:           # the tile buckets were built on the side stream
+            self._join()
+            self._tb_forked = False
         L, Bp = len(self.H), self.Bp
         HpL = self.Hp[L - 1]
         fused = grads_out is None
