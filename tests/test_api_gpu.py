@@ -133,3 +133,31 @@ def test_denoising_transfer_freezes_outer_layers(gpu):
     np.testing.assert_allclose(w1[3], new_b, rtol=1e-5, atol=1e-6)
     om.make_trainable()
     assert om.engine.trainable == [True, True, False]
+
+
+@pytest.mark.gpu
+def test_predict_after_generator_training(gpu):
+    """predict() on dense arrays after row-gather training steps runs the dense GEMM path on the
+    arrays it was given (no stale gather tables of the last generator batch): equal to the oracle
+    forward with the trained weights."""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    from omnidirectional_collaborative_filtering_amd.optimizers import Adagrad
+    data = _data()
+    N = data.num_cols
+    np.random.seed(4)
+    rd = data_reader(N, 600, dataset=data, eval_mode="fixed_split")
+    om = omni_model(1, 32, N, 128, "sigmoid", use_causal_info=False, dropout_probability=0.2,
+                    compute_dtype="float32", seed=6)
+    m = om.model
+    m.compile(Adagrad(lr=0.01), "mean_squared_error")
+    gen = rd.data_gen(128, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    m.fit_generator(gen, 2, verbose=0)
+    assert om.engine.gt is not None              # the last step took the row-gather path
+    rng = np.random.RandomState(1)
+    x = rng.rand(128, N) * (rng.rand(128, N) < 0.1)
+    mask = -1.0 * (rng.rand(128, N) < 0.2)
+    y = m.predict([x, mask]).cpu().numpy()
+    w = m.get_weights()
+    ref, _ = OmniOracle([N, 32, N], activation="sigmoid").set_params(w[0::2], w[1::2]).forward(x, mask)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5)
