@@ -47,12 +47,15 @@ __device__ __forceinline__ void store_val(void* base, int dtype, int64_t idx, fl
   else reinterpret_cast<__bf16*>(base)[idx] = (__bf16)v;
 }
 
-// Flattened launch: one thread per batch entry held by this CSR, 256 entries per workgroup, so the
+// Flattened launch: one thread per batch entry held by this CSR, SC_THREADS entries per workgroup, so the
 // load balances whatever the row lengths (full rows on one GPU, ~1/G of them per column shard).
 // Blocks [0, nblk1) take source-1 entries, the rest source-2 entries.  A thread finds its batch row
 // by binary search over the batch offsets staged in LDS.  The outputs were zeroed by
 // hipMemsetAsync on the same stream before this launch.
-constexpr int SC_THREADS = 256;
+#ifndef OCF_SC_THREADS
+#define OCF_SC_THREADS 1024   // ML-20M step, interleaved A/B: 1024 0.5042, 512 0.5078, 256 0.5073 ms
+#endif
+constexpr int SC_THREADS = OCF_SC_THREADS;
 
 __device__ __forceinline__ int find_row(const int64_t* off, int B, int64_t e) {
   int lo = 0, hi = B;   // off[lo] <= e < off[hi]; empty rows are skipped because off[b] == off[b+1]
