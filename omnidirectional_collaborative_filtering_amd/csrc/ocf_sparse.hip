@@ -375,6 +375,7 @@ void by_shape(int G, int ppl, const OcfGatherArgs& a, hipStream_t s) {
   else if (G == 32 && ppl == 1) L<32, 1>::go(a, s);
   else if (G == 32 && ppl == 2) L<32, 2>::go(a, s);
   else if (G == 16 && ppl == 4) L<16, 4>::go(a, s);
+  else if (G == 32 && ppl == 4) L<32, 4>::go(a, s);   // fp32 weights, H = 512 (exact-fp32 mode at 500 units)
   else if (G == 32 && ppl == 3) L<32, 3>::go(a, s);
   else if (G == 16 && ppl == 1) L<16, 1>::go(a, s);
   else if (G == 16 && ppl == 3) L<16, 3>::go(a, s);

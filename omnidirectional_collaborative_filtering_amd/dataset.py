@@ -26,6 +26,28 @@ from typing import List, Optional
 import numpy as np
 
 
+def stable_order(major, minor=None):
+    """argsort(major * K + minor, kind='stable') for non-negative integer keys, as LSD radix passes
+    over 16-bit digits (NumPy's stable sort is a radix sort for 16-bit keys only): O(n) per pass
+    instead of an O(n log n) 64-bit merge sort -- the Netflix-sized CSRs (80 M entries) are built in
+    seconds, not minutes."""
+    keys = [k for k in (minor, major) if k is not None]
+    order = None
+    for k in keys:
+        k = np.asarray(k)
+        hi = int(k.max()) if len(k) else 0
+        shift = 0
+        while True:
+            digit = ((k >> shift) & 0xFFFF).astype(np.uint16)
+            d = digit if order is None else digit[order]
+            o = np.argsort(d, kind="stable")
+            order = o if order is None else order[o]
+            shift += 16
+            if hi >> shift == 0:
+                break
+    return order
+
+
 def dup_chain(row_ptr: np.ndarray, col: np.ndarray) -> Optional[np.ndarray]:
     """next[e] = next entry (CSR index) in the same row with the same column, else -1.
     Returns None when the matrix has no duplicate (row, col) pairs."""
@@ -34,7 +56,7 @@ def dup_chain(row_ptr: np.ndarray, col: np.ndarray) -> Optional[np.ndarray]:
         return None
     rows = np.repeat(np.arange(len(row_ptr) - 1, dtype=np.int64), np.diff(row_ptr))
     key = rows * (int(col.max()) + 1) + col.astype(np.int64)
-    order = np.argsort(key, kind="stable")
+    order = stable_order(rows, col.astype(np.int64))
     ks = key[order]
     same = ks[1:] == ks[:-1]
     if not same.any():
@@ -80,8 +102,7 @@ class RatingsCSR:
         n_tiles = -(-int(n_cols) // tile)
         lens = self.row_lengths()
         rows = np.repeat(np.arange(self.n_rows, dtype=np.int64), lens)
-        key = rows * (int(n_cols) + 1) + self.col.astype(np.int64)
-        order = np.argsort(key, kind="stable")
+        order = stable_order(rows, self.col.astype(np.int64))
         col_s = self.col[order]
         val_s = self.val[order]
         lidx_s = (order - self.row_ptr[rows[order]]).astype(np.int32)
@@ -102,7 +123,7 @@ class RatingsCSR:
         rp = np.zeros(self.n_rows + 1, dtype=np.int64)
         np.cumsum(counts, out=rp[1:])
         c = RatingsCSR(rp, (self.col[keep] - c0).astype(np.int32), self.val[keep], list(self.keys))
-        c.dup = dup_chain(rp, c.col)
+        c.dup = None if self.dup is None else dup_chain(rp, c.col)     # a subset of a dup-free CSR has none
         c.pos = pos[keep].astype(np.int32)
         c.full_lens = self.rng_lengths()
         return c
@@ -128,16 +149,17 @@ class RatingsCSR:
         return c
 
     @classmethod
-    def from_coo(cls, rows, cols, vals, n_rows, keys=None):
-        """rows need not be sorted; within a row the given order is kept (stable)."""
+    def from_coo(cls, rows, cols, vals, n_rows, keys=None, dup_free=False):
+        """rows need not be sorted; within a row the given order is kept (stable).  dup_free: the
+        caller guarantees unique (row, col) pairs (no duplicate chain to build)."""
         rows = np.asarray(rows, dtype=np.int64)
-        order = np.argsort(rows, kind="stable")
+        order = stable_order(rows)
         counts = np.bincount(rows, minlength=n_rows)
         rp = np.zeros(n_rows + 1, dtype=np.int64)
         np.cumsum(counts, out=rp[1:])
         c = cls(rp, np.asarray(cols, dtype=np.int32)[order], np.asarray(vals, dtype=np.float32)[order],
                 list(range(n_rows)) if keys is None else list(keys))
-        c.dup = dup_chain(rp, c.col)
+        c.dup = None if dup_free else dup_chain(rp, c.col)
         return c
 
     def subset_rows(self, idx):
@@ -150,7 +172,7 @@ class RatingsCSR:
             if len(idx) else np.zeros(0, np.int64)
         c = RatingsCSR(rp, self.col[take] if len(take) else np.zeros(0, np.int32),
                        self.val[take] if len(take) else np.zeros(0, np.float32), [])
-        c.dup = dup_chain(rp, c.col)
+        c.dup = None if self.dup is None else dup_chain(rp, c.col)     # a subset of a dup-free CSR has none
         return c
 
 
@@ -228,11 +250,12 @@ def load_reference_json(filepath, reverse_user_item_data=True, use_json=True):
     )
 
 
-def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=None):
+def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=None, dup_free=False):
     """Rating-level permutation split of TrainValidTestSplit.py:74-103.
 
     valid inputs = the row's train ratings (:101, map_inputs_to_targets :183-195),
     test inputs = the row's train+valid ratings (:83, :103); rows keyed by their index.
+    dup_free: the (row, col) pairs are unique (synthetic_ratings), so no split has duplicates.
     """
     rng = np.random if rng is None else rng
     n = len(rows)
@@ -244,7 +267,7 @@ def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=N
     vals = np.asarray(vals, np.float32)
 
     def csr_of(idx):
-        return RatingsCSR.from_coo(rows[idx], cols[idx], vals[idx], n_rows)
+        return RatingsCSR.from_coo(rows[idx], cols[idx], vals[idx], n_rows, dup_free=dup_free)
 
     full_tr = csr_of(tr)
     full_va = csr_of(va)
@@ -301,4 +324,4 @@ def synthetic_fixed_split(name_or_shape, seed=0, scale_rows=None):
         shp["nnz"] = int(shp["nnz"] * scale_rows / shp["rows"])
         shp["rows"] = scale_rows
     r, c, v = synthetic_ratings(shp["rows"], shp["cols"], shp["nnz"], shp.get("half_stars", False), seed)
-    return split_ratings(r, c, v, shp["rows"], shp["cols"], rng=np.random.RandomState(seed))
+    return split_ratings(r, c, v, shp["rows"], shp["cols"], rng=np.random.RandomState(seed), dup_free=True)

@@ -125,6 +125,104 @@ class OmniOracle:
             gW = [gw + 2.0 * self.l2 * w for gw, w in zip(gW, self.W)]
         return loss, y, gW, gb
 
+    # ---- rounding-error envelope of the gradient (parity tolerances for 16-bit MFMA operands) ----
+    def grad_magnitudes(self, x_in, out_mask, targets, drop_masks=None, u=2.0 ** -11):
+        """Per-element magnitude sums of the gradient computation, for a running-error bound: the same
+        backward pass as loss_and_grads with every product replaced by its absolute value, started
+        from |y - t| + u * (|h| |W_out| + |b_out|) (a 16-bit operand rounds y by ~u of that magnitude,
+        which the residual y - t does not shrink).  A kernel whose operands are rounded to unit
+        roundoff u (f16: 2^-11, bf16: 2^-8) computes gradient element g_i within ~c * u * G_i of the
+        exact one, c = the number of roundings along the chain.  Returns (GW, Gb) shaped like (gW, gb).
+        Adagrad parity tests scale their per-element tolerance by G_i / |g_i| (the update's
+        g / sqrt(sum g^2) is ill-conditioned exactly where that ratio is large)."""
+        dt = self.dtype
+        _, (hs, zs, y_full) = self.forward(x_in, out_mask, drop_masks)
+        T = np.asarray(targets, dt)
+        M = np.asarray(out_mask, dt)
+        Bn, N = T.shape
+        L = len(self.W) - 1
+        ymag = np.abs(hs[L]) @ np.abs(self.W[L]) + np.abs(self.b[L])
+        g = (2.0 / (Bn * N)) * (np.abs(M * y_full - T) + u * ymag) * np.abs(M)
+        GW = [None] * (L + 1)
+        Gb = [None] * (L + 1)
+        GW[L] = np.abs(hs[L]).T @ g
+        Gb[L] = g.sum(0)
+        d = g @ np.abs(self.W[L]).T
+        for i in range(L - 1, -1, -1):
+            a_pre = act_fwd(self.activation, zs[i])
+            if drop_masks is not None and drop_masks[i] is not None:
+                d = d * (np.asarray(drop_masks[i], dt) / dt(1.0 - self.dropout))
+            d = d * np.abs(act_grad_from_out(self.activation, a_pre, zs[i]))
+            GW[i] = np.abs(hs[i]).T @ d
+            Gb[i] = d.sum(0)
+            if i > 0:
+                d = d @ np.abs(self.W[i]).T
+        return GW, Gb
+
+    def forward_hidden_sparse(self, X):
+        """hidden activations (inference: no dropout) of one hidden layer for a scipy CSR input"""
+        return act_fwd(self.activation, np.asarray(X @ self.W[0]) + self.b[0])
+
+    # ---- the same equations on sparse batches (ML-20M / Netflix sizes) ---------------------------
+    def loss_and_grads_sparse(self, X, out_mask, T, drop_masks=None, u=None, chunk=1 << 17):
+        """loss_and_grads for one hidden layer with the batch held sparse: X, out_mask, T are scipy
+        CSR [B, N] (out_mask / T share one sparsity pattern: the rating entries; model.py:81-86 makes
+        y zero everywhere else, so the unobserved (0 - 0)^2 terms of Keras' MSE add nothing and their
+        gradient is exactly zero).  Mathematically identical to loss_and_grads on the densified
+        arrays (checked on CPU in tests/test_model_oracle.py); the dense [B, N] arrays never exist, so
+        ML-20M (N = 138,493) and Netflix (N = 480,189) batches fit.  With u, also returns the
+        grad_magnitudes envelope (GW, Gb).  Returns loss, (entry rows, cols, y), gW, gb[, GW, Gb]."""
+        import scipy.sparse as sp
+        assert len(self.W) == 2, "sparse restatement: one hidden layer"
+        dt = self.dtype
+        Bn, N = T.shape
+        M = out_mask.tocsr()
+        Tm = T.tocsr()
+        z = np.asarray(X @ self.W[0]) + self.b[0]
+        a = act_fwd(self.activation, z)
+        h = a
+        if drop_masks is not None and drop_masks[0] is not None:
+            h = a * (np.asarray(drop_masks[0], dt) / dt(1.0 - self.dropout))
+        coo = M.tocoo()
+        r, c, m = coo.row, coo.col, coo.data.astype(dt)
+        if not (np.array_equal(M.indptr, Tm.indptr) and np.array_equal(M.indices, Tm.indices)):
+            raise ValueError("out_mask and targets must share one sparsity pattern (the rating entries)")
+        t = Tm.data.astype(dt)
+        W1 = self.W[1]
+        yf = np.empty(len(r), dt)
+        ymag = np.empty(len(r), dt) if u is not None else None
+        for s in range(0, len(r), chunk):
+            rr, cc = r[s:s + chunk], c[s:s + chunk]
+            yf[s:s + chunk] = np.einsum("ij,ji->i", h[rr], W1[:, cc]) + self.b[1][cc]
+            if u is not None:
+                ymag[s:s + chunk] = np.einsum("ij,ji->i", np.abs(h[rr]), np.abs(W1[:, cc])) + np.abs(self.b[1][cc])
+        y = m * yf
+        e = y - t
+        loss = float(np.sum(e * e) / dt(Bn * N))
+        G = sp.csr_matrix(((2.0 / (Bn * N)) * e * m, (r, c)), shape=(Bn, N))
+        gW1 = np.asarray((G.T @ h).T)                  # (H, N) = h^T G
+        gb1 = np.asarray(G.sum(0)).ravel()
+        d = np.asarray(G @ W1.T)                       # [B, H]
+        if drop_masks is not None and drop_masks[0] is not None:
+            d = d * (np.asarray(drop_masks[0], dt) / dt(1.0 - self.dropout))
+        sg = act_grad_from_out(self.activation, a, z)
+        d = d * sg
+        gW0 = np.asarray(X.T @ d)
+        gb0 = d.sum(0)
+        out = [loss, (r, c, y), [gW0, gW1], [gb0, gb1]]
+        if u is not None:
+            Ga = sp.csr_matrix(((2.0 / (Bn * N)) * (np.abs(e) + u * ymag) * np.abs(m), (r, c)), shape=(Bn, N))
+            GW1 = np.asarray((Ga.T @ np.abs(h)).T)
+            Gb1 = np.asarray(Ga.sum(0)).ravel()
+            da = np.asarray(Ga @ np.abs(W1).T)
+            if drop_masks is not None and drop_masks[0] is not None:
+                da = da * (np.asarray(drop_masks[0], dt) / dt(1.0 - self.dropout))
+            da = da * np.abs(sg)
+            Xa = X.copy()
+            Xa.data = np.abs(Xa.data)
+            out += [[np.asarray(Xa.T @ da), GW1], [da.sum(0), Gb1]]
+        return tuple(out)
+
     def params(self):
         out = []
         for w, b in zip(self.W, self.b):

@@ -1,0 +1,220 @@
+"""Shared training-parity harness for the -m gpu tests: run the GPU engine through the reference's
+API (data_reader.data_gen -> omni_model -> compile -> fit_generator, train.py:131-158), replay the
+same batches through the NumPy fp64 oracle (oracle/model_oracle.py), and compare.
+
+Tolerances (stated here, used by every parity test):
+  * exact-fp32 mode (v_mfma_f32_32x32x2_f32): per-step loss within 1e-5 relative, masked test RMSE
+    within 1e-5, every weight and bias within FP32_ABS = 1e-5 (max-abs, no quantile);
+  * f16 / bf16 MFMA operands: loss and RMSE within 2e-3 / 1e-2 relative; every weight within a
+    per-element running-error envelope (adagrad_envelope): an Adagrad update is lr * g / sqrt(sum g^2),
+    which amplifies the operand rounding of g by G_i / |g_i| (G = the gradient's magnitude sum,
+    OmniOracle.grad_magnitudes).  Elements with a well-conditioned gradient must match tightly;
+    only elements whose gradient is within rounding distance of zero may differ by up to 2 lr per
+    step (the update's sign there is not determined by 16-bit operands).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle.batch_oracle import scatter_rows_numpy
+from oracle.model_oracle import AdagradOracle, AdamOracle, OmniOracle, RMSpropOracle
+
+FP32_ABS = 1e-5
+UNIT_ROUNDOFF = {"float16": 2.0 ** -11, "bfloat16": 2.0 ** -8, "float32": 2.0 ** -24}
+# roundings along the longest gradient chain of the 16-bit path: W shadow, h, delta, dh operands
+CHAIN_ROUNDINGS = 4
+
+
+def dataset(rows=700, cols=333, nnz=14000, seed=5):
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=seed)
+    return split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(seed))
+
+
+def dense(csr, rows, N, aux):
+    return scatter_rows_numpy(csr.row_ptr, csr.col, csr.val, rows, N, aux=aux)
+
+
+def oracle_opt(name, lr=None):
+    return {"adagrad": lambda: AdagradOracle(lr=lr or 0.005, epsilon=1e-8),
+            "rmsprop": lambda: RMSpropOracle(lr=lr or 0.001),
+            "adam": lambda: AdamOracle(lr=lr or 0.001)}[name]()
+
+
+def our_opt(name, lr=None):
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    return {"adagrad": lambda: O.Adagrad(lr=lr or 0.005, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=lr or 0.001),
+            "adam": lambda: O.Adam(lr=lr or 0.001)}[name]()
+
+
+class Result:
+    """loss_g / loss_o: mean per-step loss (GPU history / oracle); step_losses_*: per step;
+    rmse_g / rmse_o: compute_full_RMSE on the test split; w: GPU weights (Keras list); ora: the oracle
+    after the same steps; env: per-parameter Adagrad tolerance envelopes (16-bit modes) or None."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def max_param_err(self):
+        out = []
+        for i, (wg, wo) in enumerate(zip(self.w[0::2], self.ora.W)):
+            out.append(("W%d" % i, float(np.abs(wg - wo).max())))
+        for i, (bg, bo) in enumerate(zip(self.w[1::2], self.ora.b)):
+            out.append(("b%d" % i, float(np.abs(bg - bo).max())))
+        return out
+
+
+def sparse_batch(csr, rows, N, aux=-1.0):
+    """the batch (inputs X, output mask, targets) of a pass-through train batch with data_sparsity
+    [1, 1] as scipy CSR [B, N] (data_reader.py:158-169 writes X = T = rating, M_out = aux at every
+    rating of the row); duplicate-free data only (last-write-wins needs the dense scatter)"""
+    import scipy.sparse as sp
+    assert csr.dup is None, "sparse_batch: duplicate (row, col) entries need scatter_rows_numpy"
+    lens = csr.row_lengths()[rows]
+    ip = np.zeros(len(rows) + 1, np.int64)
+    np.cumsum(lens, out=ip[1:])
+    take = np.concatenate([np.arange(csr.row_ptr[r], csr.row_ptr[r + 1]) for r in rows])
+    col, val = csr.col[take], csr.val[take].astype(np.float64)
+    X = sp.csr_matrix((val, col, ip), shape=(len(rows), N))
+    Mo = sp.csr_matrix((np.full(len(col), aux), col, ip), shape=(len(rows), N))
+    return X, Mo, X
+
+
+def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_type=None, causal=False,
+               gather=True, sparse_dw=None, dropout=None, data=None, n_rows=None, lr=None, eval_rmse=True,
+               envelope=False, model_hook=None, sparse_oracle=False, eval_batches=None):
+    """`steps` training steps through fit_generator (one call per step, so the engine's Philox
+    dropout masks engine.mask[l][:B, :H] can be read back after each and fed to the oracle as Keras'
+    Dropout draw, model.py:72-73), then the oracle on the same rows (the generator exposes its epoch
+    plan) and compute_full_RMSE of both models on identical test batches (train.py:225-255).
+    sparse_oracle: the oracle's sparse-batch form (OmniOracle.loss_and_grads_sparse; one hidden
+    layer, no aux inputs) for the ML-20M / Netflix widths; eval_batches: test batches evaluated."""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    data = data if data is not None else dataset()
+    N = data.num_cols
+    np.random.seed(77)
+    rd = data_reader(N, n_rows or data.train.n_rows, dataset=data, eval_mode="fixed_split")
+    om = omni_model(layers, H, N, B, dense_activation=act, use_causal_info=causal, compute_dtype=compute_dtype,
+                    seed=11, dropout_probability=dropout)
+    m = om.model
+    om.engine.use_sparse = gather
+    if sparse_dw is not None:
+        om.engine.sparse_dw = sparse_dw
+    if model_hook is not None:
+        model_hook(om)
+    m.compile(our_opt(opt_name, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
+    w0 = m.get_weights()
+    gen = rd.data_gen(B, [1.0, 1.0], "train", True, aux_type, -1, pass_through_input_training=True)
+    masks, gpu_losses = [], []
+    for _ in range(steps):
+        hist = m.fit_generator(gen, 1, epochs=1, verbose=0)
+        gpu_losses.append(hist.history["loss"][0])
+        if dropout:
+            masks.append([mk[:B, :H].cpu().numpy().astype(np.float64) for mk in om.engine.mask])
+    w_gpu = m.get_weights()
+    live_rows_used = bool(om.engine._rtag_live)        # (the eval batches below reset it)
+    k = 1 + int(causal)
+    ora = OmniOracle([k * N] + [H] * layers + [N], activation=act, dropout=dropout,
+                     dtype=np.float64).set_params(w0[0::2], w0[1::2])
+    opt = oracle_opt(opt_name, lr)
+    u = UNIT_ROUNDOFF[compute_dtype]
+    env = None
+    if envelope:
+        if opt_name != "adagrad":
+            raise ValueError("the rounding envelope is derived for Adagrad")
+        env = [np.zeros_like(p) for p in ora.params()]
+        rmax = [np.zeros_like(p) for p in ora.params()]
+    losses = []
+    for bi in range(steps):
+        dm = masks[bi] if dropout else None
+        if sparse_oracle:
+            assert layers == 1 and not causal and aux_type is None
+            X, Mo, T = sparse_batch(data.train, gen.rows_host[bi], N)
+            out = ora.loss_and_grads_sparse(X, Mo, T, drop_masks=dm, u=u if envelope else None)
+            loss, _, gW, gb = out[:4]
+            if envelope:
+                GW, Gb = out[4], out[5]
+        else:
+            m_in, m_out, x, t, m_miss = dense(data.train, gen.rows_host[bi], N, -1.0)
+            xin = np.concatenate([x, m_miss if aux_type == "causal" else m_in], 1) if causal else x
+            loss, _, gW, gb = ora.loss_and_grads(xin, m_out, t, drop_masks=dm)
+            if envelope:
+                GW, Gb = ora.grad_magnitudes(xin, m_out, t, drop_masks=dm, u=u)
+        grads = [g for pair in zip(gW, gb) for g in pair]
+        if envelope:
+            for j, (g, G) in enumerate(zip(grads, [x for pair in zip(GW, Gb) for x in pair])):
+                r = CHAIN_ROUNDINGS * u * G / np.maximum(np.abs(g), 1e-30)
+                rmax[j] = np.maximum(rmax[j], r)
+                # g/sqrt(a) with a = sum of squares of the (equally perturbed) gradients so far
+                env[j] += opt.lr * np.minimum(2.0, 3.0 * rmax[j])
+        losses.append(loss)
+        ora.set_flat(opt.step(ora.params(), grads))
+    rmse_g = rmse_o = None
+    if eval_rmse:
+        np.random.seed(99)
+        tgen = rd.data_gen(B, None, "test", True, aux_type, -1, return_target_count=True)
+        nb = rd.test_set_size // B if eval_batches is None else min(eval_batches, rd.test_set_size // B)
+        sse, cnt = m.evaluate_sse(tgen, nb)
+        rmse_g = float(np.sqrt(sse / cnt))
+        sse_o, cnt_o = 0.0, 0
+        for bi in range(nb):
+            rows = tgen.rows_host[bi]
+            if sparse_oracle:
+                sse_o += _sparse_eval_sse(ora, data, rows, N)
+                cnt_o += int(data.test_tgt.row_lengths()[rows].sum())
+                continue
+            mi, _, x, _, mm = dense(data.test_in, rows, N, -1.0)
+            _, mo, _, t, mm2 = dense(data.test_tgt, rows, N, -1.0)
+            miss = np.maximum(np.abs(mm), np.abs(mm2)) * -1.0
+            xin = np.concatenate([x, miss if aux_type == "causal" else mi], 1) if causal else x
+            y, _ = ora.forward(xin, mo)
+            sse_o += float(((y - t) ** 2).sum())
+            cnt_o += int(data.test_tgt.row_lengths()[rows].sum())
+        assert cnt == cnt_o
+        rmse_o = float(np.sqrt(sse_o / cnt_o))
+    return Result(loss_g=float(np.mean(gpu_losses)), loss_o=float(np.mean(losses)), step_losses_g=gpu_losses,
+                  step_losses_o=losses, rmse_g=rmse_g, rmse_o=rmse_o, w=w_gpu, ora=ora, env=env, om=om, gen=gen,
+                  live_rows_used=live_rows_used,
+                  reader=rd, masks=masks)
+
+
+def _sparse_eval_sse(ora, data, rows, N):
+    """compute_full_RMSE's squared error of one test batch (train.py:243-252) from the sparse
+    forward: inputs from test_in, predictions only at the test_tgt entries (elsewhere y = T = 0)"""
+    import scipy.sparse as sp
+    X, _, _ = sparse_batch(data.test_in, rows, N)
+    h = ora.forward_hidden_sparse(X)
+    Tt, _, _ = sparse_batch(data.test_tgt, rows, N)
+    coo = Tt.tocoo()
+    y = -1.0 * (np.einsum("ij,ji->i", h[coo.row], ora.W[1][:, coo.col]) + ora.b[1][coo.col])
+    return float(((y - coo.data) ** 2).sum())
+
+
+def assert_fp32(res, loss_rel=FP32_ABS, rmse_abs=FP32_ABS, w_abs=FP32_ABS):
+    """the exact-fp32 bar: per-step loss, test RMSE, and the max-abs error of every parameter"""
+    for lg, lo in zip(res.step_losses_g, res.step_losses_o):
+        assert abs(lg - lo) <= loss_rel * abs(lo), (lg, lo)
+    if res.rmse_g is not None:
+        assert abs(res.rmse_g - res.rmse_o) <= rmse_abs, (res.rmse_g, res.rmse_o)
+    for name, err in res.max_param_err():
+        assert err <= w_abs, (name, err)
+
+
+def assert_low_precision(res, tol):
+    """16-bit operands: loss / RMSE within `tol` relative; every parameter inside its Adagrad
+    rounding envelope (+ FP32_ABS); returns the worst |error| / envelope ratio"""
+    for lg, lo in zip(res.step_losses_g, res.step_losses_o):
+        assert abs(lg - lo) <= tol * abs(lo), (lg, lo)
+    if res.rmse_g is not None:
+        assert abs(res.rmse_g - res.rmse_o) <= tol * res.rmse_o, (res.rmse_g, res.rmse_o)
+    worst = 0.0
+    got = list(res.w)
+    want = res.ora.params()
+    for j, (g, o, e) in enumerate(zip(got, want, res.env)):
+        err = np.abs(g - o)
+        lim = FP32_ABS + e
+        ratio = float((err / lim).max())
+        worst = max(worst, ratio)
+        assert ratio <= 1.0, ("param %d" % j, float(err.max()), int((err > lim).sum()))
+    return worst

@@ -87,4 +87,4 @@ def test_feature_parallel_equals_single_engine(gpu, causal):
         pairs = [(w_r[0], w[0][rows]), (w_r[1], w[1]), (w_r[2], w[2][:, c0:c1]), (w_r[3], w[3][c0:c1])]
         for got, want in pairs:
             assert got.shape == want.shape
-            assert np.quantile(np.abs(got - want), 0.999) < 1e-5
+            assert np.abs(got - want).max() <= 1e-5, float(np.abs(got - want).max())

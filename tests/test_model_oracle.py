@@ -81,3 +81,31 @@ def test_metrics_closed_forms():
     assert np.isclose(M.from_stats("accurate_RMSE", sse, sae, cnt, rs, B, N, 4.0), ref["accurate_RMSE"])
     assert np.isclose(M.from_stats("mean_absolute_error", sse, sae, cnt, rs, B, N, 4.0), ref["mean_absolute_error"])
     assert np.isclose(compute_full_RMSE([y], [t], cnt), np.sqrt(sse / cnt))
+
+
+@pytest.mark.parametrize("dropout", [None, 0.2])
+@pytest.mark.parametrize("act", ["sigmoid", "tanh"])
+def test_sparse_restatement_equals_dense(dropout, act):
+    """OmniOracle.loss_and_grads_sparse (the ML-20M / Netflix-width form) is the dense oracle on the
+    same batch: loss, gradients and the rounding envelope agree to fp64 roundoff"""
+    import scipy.sparse as sp
+    rng = np.random.RandomState(3)
+    B, N, H = 12, 57, 7
+    pat = rng.rand(B, N) < 0.15
+    t = np.where(pat, rng.randint(1, 11, size=(B, N)) / 2.0, 0.0)
+    m = -1.0 * pat
+    ora = OmniOracle([N, H, N], activation=act, dropout=dropout).init(1)
+    ora.W = [w.astype(np.float64) for w in ora.W]
+    ora.b = [rng.randn(*b.shape) * 0.1 for b in ora.b]
+    drop = [(rng.rand(B, H) >= dropout).astype(np.float64)] if dropout else None
+    loss, _, gW, gb = ora.loss_and_grads(t, m, t, drop)
+    GW, Gb = ora.grad_magnitudes(t, m, t, drop, u=2.0 ** -11)
+    X = sp.csr_matrix(t)
+    M = sp.csr_matrix(m)
+    ls, _, sW, sb, sGW, sGb = ora.loss_and_grads_sparse(X, M, X, drop, u=2.0 ** -11, chunk=5)
+    assert abs(ls - loss) <= 1e-13 * abs(loss)
+    for a, b in zip(gW + gb + GW + Gb, sW + sb + sGW + sGb):
+        np.testing.assert_allclose(np.asarray(b), a, rtol=1e-11, atol=1e-16)
+    h = ora.forward_hidden_sparse(X)
+    y, _ = ora.forward(t, m)
+    np.testing.assert_allclose(-(h @ ora.W[1] + ora.b[1]) * pat, y, rtol=1e-12, atol=1e-15)
