@@ -95,46 +95,53 @@ void jobs_after(const OcfGemmArgs& g, hipStream_t s) {
               ocf_last_error());
 }
 
-// EPI_OPTIM over a sparse batch operand given as row lists: one wave per weight row (ocf_rows_dw.h)
+// EPI_OPTIM over a sparse batch operand given as row lists: the row-stream kernel (ocf_rows_dw.h),
+// one wave per weight row.  Takes 16-bit compute, Adagrad / RMSprop / Adam with their slots, N a
+// multiple of 128 up to 512 and a row-major shadow; anything else returns false (the tile kernels).
 template <typename CT>
 bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
-  const int cpl = g.N / 64;
-  if (!(g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N)) return false;
-  if (ep.shadow && ep.shadow_blocked && cpl % 4 != 0) return false;
-  RowsDwArgs ra{};
-  ra.p = g.p; ra.s1 = g.s1; ra.s2 = g.s2; ra.ld = g.ld_out; ra.M = g.M; ra.N = g.N;
-  ra.B = g.B; ra.ldb = g.ldb;
-  ra.rowptr = g.sp_rowptr; ra.rowent = reinterpret_cast<const int2*>(g.sp_rowent); ra.vals = g.sp_vals;
-  ra.op = g.opt;
-  ra.shadow = ep.shadow; ra.shadow_dtype = ep.shadow_dtype; ra.shadow_blocked = ep.shadow_blocked;
-  ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
-  ra.skip_empty = g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f;
-  const WsJobs jb = ws_jobs(g);
-  const int waves = (g.M + RW_BLOCK - 1) / RW_BLOCK;
-  const int grid = std::max(1, (std::max(waves, jb.count()) + 3) / 4);
-  auto go = [&](auto kind_tag, auto cpl_tag) {
-    constexpr int KIND = decltype(kind_tag)::value, CPL = decltype(cpl_tag)::value;
-    hipLaunchKernelGGL((optim_rows_kernel<CT, KIND, CPL>), dim3(grid), dim3(RW_THREADS), 0, s, ra, jb);
-  };
-  auto by_cpl = [&](auto kind_tag) {
-    switch (cpl) {
-      case 2: go(kind_tag, std::integral_constant<int, 2>{}); break;
-      case 4: go(kind_tag, std::integral_constant<int, 4>{}); break;
-      case 6: go(kind_tag, std::integral_constant<int, 6>{}); break;
-      default: go(kind_tag, std::integral_constant<int, 8>{});
+  if constexpr (sizeof(CT) != 2) {
+    return false;   // a lane's B elements are one 4- or 8-B load of 16-bit values
+  } else {
+    const bool kind_ok = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
+                         (g.opt.kind == OCF_OPT_ADAM && g.s2);
+    if (!(kind_ok && g.s1 && g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N && g.M % 128 == 0))
+      return false;
+    if (ep.shadow && ep.shadow_blocked) return false;
+    RowsDwArgs ra{};
+    ra.p = g.p; ra.s1 = g.s1; ra.s2 = g.s2; ra.ld = g.ld_out; ra.M = g.M; ra.N = g.N;
+    ra.B = g.B; ra.ldb = g.ldb;
+    ra.rowptr = g.sp_rowptr; ra.rowent = reinterpret_cast<const int2*>(g.sp_rowent); ra.vals = g.sp_vals;
+    ra.live = g.row_live;
+    ra.op = g.opt;
+    ra.shadow = ep.shadow;
+    ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
+    const WsJobs jb = ws_jobs(g);
+    constexpr int PARTS = 8;
+    const int grid = std::max(g.M / 128 * PARTS, (jb.count() + 3) / 4);
+    // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
+    auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
+      constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
+      constexpr int NCH = decltype(nch_tag)::value;
+      hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
+    };
+    using std::integral_constant;
+    auto by_n = [&](auto k) {
+      switch (g.N) {
+        case 128: go(k, integral_constant<int, 2>{}, integral_constant<int, 1>{}); break;
+        case 256: go(k, integral_constant<int, 4>{}, integral_constant<int, 1>{}); break;
+        case 384: go(k, integral_constant<int, 2>{}, integral_constant<int, 3>{}); break;
+        default: go(k, integral_constant<int, 4>{}, integral_constant<int, 2>{});
+      }
+    };
+    switch (g.opt.kind) {
+      case OCF_OPT_ADAGRAD: by_n(integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
+      case OCF_OPT_RMSPROP: by_n(integral_constant<int, OCF_OPT_RMSPROP>{}); break;
+      default: by_n(integral_constant<int, OCF_OPT_ADAM>{});
     }
-  };
-  switch (g.opt.kind) {
-    case OCF_OPT_ADAGRAD: by_cpl(std::integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
-    case OCF_OPT_RMSPROP: by_cpl(std::integral_constant<int, OCF_OPT_RMSPROP>{}); break;
-    case OCF_OPT_ADAM:
-      OCF_CHECK(g.s2, "ocf_gemm OPTIM: Adam needs both slots");
-      by_cpl(std::integral_constant<int, OCF_OPT_ADAM>{});
-      break;
-    default: by_cpl(std::integral_constant<int, 0>{});
+    OCF_HIP(hipGetLastError());
+    return true;
   }
-  OCF_HIP(hipGetLastError());
-  return true;
 }
 
 // EPI_OPTIM on [K][M] x [K][N] operands (the dW GEMMs) through the persistent role-split kernel

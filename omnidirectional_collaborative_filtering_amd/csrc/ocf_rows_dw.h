@@ -1,220 +1,262 @@
-// Row-list weight-gradient + optimizer kernel (EPI_OPTIM over a sparse batch operand), gfx950.
+// Row-stream weight-gradient + optimizer kernel (EPI_OPTIM over a sparse batch operand), gfx950.
 //
 // The weight gradient of a first/last layer on a sparse batch is dW[m][:] = sum over the batch entries
-// (v, k) of column m of v * B[k][:] (B = the hidden activations h or deltas dh, [K][N]); v is the
-// live input (dW_in) or the output delta (dW_out).  At ML-20M a batch holds 0.5 % of the [K][M]
-// operand, so the MFMA form (optim_ws_kernel) spends its matrix-core and LDS work on zeros; here the
-// entries come as row lists (ocf_sparse_tiles row_ptr / row_ent: column m's entries in batch-row
-// order) and one wave owns one weight row at a time:
-//   lane l holds columns [l*CPL, l*CPL + CPL) of the row (CPL = N / 64), so every load / store of
-//   the row is one contiguous N*4-byte (or N*2-byte shadow) wave access;
-//   g = sum over the row's entries, in k order, of v * B[k][cols] (fp32 FMA, v and B as stored:
-//   fp32 values, compute-dtype B), then the optimizer update of p / slots, the shadow write, and for
-//   the output layer the column sum of v (the output-bias gradient) and its update.
-// One wave per task of RW_BLOCK consecutive rows (ballot over the row lengths); with Adagrad and
-// l2 == 0 rows without entries are skipped (zero gradient: identity update), otherwise every row is
-// updated (g = 0).  A row's parameter / slot loads are issued with its entry list, so the row costs
-// about two memory latencies; the many resident waves (small register footprint) keep HBM busy.
+// (v, k) of column m of v * B[k][:] (B = the hidden activations h or deltas dh, [K][N] in the compute
+// dtype; v = the live input (dW_in) or the output delta (dW_out), in fp32: one rounding fewer than the
+// MFMA form, which stages v in the compute dtype).  At ML-20M a batch holds 0.5 % of the [K][M]
+// operand and a live weight row has about two entries: its gradient is two 1-KB row reads from L2,
+// and the launch's real cost is the optimizer stream over the parameter / slot rows (Adagrad: 16 B
+// per element + the 2-B shadow).  The role-split MFMA kernel (ocf_optim_ws.h) streams that in 128 x
+// 128 tiles, i.e. 512-B row pieces 2 KB apart, beside a K-loop over 99.5 % zeros.
+//
+// This kernel is shaped after the stream instead: one wave per weight row, whole rows, rows in order.
+// Lane l owns the CW-float chunks l + 64 j (j < NCH, N = 64 CW NCH), so each wave instruction reads or
+// writes 64 CW * 4 contiguous bytes (tools/probes/opt_stream.hip, the parameter stream alone: whole
+// 2-KB rows with nt loads and stores 6.05 TB/s with 67 % of the rows live, 128-column tile pieces
+// 5.31 TB/s).  A row's entry list is wave-uniform: entries and values are scalar loads and each
+// entry's B piece is one coalesced wave load.  Rows come from the live-row records (ocf.h
+// OCF_LIVE_REC, compacted per 128-row tile; Adagrad with l2 == 0: a row without entries has the
+// identity update) or, without records, every row.  Per element the sum over the entries runs in
+// entry (batch-row) order in fp32.  Measured (ML-20M step, dW_in launch, HIP events): 199 us for the
+// role-split MFMA kernel; 194 us one row batch per wave without pipelining (the chain record -> row
+// pointer -> entry -> value, B row ran after the HBM loads); 150-155 us pipelined as below.
 #pragma once
 #include "ocf_epilogues.h"
 #include "ocf_optim_ws.h"
 
 namespace ocf {
 
-constexpr int RW_THREADS = 256;
+constexpr int RS_THREADS = 256;
+constexpr int RS_E0 = 2;   // entries per row loaded with the row's first loads (E0 = 1 / 3: equal / 3 % slower)
+constexpr int RS_ET = 4;   // entries loaded together beyond those (rows of long batches)
 
 struct RowsDwArgs {
   float* p; float* s1; float* s2;
   int64_t ld;                 // parameter row stride (floats) = N
   int M, N;
-  const void* B; int64_t ldb; // [K][ldb] compute dtype (or fp32)
+  const void* B; int64_t ldb; // [K][ldb] compute dtype
   const int32_t* rowptr; const int2* rowent; const float* vals;
+  const uint8_t* live;        // live-row records per 128-row tile, or null (every row)
   OcfOptParams op;
-  void* shadow; int shadow_dtype; bool shadow_blocked;
+  void* shadow;               // row-major compute-dtype copy of p, or null
   float* colsum; float colsum_scale;
-  int skip_empty;
 };
 
-constexpr int RW_BLOCK = 16;     // rows per wave task (one wave per task)
-constexpr int RW_EB = 8;         // entries whose B rows are loaded together
-
-// one weight row in flight: its parameters / slots (this lane's columns), entry range, the entry of
-// this lane (< 64), and the first RW_EB entries' values and B pieces
-template <typename BT, int CPL, int NS> struct RwRow {
-  float p[CPL], a[CPL], b[NS == 2 ? CPL : 1];
-  int m, lo, n;
-  int2 en;
-  float ve;
-  BT bv[RW_EB][CPL];
-  float vv[RW_EB];
-};
-
-template <typename BT, int KIND, int CPL>
-__global__ void __launch_bounds__(RW_THREADS) optim_rows_kernel(RowsDwArgs ra, WsJobs jobs) {
-  constexpr int NS = KIND == OCF_OPT_ADAM ? 2 : 1;
-  static_assert(CPL % 2 == 0, "columns per lane");
-  using Row = RwRow<BT, CPL, NS>;
-  const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * (RW_THREADS / 64) + (threadIdx.x >> 6);
-  const int nwaves = gridDim.x * (RW_THREADS / 64);
-  {  // folded small jobs (bias updates, stats): one per wave
-    const int nj = jobs.count();
-    for (int j = wave; j < nj; j += nwaves) jobs.run<KIND>(j, lane);
+template <int CW> struct RsVec;
+template <> struct RsVec<4> {
+  using F = float4;
+  using H = uint2;     // four 16-bit values
+  static __device__ __forceinline__ F ld(__amdgpu_buffer_rsrc_t r, const float* base, uint32_t o) {
+    return ld_pol16<OCF_OPT_LD_POL>(r, base, o);
   }
-  const int r0 = wave * RW_BLOCK;
-  if (r0 >= ra.M) return;
-  const int c0 = lane * CPL;
-  const BT* Bg = reinterpret_cast<const BT*>(ra.B);
-  const __amdgpu_buffer_rsrc_t rp = wt_rsrc(ra.p), r1 = wt_rsrc(ra.s1), r2 = wt_rsrc(ra.s2);
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, float* base, uint32_t o, const F& v) {
+    st_pol16<OCF_OPT_ST_POL>(r, base, o, v);
+  }
+  static __device__ __forceinline__ F zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+};
+template <> struct RsVec<2> {
+  using F = float2;
+  using H = uint32_t;  // two 16-bit values
+  static __device__ __forceinline__ F ld(__amdgpu_buffer_rsrc_t r, const float* base, uint32_t o) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    const u2 u = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, OCF_OPT_LD_POL);
+    F f;
+    __builtin_memcpy(&f, &u, 8);
+    (void)base;
+    return f;
+  }
+  static __device__ __forceinline__ void st(__amdgpu_buffer_rsrc_t r, float* base, uint32_t o, const F& v) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    u2 u;
+    __builtin_memcpy(&u, &v, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, o, 0, OCF_OPT_ST_POL);
+    (void)base;
+  }
+  static __device__ __forceinline__ F zero() { return make_float2(0.f, 0.f); }
+};
 
-  // 16-B buffer loads / stores with the optimizer streams' cache policy (CPL % 4 == 0), else 8-B
-  auto ldv = [&](__amdgpu_buffer_rsrc_t r, const float* base, uint32_t ob, float* dst) {
-    if constexpr (CPL % 4 == 0) {
+// A workgroup takes one of PARTS equal parts of a tile's live rows and each wave walks its
+// rows (ranks kb + wave + 4 i) one per iteration, with the index chain run ahead of the data:
+//   A (row i+3): record byte -> row m;             B (row i+2): row pointers, p / slot loads (HBM);
+//   C (row i+1): the first RS_E0 entries;          D (row i+1): their values and B pieces (L2);
+//   E (row i):   gradient, update, stores.
+// Scalar loads return out of order (a use waits for every outstanding one), so each iteration
+// advances every row by one stage and the chain never waits on the HBM loads or they on it.
+// PARTS = 8 (about 11 rows per wave at ML-20M): 2 and 4 parts 177 / 165 us, 6-12 within noise.
+template <int CW, int NCH, int E0, bool ADAM> struct RpRow {
+  using F = typename RsVec<CW>::F;
+  using H = typename RsVec<CW>::H;
+  int m, lo, n;
+  bool lv;
+  int2 e[E0];
+  float v[E0];
+  H h[E0][NCH];
+  F p[NCH], a[NCH], b[ADAM ? NCH : 1];
+  WsJobs::BiasPre bias;   // output-layer bias and its slots (colsum rows with a folded bias update)
+};
+
+template <typename CT, int KIND, int CW, int NCH, int PARTS>
+__global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
+  using V = RsVec<CW>;
+  using F = typename V::F;
+  using H = typename V::H;
+  constexpr bool ADAM = KIND == OCF_OPT_ADAM;
+  constexpr int E0 = RS_E0;
+  using Row = RpRow<CW, NCH, E0, ADAM>;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {  // folded small jobs (hidden-bias update from the decoder's partials, the step's stats): one per wave
+    const int nj = jobs.count();
+    for (int j = blockIdx.x * 4 + wave; j < nj; j += gridDim.x * 4) jobs.run<KIND>(j, lane);
+  }
+  const int t = blockIdx.x / PARTS, part = blockIdx.x % PARTS;
+  const int m0 = t * 128;
+  const uint8_t* rec = ra.live ? ra.live + (int64_t)t * OCF_LIVE_REC : nullptr;
+  const int L = rec ? *reinterpret_cast<const int*>(rec) : (ra.M - m0 < 128 ? ra.M - m0 : 128);
+  auto row_of = [&](int k) { return rec ? (int)rec[16 + (k & 7) * 16 + (k >> 3)] : k; };
+  if (ra.colsum && rec && part == 0) {      // rows without entries: zero output-bias gradient
+    __shared__ uint8_t live_fl[128];
+    if (tid < 128) live_fl[tid] = 0;
+    __syncthreads();
+    if (tid < L) live_fl[row_of(tid)] = 1;
+    __syncthreads();
+    if (tid < 128 && !live_fl[tid]) ra.colsum[m0 + tid] = 0.f;
+  }
+  // this part's ranks [kb, ke), this wave's: kb + wave + 4 i, i < nr
+  const int kb = part * L / PARTS, ke = (part + 1) * L / PARTS;
+  const int nr = __builtin_amdgcn_readfirstlane(ke - kb - wave > 0 ? (ke - kb - wave + 3) / 4 : 0);
+  if (nr == 0) return;
+
+  const __amdgpu_buffer_rsrc_t rp = wt_rsrc(ra.p), r1 = wt_rsrc(ra.s1), r2 = wt_rsrc(ra.s2);
+  const CT* Bg = reinterpret_cast<const CT*>(ra.B);
+  auto col = [&](int j) { return (lane + 64 * j) * CW; };
+  auto off = [&](int m, int j) { return (uint32_t)(((int64_t)m * ra.ld + col(j)) * 4); };   // < 2 GiB: host check
+  auto bpiece = [&](int k, int j) { return *reinterpret_cast<const H*>(Bg + (int64_t)k * ra.ldb + col(j)); };
+  auto stA = [&](Row& r, int i) {
+    r.lv = i < nr;
+    r.m = m0 + __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * (i < nr ? i : 0)));
+  };
+  auto stB = [&](Row& r) {
+    if (!r.lv) return;
+    r.lo = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m]);
+    r.n = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m + 1]) - r.lo;
 #pragma unroll
-      for (int c = 0; c < CPL; c += 4) {
-        const float4 x = ld_pol16<OCF_OPT_LD_POL>(r, base, ob + c * 4);
-        dst[c] = x.x; dst[c + 1] = x.y; dst[c + 2] = x.z; dst[c + 3] = x.w;
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < CPL; c += 2) {
-        const float2 x = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(base) + ob + c * 4);
-        dst[c] = x.x; dst[c + 1] = x.y;
-      }
+    for (int j = 0; j < NCH; ++j) {
+      const uint32_t o = off(r.m, j);
+      r.p[j] = V::ld(rp, ra.p, o);
+      r.a[j] = V::ld(r1, ra.s1, o);
+      if constexpr (ADAM) r.b[j] = V::ld(r2, ra.s2, o);
     }
   };
-  auto stv = [&](__amdgpu_buffer_rsrc_t r, float* base, uint32_t ob, const float* src) {
-    if constexpr (CPL % 4 == 0) {
+  auto stC = [&](Row& r) {
+    if (!r.lv) return;
 #pragma unroll
-      for (int c = 0; c < CPL; c += 4)
-        st_pol16<OCF_OPT_ST_POL>(r, base, ob + c * 4, make_float4(src[c], src[c + 1], src[c + 2], src[c + 3]));
-    } else {
-#pragma unroll
-      for (int c = 0; c < CPL; c += 2)
-        *reinterpret_cast<float2*>(reinterpret_cast<char*>(base) + ob + c * 4) = make_float2(src[c], src[c + 1]);
-    }
+    for (int e = 0; e < E0; ++e) r.e[e] = e < r.n ? ra.rowent[r.lo + e] : make_int2(0, 0);
+    if (ra.colsum && jobs.cb_p) r.bias = jobs.colsum_pre(r.m);
   };
-  auto off = [&](int m) { return (uint32_t)(((int64_t)m * ra.ld + c0) * 4); };   // < 2 GiB: host check
-  // stage 1: parameters, slots and the entry list of a row (HBM)
-  auto stage1 = [&](Row& r, int m, int lo, int n) {
-    r.m = m; r.lo = lo; r.n = n;
-    const uint32_t ob = off(m);
-    ldv(rp, ra.p, ob, r.p);
-    ldv(r1, ra.s1, ob, r.a);
-    if constexpr (NS == 2) ldv(r2, ra.s2, ob, r.b);
-    r.en = lane < n ? ra.rowent[lo + lane] : make_int2(0, 0);
-  };
-  // stage 2a: the values and B pieces of the row's first RW_EB entries (L2)
-  auto load_ents = [&](Row& r, int e0) {
+  auto stD = [&](Row& r) {
+    if (!r.lv) return;
 #pragma unroll
-    for (int u = 0; u < RW_EB; ++u) {
-      const int e = e0 + u;
-      r.vv[u] = 0.f;
+    for (int e = 0; e < E0; ++e) {
+      r.v[e] = 0.f;
       if (e < r.n) {
-        int k;
-        if (e < 64) {
-          k = __builtin_amdgcn_readlane(r.en.y, e);
-          r.vv[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, r.ve), e));
-        } else {
-          const int2 x = ra.rowent[r.lo + e];
-          k = x.y;
-          r.vv[u] = ra.vals[x.x];
-        }
-        __builtin_memcpy(r.bv[u], Bg + (int64_t)k * ra.ldb + c0, sizeof(r.bv[u]));
+        r.v[e] = ra.vals[r.e[e].x];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) r.h[e][j] = bpiece(r.e[e].y, j);
       }
     }
   };
-  auto stage2a = [&](Row& r) {
-    r.ve = lane < r.n ? ra.vals[r.en.x] : 0.f;
-    load_ents(r, 0);
-  };
-  // stage 2b: g = sum over the entries, in k order, of v * B[k][cols]; the update; the stores
-  auto stage2b = [&](Row& r) {
-    float g[CPL];
+  const OcfOptParams o = ra.op;
+  auto acc = [&](F& g, float v, H h) {
+    CT x[CW];
+    __builtin_memcpy(x, &h, sizeof(h));
+    float* gf = reinterpret_cast<float*>(&g);
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) g[c] = 0.f;
+    for (int i = 0; i < CW; ++i) gf[i] += v * CvtT<CT>::from(x[i]);
+  };
+  auto stE = [&](Row& r) {
+    if (!r.lv) return;
+    F g[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) g[j] = V::zero();
     float cs = 0.f;
-    for (int e0 = 0; e0 < r.n; e0 += RW_EB) {
-      if (e0 > 0) load_ents(r, e0);   // rows with more than RW_EB entries
 #pragma unroll
-      for (int u = 0; u < RW_EB; ++u) {
-        if (e0 + u < r.n) {
+    for (int e = 0; e < E0; ++e)
+      if (e < r.n) {
 #pragma unroll
-          for (int c = 0; c < CPL; ++c) g[c] += r.vv[u] * (float)r.bv[u][c];
-          cs += r.vv[u];
+        for (int j = 0; j < NCH; ++j) acc(g[j], r.v[e], r.h[e][j]);
+        cs += r.v[e];
+      }
+    for (int e0 = E0; e0 < r.n; e0 += RS_ET) {            // rows with more entries: RS_ET at a time
+      int2 x[RS_ET];
+      float v[RS_ET];
+      H hx[RS_ET][NCH];
+#pragma unroll
+      for (int e = 0; e < RS_ET; ++e) x[e] = e0 + e < r.n ? ra.rowent[r.lo + e0 + e] : make_int2(0, 0);
+#pragma unroll
+      for (int e = 0; e < RS_ET; ++e) {
+        v[e] = 0.f;
+        if (e0 + e < r.n) {
+          v[e] = ra.vals[x[e].x];
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) hx[e][j] = bpiece(x[e].y, j);
         }
       }
-    }
-    const OcfOptParams o = ra.op;
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      float bb = 0.f;
-      if constexpr (NS == 2) bb = r.b[c];
-      opt_update_k<KIND>(o, g[c] * o.gscale, r.p[c], r.a[c], bb);
-      if constexpr (NS == 2) r.b[c] = bb;
-    }
-    const uint32_t ob = off(r.m);
-    stv(rp, ra.p, ob, r.p);
-    stv(r1, ra.s1, ob, r.a);
-    if constexpr (NS == 2) stv(r2, ra.s2, ob, r.b);
-    if (ra.shadow) {
-      if (ra.shadow_blocked) {   // 64x64 blocks (CPL % 4 == 0, checked on the host)
-        EpiOptim::Params sh{};
-        sh.ld = ra.ld; sh.shadow = ra.shadow; sh.shadow_dtype = ra.shadow_dtype; sh.shadow_blocked = true;
+      for (int e = 0; e < RS_ET; ++e)
+        if (e0 + e < r.n) {
 #pragma unroll
-        for (int c = 0; c + 3 < CPL; c += 4)
-          EpiOptim::store_shadow(sh, r.m, c0 + c, make_float4(r.p[c], r.p[c + 1], r.p[c + 2], r.p[c + 3]));
-      } else {
-        char* dst = reinterpret_cast<char*>(ra.shadow) + ((int64_t)r.m * ra.ld + c0) * 2;
-        uint16_t hv[CPL];
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          if (ra.shadow_dtype == OCF_F16) {
-            const _Float16 x = (_Float16)r.p[c];
-            __builtin_memcpy(&hv[c], &x, 2);
-          } else {
-            const __bf16 x = (__bf16)r.p[c];
-            __builtin_memcpy(&hv[c], &x, 2);
-          }
+          for (int j = 0; j < NCH; ++j) acc(g[j], v[e], hx[e][j]);
+          cs += v[e];
         }
-        __builtin_memcpy(dst, hv, sizeof(hv));
+    }
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      F p = r.p[j], a = r.a[j], b = V::zero();
+      if constexpr (ADAM) b = r.b[j];
+      float* pf = reinterpret_cast<float*>(&p);
+      float* af = reinterpret_cast<float*>(&a);
+      float* bf = reinterpret_cast<float*>(&b);
+      const float* gf = reinterpret_cast<const float*>(&g[j]);
+#pragma unroll
+      for (int i = 0; i < CW; ++i) opt_update_k<KIND>(o, gf[i] * o.gscale, pf[i], af[i], bf[i]);
+      const uint32_t ob = off(r.m, j);
+      V::st(rp, ra.p, ob, p);
+      V::st(r1, ra.s1, ob, a);
+      if constexpr (ADAM) V::st(r2, ra.s2, ob, b);
+      if (ra.shadow) {
+        CT hh[CW];
+#pragma unroll
+        for (int i = 0; i < CW; ++i) hh[i] = CvtT<CT>::to(pf[i]);
+        H w;
+        __builtin_memcpy(&w, hh, sizeof(w));
+        *reinterpret_cast<H*>(reinterpret_cast<char*>(ra.shadow) + ((int64_t)r.m * ra.ld + col(j)) * 2) = w;
       }
     }
-    if (ra.colsum && lane == 0) {   // output-bias gradient (column sum of the entries, k order) + update
+    if (ra.colsum && lane == 0) {   // output-bias gradient (column sum of the entries) and its update
       const float v = cs * ra.colsum_scale;
       ra.colsum[r.m] = v;
-      if (jobs.cb_p) jobs.colsum_bias<KIND>(r.m, v, jobs.colsum_pre(r.m));
+      if (jobs.cb_p) jobs.colsum_bias<KIND>(r.m, v, r.bias);
     }
   };
-
-  // the task's row lengths (lanes < RW_BLOCK), then its rows through a two-row pipeline: the next
-  // row's HBM loads are issued after the current row's L2 loads and before the current row waits
-  int lo = 0, n = 0;
-  if (lane < RW_BLOCK && r0 + lane < ra.M) {
-    lo = ra.rowptr[r0 + lane];
-    n = ra.rowptr[r0 + lane + 1] - lo;
-    if (ra.colsum && n == 0 && ra.skip_empty) ra.colsum[r0 + lane] = 0.f;   // skipped rows: zero column sum
-  }
-  uint64_t todo = __ballot(lane < RW_BLOCK && r0 + lane < ra.M && (n > 0 || !ra.skip_empty));
-  if (!todo) return;
-  Row cur, nxt;
-  {
-    const int l = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    stage1(cur, r0 + l, __builtin_amdgcn_readlane(lo, l), __builtin_amdgcn_readlane(n, l));
-  }
-  while (true) {
-    stage2a(cur);
-    const bool more = todo != 0;
-    if (more) {
-      const int l = __builtin_ctzll(todo);
-      todo &= todo - 1;
-      stage1(nxt, r0 + l, __builtin_amdgcn_readlane(lo, l), __builtin_amdgcn_readlane(n, l));
-    }
-    stage2b(cur);
-    if (!more) break;
-    cur = nxt;
+  // prologue: row 0 through D, row 1 through B, row 2 through A
+  Row r0, r1s, r2s;
+  stA(r0, 0);
+  stA(r1s, 1);
+  stB(r0);
+  stA(r2s, 2);
+  stB(r1s);
+  stC(r0);
+  stD(r0);
+  for (int i = 0; i < nr; ++i) {
+    Row r3;
+    stA(r3, i + 3);
+    stB(r2s);
+    stC(r1s);
+    stD(r1s);
+    stE(r0);
+    r0 = r1s;
+    r1s = r2s;
+    r2s = r3;
   }
 }
-
 }  // namespace ocf

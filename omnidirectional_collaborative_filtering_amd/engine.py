@@ -239,11 +239,11 @@ class Engine:
         # (K = 512) 0.453 vs 0.509, 4-way (K = 1,024) 0.42 vs 0.38, 8-way (K = 2,048) 0.46 vs 0.375.
         self.sparse_dw = Bp <= 512
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
-        # ... or as row lists (the buckets' transpose): the weight gradient row by row from the entries,
-        # one wave per weight row, no MFMA over the mostly-zero batch operand (ocf_rows_dw.h).  Measured
-        # slower than the role-split MFMA kernel (ML-20M step 0.534 vs 0.508 ms; 8-way feature-parallel
-        # rank step 0.411 vs 0.374 on the generic kernel): each row pays a dependent entry -> B chain.
-        self.dw_rows = False
+        # ... and as row lists (the buckets' transpose) for the row-stream kernel (ocf_rows_dw.h): one
+        # wave per live weight row streams whole parameter / slot rows and forms the row's gradient from
+        # its ~2 entries, no MFMA over the mostly-zero batch operand.  ML-20M step 0.50 -> 0.44 ms
+        # (dW 200 -> 150-165 us per launch).  16-bit compute only (the library falls back otherwise).
+        self.dw_rows = self.cdt != _lib.DT_F32
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)

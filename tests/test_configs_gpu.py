@@ -17,7 +17,7 @@ Adagrad rounding envelopes).  The wide configurations use the oracle's sparse-ba
 import numpy as np
 import pytest
 
-from parity import assert_fp32, assert_low_precision, run_parity
+from parity import CHAIN_ROUNDINGS, assert_fp32, assert_low_precision, run_parity
 
 
 def _synth(name, **kw):
@@ -110,27 +110,45 @@ def _jester_fit_vs_oracle(n_users, validation_split):
     idx = np.arange(split_at)
     np.random.shuffle(idx)
     losses = []
+    env = [np.zeros_like(p) for p in ora.params()]
+    rmax = [np.zeros_like(p) for p in ora.params()]
     for s in range(split_at // B):
         sel = idx[s * B:(s + 1) * B]
         xin = np.concatenate([inputs[sel], observed[sel]], 1)
         loss, _, gW, gb = ora.loss_and_grads(xin, out_m[sel], targets[sel])
+        grads = [g for pair in zip(gW, gb) for g in pair]
+        if s < ENVELOPE_STEPS:
+            GW, Gb = ora.grad_magnitudes(xin, out_m[sel], targets[sel], u=FP32_U)
+            for j, (g, G) in enumerate(zip(grads, [x for pair in zip(GW, Gb) for x in pair])):
+                rmax[j] = np.maximum(rmax[j], CHAIN_ROUNDINGS * FP32_U * G / np.maximum(np.abs(g), 1e-30))
+                # RMSprop's step lr g / sqrt(a) is at most lr / sqrt(1 - rho) and moves by ~2 r relative
+                env[j] += opt.lr / np.sqrt(1.0 - opt.rho) * np.minimum(2.0, 3.0 * rmax[j])
         losses.append(loss)
-        ora.set_flat(opt.step(ora.params(), [g for pair in zip(gW, gb) for g in pair]))
+        ora.set_flat(opt.step(ora.params(), grads))
     vl = []
     for s in range((n - split_at) // B):
         sel = np.arange(split_at + s * B, split_at + (s + 1) * B)
         y, _ = ora.forward(np.concatenate([inputs[sel], observed[sel]], 1), out_m[sel])
         vl.append(float(((y - targets[sel]) ** 2).mean()))
-    return h, losses, vl, m.get_weights(), ora.params()
+    return h, losses, vl, m.get_weights(), ora.params(), env
+
+
+FP32_U = 2.0 ** -24
+ENVELOPE_STEPS = 8
 
 
 @pytest.mark.gpu
 def test_jester_fit_steps_fp32(gpu):
-    """four Model.fit steps (512 users, no hold-out): the exact-fp32 bar, every weight within 1e-5"""
-    h, losses, _, w, p = _jester_fit_vs_oracle(512, 0.0)
+    """four Model.fit steps (512 users, no hold-out): the exact-fp32 bar, every weight within 1e-5
+    plus its fp32 conditioning envelope.  RMSprop's first steps are lr g / sqrt((1 - rho) g^2) =
+    +-lr / sqrt(0.1) whatever |g|, so an element whose gradient is within fp32 rounding distance of
+    zero (|g| <~ 4 u G, G = OmniOracle.grad_magnitudes) has a sign the fp32 kernel and the fp64
+    oracle need not agree on; measured: 2.4e-5 on 1 of 51,200 W0 elements with 1e-5 flat"""
+    h, losses, _, w, p, env = _jester_fit_vs_oracle(512, 0.0)
     assert abs(h.history["loss"][0] - np.mean(losses)) <= 1e-5 * np.mean(losses)
-    for i, (g, o) in enumerate(zip(w, p)):
-        assert np.abs(g - o).max() <= 1e-5, (i, float(np.abs(g - o).max()))
+    for i, (g, o, e) in enumerate(zip(w, p, env)):
+        err = np.abs(g - o)
+        assert (err <= 1e-5 + e).all(), (i, float(err.max()), int((err > 1e-5).sum()))
 
 
 @pytest.mark.gpu
@@ -140,7 +158,7 @@ def test_jester_fit_epoch_fp32(gpu):
     val_loss), exact fp32: epoch loss and val_loss within 1e-5 relative; after 516 steps the fp32
     weights have drifted from the fp64 oracle's by accumulated rounding, so the weight bar for the
     whole epoch is 1e-4 (measured 7.2e-5 on the hidden->hidden kernel; 4 steps hold 1e-5, above)"""
-    h, losses, vl, w, p = _jester_fit_vs_oracle(73_421, 0.1)
+    h, losses, vl, w, p, _ = _jester_fit_vs_oracle(73_421, 0.1)
     assert abs(h.history["loss"][0] - np.mean(losses)) <= 1e-5 * np.mean(losses)
     assert abs(h.history["val_loss"][0] - np.mean(vl)) <= 1e-5 * np.mean(vl)
     for i, (g, o) in enumerate(zip(w, p)):

@@ -40,7 +40,7 @@ def phase_of(name, seen):
     if "EpiSlab" in name:
         k = seen["slab"] = seen.get("slab", -1) + 1
         return ("enc_gemm", "dec_bwd_gemm")[k % 2]
-    if "EpiOptim" in name:
+    if "EpiOptim" in name or "optim_rowpipe" in name:
         k = seen["optim"] = seen.get("optim", -1) + 1
         return ("dW_out", "dW_in")[k % 2]
     if "scatter_flat" in name:
