@@ -56,15 +56,11 @@ def parse():
                          "numerics of a partial model); not a bench line")
     ap.add_argument("--emulate-comm", type=int, default=1,
                     help="with --emulate-shards: run the rank's collective code path with no-op collectives")
-    ap.add_argument("--sparse-clear", type=int, default=0,
-                    help="clear the previous batch's layer-0 entries instead of a dense memset")
     ap.add_argument("--sparse-dw", type=int, default=-1,
                     help="weight-gradient GEMMs build their batch operand in LDS from the entries (-1: engine's "
                          "choice by batch size)")
     ap.add_argument("--gather", type=int, default=1,
                     help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
-    ap.add_argument("--nt-operands", type=int, default=0,
-                    help="non-temporal loads for GEMM operands at their last use in the step")
     ap.add_argument("--ws-max-k", type=int, default=0,
                     help="largest batch K routed to the role-split dW kernel (0: library default)")
     ap.add_argument("--fold-jobs", type=int, default=1,
@@ -72,22 +68,22 @@ def parse():
     ap.add_argument("--shadow-blocked", type=int, default=-1,
                     help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
     ap.add_argument("--dw-rows", type=int, default=-1,
-                    help="weight gradients row by row from the entries (1) or by the MFMA role-split kernel (0)")
+                    help="weight gradients by the row-stream kernel (1) or the role-split MFMA kernel (0); -1: engine default")
     ap.add_argument("--split-dw", type=int, default=1,
                     help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
-    ap.add_argument("--split-dw-1gpu", type=int, default=0,
-                    help="single GPU: the two persistent dW kernels on two streams")
     ap.add_argument("--fuse-enc", type=int, default=1,
                     help="single GPU, one hidden layer: the decoder gather applies the hidden layer's bias / "
                          "activation / dropout to the encoder partials itself (0: separate row-reduce launch)")
-    ap.add_argument("--async-tb", type=int, default=0,
-                    help="per-batch tile buckets on the side stream, overlapping the row gathers (0: main stream)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
-                         "(replicated weights, gradient all-reduce)")
+                         "(replicated weights, gradient exchange)")
+    ap.add_argument("--dp-mode", default="sharded", choices=["sharded", "allreduce"],
+                    help="dp: reduce-scatter + sharded optimizer + all-gather, or one all-reduce + full optimizer")
+    ap.add_argument("--dp-grad-dtype", default="float32", choices=["float32", "bfloat16"],
+                    help="dp sharded: gradient dtype of the reduce-scatter")
     return ap.parse_args()
 
 
@@ -142,9 +138,8 @@ def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps):
 
 def main():
     args = parse()
-    from omnidirectional_collaborative_filtering_amd.parallel import (GradBucket, dp_train_step,
-                                                                      feature_shard_range, init_from_env, make_comm,
-                                                                      shard_batches)
+    from omnidirectional_collaborative_filtering_amd.parallel import (DataParallel, feature_shard_range,
+                                                                      init_from_env, make_comm, shard_batches)
     rank, world, local = init_from_env()
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
@@ -183,17 +178,13 @@ def main():
     m.compile(optim(args.optimizer, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
     w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
     eng = om.engine
-    eng.sparse_clear = bool(args.sparse_clear)
-    eng.nt_operands = bool(args.nt_operands)
     if args.sparse_dw >= 0:
         eng.sparse_dw = bool(args.sparse_dw)
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
     eng.split_dw_streams = bool(args.split_dw)
-    eng.split_dw_streams_1gpu = bool(args.split_dw_1gpu)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
-    eng.async_tile_buckets = bool(args.async_tb)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
@@ -205,17 +196,18 @@ def main():
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)
-    bucket = GradBucket(eng) if (world > 1 and not fp) else None
+    dpo = DataParallel(eng, rank, world, mode=args.dp_mode, grad_dtype=args.dp_grad_dtype) \
+        if (world > 1 and not fp) else None
     nnz_of = gen.nnz1
     setup_s = time.time() - t0
 
     def step(i):
         bi = batches[i % len(batches)]
         m._load(None, gen, bi)
-        if fp:
-            eng.train_step()
+        if dpo is not None:
+            dpo.step()
         else:
-            dp_train_step(eng, bucket, world)
+            eng.train_step()
         return int(nnz_of[bi])
 
     # warm-up (untimed): every phase bracketed by HIP events -> per-phase breakdown and the dominant
@@ -307,7 +299,8 @@ def main():
     roof = None
     if dom is not None and dom_timed:
         if world > 1 and not fp and dom in ("dW_in", "dW_out"):
-            alg[dom] = P * 4 + B * N * 2 + B * H * 2     # gradient store instead of the fused update
+            # gradient store instead of the fused update
+            alg[dom] = P * (2 if args.dp_grad_dtype == "bfloat16" else 4) + a_bytes + B * H * 2
         ms = dom_timed["mean_ms"]
         ach = alg[dom] / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -93,7 +93,7 @@ typedef struct OcfScatterArgs {
   const int64_t* lboff1; const int64_t* lboff2;
   int64_t E1, E2;
   uint8_t* tflag1; uint8_t* tflag2;
-  /* 1: xin is already zero (the caller cleared the previous batch with ocf_scatter_clear), so the
+  /* 1: xin is already zero (nothing was written to it since it was last cleared), so the
    * [B_pad][xin_ld] memset is skipped */
   int xin_clean;
   /* per batch-local source-1 entry: its rating if it is a live input (the value X keeps after
@@ -110,11 +110,6 @@ typedef struct OcfScatterArgs {
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
-
-/* Zero the xin entries a previous ocf_scatter_batch call with the same arguments wrote (every
- * block of every source entry's column): a sparse clear replacing the dense memset of the next
- * batch.  Only xin is touched. */
-int ocf_scatter_clear(const OcfScatterArgs* args, void* stream);
 
 /*
  * Row-gather products for sparse batches (csrc/ocf_sparse.hip): the encoder sum over a batch row's
@@ -194,7 +189,8 @@ typedef struct OcfGemmArgs {
   int order;                 /* tile order: 0 n-fastest, 1 m-fastest                            */
   int epi;
   /* epilogue operands (meaning per epilogue; unused ones may be NULL/0) */
-  float* out; int64_t ld_out; int64_t split_stride;          /* SLAB, GRAD, PREDICT          */
+  float* out; int64_t ld_out; int64_t split_stride;          /* SLAB, GRAD, PREDICT; GRAD writes
+                                                                 bf16 when h_dtype == OCF_BF16  */
   const float* bias;                                          /* BIAS_ACT, PREDICT, MSE       */
   int act; float keep; uint64_t seed, stream;                 /* BIAS_ACT, GRAD_ACT           */
   const uint8_t* mask_in; uint8_t* mask_out;                  /* dropout masks                */
@@ -280,6 +276,11 @@ int ocf_opt_step(float* p, const float* g, float* s1, float* s2, int64_t n, cons
 /* bias update from per-row-tile column partials db_part[parts][ld] (fixed summation order). */
 int ocf_bias_opt_from_partials(float* b, const float* db_part, int parts, int64_t ld, int n, float* s1, float* s2,
                                float* g_out, const OcfOptParams* opt, void* stream);
+
+/* ocf_sumsq -- out[0] += scale * sum(x[i]^2) over n elements (fixed summation order; ws: scratch of
+ * 1,024 floats).  The l2 kernel-regulariser term Keras adds to the logged loss
+ * (/root/reference/model.py:66,82 W_regularizer=l2(l2_weight_regulatization)). */
+int ocf_sumsq(const float* x, int64_t n, float scale, float* ws, float* out, void* stream);
 
 /* reduce OCF_EPI_MASKED_MSE partials to out[4 + M] = {sse, sae, nnz(T+yhat), 0, row_sse[M]}. */
 int ocf_stats_finalize(const float* stats_part, int n_parts, const float* row_sse_part, int n_tiles, int M,

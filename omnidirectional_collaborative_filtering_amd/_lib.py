@@ -110,7 +110,6 @@ class OcfTileBucketArgs(ctypes.Structure):
 # every symbol include/ocf.h declares, with its ctypes signature
 SIGNATURES = {
     "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
-    "ocf_scatter_clear": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
     "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P]),
     "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
@@ -119,6 +118,7 @@ SIGNATURES = {
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),
     "ocf_bias_opt_from_partials": (I32, [P, P, I32, I64, I32, P, P, P, ctypes.POINTER(OcfOptParams), P]),
     "ocf_stats_finalize": (I32, [P, I32, P, I32, I32, P, P]),
+    "ocf_sumsq": (I32, [P, I64, F32, P, P, P]),
     "ocf_gather_encoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
     "ocf_gather_decoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
     "ocf_rows_reduce": (I32, [ctypes.POINTER(OcfRowsReduceArgs), P]),

@@ -88,15 +88,7 @@ __device__ __forceinline__ uint4 philox4(uint4 c, uint2 k) {
   }
   return c;
 }
-// uniform in [0,1) with 24 random bits
-// ---- write-through streaming stores -----------------------------------------------------
-// 16-B stores with the sc1 cache policy leave nothing dirty in the XCD's L2, so the kernel-end
-// writeback of a streaming kernel's output (~L2 size / 6 TB/s per boundary) disappears.  The
-// descriptor must be built from a wave-uniform base; byte offsets stay below 2^31.  Measured
-// neutral on the ML-20M step (within run-to-run noise), so plain stores are the default.
-#ifndef OCF_WT
-#define OCF_WT 0
-#endif
+// ---- cache-policy loads / stores through buffer descriptors ----------------------------
 typedef unsigned int ocf_u4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -128,20 +120,7 @@ __device__ __forceinline__ float4 ld_pol16(__amdgpu_buffer_rsrc_t r, const void*
     return f;
   }
 }
-template <typename T16>
-__device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, void* base, uint32_t byte_off, const T16& v) {
-  static_assert(sizeof(T16) == 16, "16-byte store");
-#if OCF_WT
-  (void)base;
-  ocf_u4 u;
-  __builtin_memcpy(&u, &v, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(u, r, byte_off, 0, 16 /* sc1 */);
-#else
-  (void)r;
-  *reinterpret_cast<T16*>(reinterpret_cast<char*>(base) + byte_off) = v;
-#endif
-}
-
+// uniform in [0,1) with 24 random bits
 __device__ __forceinline__ float philox_uniform(uint64_t seed, uint64_t stream, uint64_t idx) {
   uint4 c = make_uint4((uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)stream, (uint32_t)(stream >> 32));
   uint4 r = philox4(c, make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));

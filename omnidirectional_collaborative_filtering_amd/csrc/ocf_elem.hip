@@ -126,9 +126,47 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(const float* sp, in
   if (lane == 0) out[4 + m] = r;
 }
 
+// sum of squares, two passes with a fixed order: 1,024 block partials (block b: elements b*256 + i,
+// strided by the grid, a fixed LDS tree), then one block adds them in order and accumulates
+// scale * sum into out[0] (the l2 penalty of Keras' W_regularizer, model.py:66,82)
+constexpr int SUMSQ_BLOCKS = 1024;
+__global__ void __launch_bounds__(256) sumsq_partials_kernel(const float* x, int64_t n, float* ws) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)SUMSQ_BLOCKS * 256) a += x[i] * x[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[blockIdx.x] = red[0];
+}
+__global__ void __launch_bounds__(256) sumsq_final_kernel(const float* ws, float scale, float* out) {
+  __shared__ float red[256];
+  float a = 0.f;
+  for (int i = threadIdx.x; i < SUMSQ_BLOCKS; i += 256) a += ws[i];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] += scale * red[0];
+}
+
 }  // namespace ocf
 
 using namespace ocf;
+
+extern "C" int ocf_sumsq(const float* x, int64_t n, float scale, float* ws, float* out, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(x && ws && out, "ocf_sumsq: null pointer");
+  hipLaunchKernelGGL(sumsq_partials_kernel, dim3(SUMSQ_BLOCKS), dim3(256), 0, (hipStream_t)stream, x, n, ws);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, ws, scale, out);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
 
 extern "C" int ocf_version(void) { return 1; }
 extern "C" const char* ocf_last_error(void) { return g_last_error.c_str(); }

@@ -9,19 +9,6 @@ struct NoPre {};
 // two K-steps of operand loads in flight (gemm_kernel DEEP), per epilogue family.  Off by default:
 // measured neutral on the ML-20M shapes (the K-loop is issue-bound, not latency-bound) and it costs
 // occupancy where the epilogue is register-heavy.
-#ifndef OCF_DEEP_SLAB
-#define OCF_DEEP_SLAB false
-#endif
-#ifndef OCF_DEEP_MSE
-#define OCF_DEEP_MSE false
-#endif
-#ifndef OCF_DEEP_OPTIM   // generic OPTIM kernel: with the output-bias column sums the two register sets drop it to
-                         // one workgroup per CU (8-way rank step 0.42 vs 0.37 ms), so off
-#define OCF_DEEP_OPTIM false
-#endif
-#ifndef OCF_DEEP_OTHER
-#define OCF_DEEP_OTHER false
-#endif
 #define OCF_NO_PROLOGUE                                                                            \
   using Pre = NoPre;                                                                             \
   template <class P>                                                                             \
@@ -77,7 +64,6 @@ __device__ __forceinline__ void opt_update(const OcfOptParams& o, float g, float
 
 // ---- split-K partial slab: out[split][m][n] --------------------------------------------
 struct EpiSlab {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_SLAB;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
@@ -132,7 +118,6 @@ __device__ __forceinline__ void bias_act_store(const BiasActParams& p, int m, in
 }
 
 struct EpiBiasAct {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   using Params = BiasActParams;
@@ -176,7 +161,6 @@ __device__ __forceinline__ void store_ct(void* out, int dtype, int64_t idx, floa
 }
 
 struct EpiGradAct {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 2 * GT_BN * 4;
   using Params = GradActParams;
@@ -214,16 +198,21 @@ struct EpiGradAct {
 
 // ---- raw gradient store (data-parallel path: all-reduce before the optimizer) ------------
 struct EpiGradStore {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
     float* g;
     int64_t ld;
     float gscale;
+    int bf16;   // 1: the gradient in bf16 (data parallel: half the bytes of the reduce-scatter)
   };
   __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&, const Pre&) {
-    for_each_acc(acc, c, [&](int m, int n, float v) { p.g[(int64_t)m * p.ld + n] = v * p.gscale; });
+    if (p.bf16) {
+      __bf16* g = reinterpret_cast<__bf16*>(p.g);
+      for_each_acc(acc, c, [&](int m, int n, float v) { g[(int64_t)m * p.ld + n] = (__bf16)(v * p.gscale); });
+    } else {
+      for_each_acc(acc, c, [&](int m, int n, float v) { p.g[(int64_t)m * p.ld + n] = v * p.gscale; });
+    }
   }
 };
 
@@ -234,9 +223,6 @@ struct EpiGradStore {
 // writes them back.  This is the HBM-bound part of the step (16 B/param for Adagrad).
 #ifndef OCF_OPT_U
 #define OCF_OPT_U 4
-#endif
-#ifndef OCF_OPT_PRE
-#define OCF_OPT_PRE 0
 #endif
 // cache policy of the optimizer's parameter / slot streams (0 plain, 2 nt, 16 sc1).  nt on both
 // keeps the fp32 master weights and slots (4 x P bytes, read and written once per step) from
@@ -249,7 +235,6 @@ struct EpiGradStore {
 #define OCF_OPT_LD_POL 2
 #endif
 struct EpiOptim {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_OPTIM;
   static constexpr int YS = GT_BN + 4;
   static constexpr int LDS_NEED = GT_BM * YS * 4;
   static constexpr int CH = GT_BM * (GT_BN / 4) / GT_THREADS;   // 16 chunks of 4 per thread
@@ -267,13 +252,7 @@ struct EpiOptim {
     // listed have a zero gradient and an identity update (Adagrad, l2 = 0); their traffic is skipped
     const uint8_t* row_live = nullptr;
   };
-  // the parameter / slot values of the first chunk group do not depend on the product: with
-  // OCF_OPT_PRE they are loaded before the K-loop
-  struct Pre {
-#if OCF_OPT_PRE
-    float4 pv[U], av[U], bv[U];
-#endif
-  };
+  struct Pre {};
   __device__ static int64_t chunk_off(const Params& p, int m0, int n0, int tid, int g, int u, int& ml, int& c4) {
     const int ch = tid + (g + u) * GT_THREADS;
     ml = ch >> 5;
@@ -292,13 +271,7 @@ struct EpiOptim {
       bv[u] = p.s2 ? ld_pol16<OCF_OPT_LD_POL>(r2, p.s2, (uint32_t)(off * 4)) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  __device__ static Pre prologue(const Params& p, int, int, int m0, int n0, int tid, const GemmShape&) {
-    Pre q;
-#if OCF_OPT_PRE
-    load_group(p, m0, n0, tid, 0, q.pv, q.av, q.bv);
-#endif
-    return q;
-  }
+  __device__ static Pre prologue(const Params&, int, int, int, int, int, const GemmShape&) { return Pre{}; }
   __device__ static void store_shadow(const Params& p, int row, int col, const float4& v) {
     const int64_t off = p.shadow_blocked
                             ? (((int64_t)(row >> 6) * (p.ld >> 6) + (col >> 6)) << 12) + (row & 63) * 64 + (col & 63)
@@ -314,7 +287,7 @@ struct EpiOptim {
     *reinterpret_cast<uint2*>(reinterpret_cast<char*>(p.shadow) + off * 2) = u;
   }
   __device__ static void apply(const Params& p, ocf_f16v (&acc)[2][2], const TileCtx& c, const GemmShape&,
-                               const Pre& q) {
+                               const Pre&) {
     float* Y = reinterpret_cast<float*>(c.lds);
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
@@ -331,16 +304,7 @@ struct EpiOptim {
       float4 pv[U], av[U], bv[U], gv[U];
       int64_t off[U];
       int rw[U], cl[U];
-#if OCF_OPT_PRE
-      if (g == 0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) { pv[u] = q.pv[u]; av[u] = q.av[u]; bv[u] = q.bv[u]; }
-      } else {
-        load_group(p, c.m0, c.n0, c.tid, g, pv, av, bv);
-      }
-#else
       load_group(p, c.m0, c.n0, c.tid, g, pv, av, bv);
-#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         int ml, c4;
@@ -366,7 +330,6 @@ struct EpiOptim {
 
 // ---- predict: y = mask * (acc + b) (model.py:82-86) -------------------------------------
 struct EpiPredict {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_OTHER;
   OCF_NO_PROLOGUE
   static constexpr int LDS_NEED = 0;
   struct Params {
@@ -397,7 +360,6 @@ struct EpiPredict {
 // GEMMs, its column sums give the output-bias gradient, and SSE / SAE / count_nonzero(T+yhat)
 // / per-row SSE feed the loss and the train.py metrics.
 struct EpiMaskedMSE {
-  static constexpr bool DEEP_PIPE = OCF_DEEP_MSE;
   static constexpr int YS = GT_BN + 4;   // LDS row stride (floats) of the staged tile
   static constexpr int NPRE = 2;         // bucket entries per thread loaded in the prologue
   static constexpr int LDS_NEED = GT_BM * YS * 4 + GT_BM * 4 * 4 + GT_BM * 4 + 4 * GT_BN * 4 + 3 * 4 * 4;
@@ -573,20 +535,20 @@ struct EpiMaskedMSE {
         }
         int64_t off = (int64_t)(c.m0 + ml) * p.ld_d + c.n0 + c8;
         if (p.d_dtype == OCF_F32) {
-          st_wt16(rd, p.d_out, (uint32_t)(off * 4), make_float4(v[0], v[1], v[2], v[3]));
-          st_wt16(rd, p.d_out, (uint32_t)(off * 4 + 16), make_float4(v[4], v[5], v[6], v[7]));
+          st_pol16<0>(rd, p.d_out, (uint32_t)(off * 4), make_float4(v[0], v[1], v[2], v[3]));
+          st_pol16<0>(rd, p.d_out, (uint32_t)(off * 4 + 16), make_float4(v[4], v[5], v[6], v[7]));
         } else if (p.d_dtype == OCF_F16) {
           _Float16 h[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = (_Float16)v[j];
           uint4 u; __builtin_memcpy(&u, h, 16);
-          st_wt16(rd, p.d_out, (uint32_t)(off * 2), u);
+          st_pol16<0>(rd, p.d_out, (uint32_t)(off * 2), u);
         } else {
           __bf16 h[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) h[j] = (__bf16)v[j];
           uint4 u; __builtin_memcpy(&u, h, 16);
-          st_wt16(rd, p.d_out, (uint32_t)(off * 2), u);
+          st_pol16<0>(rd, p.d_out, (uint32_t)(off * 2), u);
         }
       }
       if (p.db_part) {

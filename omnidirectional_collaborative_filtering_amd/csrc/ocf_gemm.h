@@ -409,11 +409,6 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
   char* buf0 = lds;
   char* buf1 = lds + Cfg::BUF;
 
-  // Two K-steps of operand loads in flight (two register sets used in turn, the loop unrolled by
-  // two so neither set is ever copied and every wait the compiler inserts covers exactly the set
-  // about to be written to LDS); only for 16-bit operands, where two sets fit the register budget
-  // of two workgroups per CU.
-  constexpr bool DEEP = !SPA && Epi::DEEP_PIPE && sizeof(CT) == 2 && sizeof(AGT) == 2 && sizeof(BGT) == 2;
   // output-column sums of a [K][M] A for the tile_n == 0 workgroups (the output-bias gradient), in
   // fixed k order, from each K-step's A image once it is in LDS
   const bool colsum = ACOL && sh.sp_colsum && tile_n == 0;
@@ -423,68 +418,7 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
       if (colsum && tid < GT_BM) csum += colsum_kstep<CT, BK>(img, Img<CT, GT_BM, true>::STRIDE, tid);
     }
   };
-  if constexpr (DEEP) {
-    Stager<AGT, CT, GT_BM, ACOL> sa0, sa1;
-    Stager<BGT, CT, GT_BN, BCOL> sb0, sb1;
-    // the scheduling barrier keeps the compiler from sinking a set's loads below the other set's
-    // LDS writes (which would drain the older set before the younger one is issued)
-    const uint32_t sta = decltype(sa0)::step_bytes(sh.lda, false), stb = decltype(sb0)::step_bytes(sh.ldb, bblk);
-    auto ld0 = [&](int kt) {
-      sa0.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
-      sb0.load(rb, sh.ldb, kt * stb, tid, sh.b_nt, bblk);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto ld1 = [&](int kt) {
-      sa1.load(ra, sh.lda, kt * sta, tid, sh.a_nt);
-      sb1.load(rb, sh.ldb, kt * stb, tid, sh.b_nt, bblk);
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    auto st0 = [&](char* b) { sa0.store(b, tid); sb0.store(b + Cfg::ImgA::BYTES, tid); };
-    auto st1 = [&](char* b) { sa1.store(b, tid); sb1.store(b + Cfg::ImgA::BYTES, tid); };
-    if (nk > 0) {
-      ld0(0);
-      if (nk > 1) ld1(1);
-      st0(buf0);
-      __syncthreads();
-      sum_a(buf0);
-      int kt = 0;
-      // steady state: buf0 holds step kt, set 1 carries step kt+1
-      for (; kt + 3 < nk; kt += 2) {
-        ld0(kt + 2);
-        compute(buf0);
-        st1(buf1);
-        __syncthreads();
-        sum_a(buf1);
-        ld1(kt + 3);
-        compute(buf1);
-        st0(buf0);
-        __syncthreads();
-        sum_a(buf0);
-      }
-      const int rem = nk - kt;   // 1, 2 or 3 steps left
-      if (rem == 3) {
-        ld0(kt + 2);
-        compute(buf0);
-        st1(buf1);
-        __syncthreads();
-        sum_a(buf1);
-        compute(buf1);
-        st0(buf0);
-        __syncthreads();
-        sum_a(buf0);
-        compute(buf0);
-      } else if (rem == 2) {
-        compute(buf0);
-        st1(buf1);
-        __syncthreads();
-        sum_a(buf1);
-        compute(buf1);
-      } else {
-        compute(buf0);
-      }
-      __syncthreads();
-    }
-  } else {
+  {
     Stager<AGT, CT, GT_BM, ACOL> sa;
     Stager<BGT, CT, GT_BN, BCOL> sb;
     const uint32_t sta = decltype(sa)::step_bytes(sh.lda, false), stb = decltype(sb)::step_bytes(sh.ldb, bblk);
@@ -504,16 +438,13 @@ gemm_kernel(GemmShape sh, typename Epi::Params ep) {
       __syncthreads();
       sum_a(buf0);
     }
-#ifndef OCF_KLOOP_EXP
-#define OCF_KLOOP_EXP 0   // diagnostics only: 1 = no operand traffic in the loop, 2 = no MFMA
-#endif
     for (int kt = 0; kt < nk; ++kt) {
-      const bool more = kt + 1 < nk && OCF_KLOOP_EXP != 1;
+      const bool more = kt + 1 < nk;
       if (more) {
         if constexpr (!SPA) sa.load(ra, sh.lda, (kt + 1) * sta, tid, sh.a_nt);
         sb.load(rb, sh.ldb, (kt + 1) * stb, tid, sh.b_nt, bblk);
       }
-      if (OCF_KLOOP_EXP != 2) compute((kt & 1) ? buf1 : buf0);
+      compute((kt & 1) ? buf1 : buf0);
       if (more) {
         char* nb = ((kt + 1) & 1) ? buf1 : buf0;
         if constexpr (SPA) fill_a(nb, kt + 1);

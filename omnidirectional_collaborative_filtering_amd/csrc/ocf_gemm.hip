@@ -278,7 +278,8 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
       break;
     case OCF_EPI_GRAD:
       if constexpr (!FP32_W || std::is_same<CT, float>::value) if constexpr (BCOL) {
-        EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale};
+        OCF_CHECK(g.h_dtype == OCF_F32 || g.h_dtype == OCF_BF16, "ocf_gemm GRAD: fp32 or bf16 gradient output");
+        EpiGradStore::Params p{g.out, g.ld_out, g.opt.gscale, g.h_dtype == OCF_BF16 ? 1 : 0};
         if constexpr (ACOL) {
           if (g.a_sparse) {
             launch<CT, ACOL, BCOL, CT, EpiGradStore, true>(g, p, s);

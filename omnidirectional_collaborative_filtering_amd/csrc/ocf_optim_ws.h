@@ -433,11 +433,7 @@ optim_ws_kernel(GemmShape sh, EpiOptim::Params ep, WsJobs jobs) {
       const int kt = q % nk;
       int m0, n0;
       tile_of(q, m0, n0);
-#ifdef OCF_WS_DIAG_NOCOLSUM
-      const bool colsum = false;   // diagnostics only (wrong bias gradient): the cost of the column sums
-#else
       const bool colsum = sh.sp_colsum && n0 == 0 && wn == 0;
-#endif
       if (kt == 0) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)

@@ -145,23 +145,6 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a,
   }
 }
 
-// sparse clear of a previous batch's xin entries (all blocks of every entry's column)
-__global__ void __launch_bounds__(SC_THREADS) clear_flat_kernel(ScatterArgs a, int nblk1) {
-  extern __shared__ int64_t sh_off[];
-  const bool src2 = (int)blockIdx.x >= nblk1;
-  const int64_t* lboff = src2 ? a.lboff2 : (a.lboff1 ? a.lboff1 : a.boff1);
-  const int B = a.B;
-  for (int i = threadIdx.x; i <= B; i += SC_THREADS) sh_off[i] = lboff[i];
-  __syncthreads();
-  const int64_t e = (int64_t)(src2 ? (int)blockIdx.x - nblk1 : (int)blockIdx.x) * SC_THREADS + threadIdx.x;
-  if (e >= (src2 ? a.E2 : a.E1)) return;
-  const int b = find_row(sh_off, B, e);
-  const int64_t j = e - sh_off[b];
-  const int c = src2 ? a.col2[a.rp2[a.rows2[b]] + j] : a.col1[a.rp1[a.rows1[b]] + j];
-  const int nblk = 1 + ((a.feed == 1 || a.feed == 2) ? 1 : 0) + (a.both ? 1 : 0);
-  const int64_t ox = (int64_t)b * a.xin_ld + c;
-  for (int k = 0; k < nblk; ++k) store_val(a.xin, a.xin_dtype, ox + k * a.xin_block, 0.f);
-}
 
 // exclusive scan of per-tile target counts -> bucket pointers; resets counts for next batch
 __global__ void __launch_bounds__(1024) bucket_scan_kernel(int* tile_cnt, int* bk_ptr, int* bk_cur, int n_tiles) {
@@ -314,22 +297,6 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   OCF_TRY_END
 }
 
-extern "C" int ocf_scatter_clear(const ScatterArgs* args, void* stream) {
-  OCF_TRY_BEGIN
-  const ScatterArgs& a = *args;
-  hipStream_t s = (hipStream_t)stream;
-  if (!a.xin || a.B == 0) return 0;
-  OCF_CHECK(a.B <= 16384, "ocf_scatter_clear: B too large for the LDS offset table");
-  OCF_CHECK(a.E2 == 0 || (a.rows2 && a.lboff2), "ocf_scatter_clear: source 2 needs rows2 / lboff2");
-  OCF_CHECK(a.E1 == 0 || (a.rows1 && (a.lboff1 || a.boff1)), "ocf_scatter_clear: source 1 needs rows1 / offsets");
-  const int nblk1 = (int)((a.E1 + SC_THREADS - 1) / SC_THREADS);
-  const int nblk2 = (int)((a.E2 + SC_THREADS - 1) / SC_THREADS);
-  if (nblk1 + nblk2 > 0)
-    hipLaunchKernelGGL(clear_flat_kernel, dim3(nblk1 + nblk2), dim3(SC_THREADS), (size_t)(a.B + 1) * sizeof(int64_t), s,
-                       a, nblk1);
-  OCF_HIP(hipGetLastError());
-  OCF_TRY_END
-}
 
 extern "C" int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,
                                  int* bk_ptr, int* bk_cur, int* bk_rc, float* bk_t, float* bk_m, void* stream) {

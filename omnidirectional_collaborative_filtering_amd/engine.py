@@ -87,6 +87,11 @@ class Engine:
         self.pad_dims = [self.k * self.Np] + self.Hp + [self.Np]
         self.n_tiles = self.Np // TILE
         self.step_count = 0
+        # row data parallelism (parallel.DataParallel): the rank is mixed into the dropout stream so the
+        # G local batches draw independent masks, like one global batch; grad_hook(i) is called once
+        # layer i's raw gradients are written (grads_out steps), so its exchange can start right away
+        self.dp_rank, self.dp_world = 0, 1
+        self.grad_hook = None
         self.opt = None
         self.slots = []
         self._alloc_params()
@@ -218,15 +223,8 @@ class Engine:
         self.bk_cap = 0
         self._grow_buckets(1 << 16)
         self.tflag = torch.zeros(1 << 16, device=d, dtype=torch.uint8)   # live-target flag per batch entry
-        # xin is zeroed once; afterwards each generator batch clears only the previous batch's entries
+        # xin (dense path) is cleared by the scatter's memset unless already clean
         self._xin_clean = True
-        self._xin_prev = None       # (OcfScatterArgs copy, owner keeping its device buffers alive)
-        # sparse clear (ocf_scatter_clear) instead of the dense memset: measured ~4% SLOWER per step on
-        # ML-20M -- the memset leaves xin resident in the Infinity Cache, so the encoder GEMM reads it
-        # on-die; after a sparse clear it streams from HBM.  Off by default.
-        self.sparse_clear = False
-        # non-temporal loads for operands at their last use in the step (A/B switch)
-        self.nt_operands = False   # measured neutral-to-worse: nt loads forfeit Infinity-Cache hits
         self.tseg = None            # row-segment target descriptor of the loaded batch (None: buckets)
         # row-gather (sparse batch) path: chunk tables of the loaded batch (None: dense GEMM path)
         self.gt = None
@@ -248,15 +246,9 @@ class Engine:
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
         self.split_dw_streams = True
-        self.split_dw_streams_1gpu = False   # the same for the single-GPU persistent dW kernels (A/B switch)
         # one hidden layer, one GPU: the decoder gather applies the hidden layer's epilogue to the encoder's
         # chunk partials (no separate row-reduce launch between the two gathers)
         self.fuse_enc_epilogue = True
-        # the per-batch tile buckets (ocf_sparse_tiles) on the side stream, overlapping the row gathers:
-        # measured neutral (ML-20M step 0.5052 vs 0.5056 ms, 4 interleaved runs; the fork/join events
-        # cost what the overlap saves), so off
-        self.async_tile_buckets = False
-        self._tb_forked = False
         self._enc_fused = None
         # row skipping (ocf.h OcfGemmArgs row_tag): the scatter tags the columns holding a live input /
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
@@ -379,10 +371,26 @@ class Engine:
             return
         cap = max(n, 2 * self.stats_cap)
         new = torch.zeros(cap, 4 + self.Bp, device=self.dev, dtype=torch.float32)
+        # l2 penalty per step: [cap][2] = (column-sharded kernels, replicated kernels)
+        pen = torch.zeros(cap, 2, device=self.dev, dtype=torch.float32)
         if self.stats_hist is not None and self.n_stats:
             new[: self.n_stats] = self.stats_hist[: self.n_stats]
+            pen[: self.n_stats] = self.pen_hist[: self.n_stats]
         self.stats_hist = new
+        self.pen_hist = pen
         self.stats_cap = cap
+
+    def _l2_penalty(self):
+        """Keras adds l2 * sum(W^2) of every kernel with a W_regularizer (all of them,
+        /root/reference/model.py:66,82) to the logged loss, at the weights the batch starts from.
+        Under feature parallelism the first and last kernels are column shards (summed over the
+        ranks in take_stats), the hidden ones replicas (counted once)."""
+        self._grow_stats(self.n_stats + 1)
+        ws = self._buf("sumsq_ws", 1024)
+        for i, w in enumerate(self.W):
+            sharded = self.comm is not None and i in (0, len(self.W) - 1)
+            dst = self.pen_hist[self.n_stats, 0 if sharded else 1:]
+            call("ocf_sumsq", ptr(w), w.numel(), self.l2, ptr(ws), ptr(dst), cur_stream())
 
     # ---------------------------------------------------------------- batch assembly
     def scatter_args(self):
@@ -406,7 +414,7 @@ class Engine:
         a.s0 = a.s1 = 1.0
         return a
 
-    def load_batch(self, a, targets, owner=None, gather=None):
+    def load_batch(self, a, targets, gather=None):
         """K1 scatter for a batch described by OcfScatterArgs (pointers filled by the caller).
 
         ``targets`` (BatchGenerator.targets) names the target CSR's tile index: the scatter marks
@@ -445,20 +453,9 @@ class Engine:
                 a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
             self.gt = dict(gather, xval=xval, aux=float(targets["t_aux"]), E=int(targets["E"]))
         with self.phase("scatter"):
-            if self._xin_prev is not None:
-                call("ocf_scatter_clear", self._xin_prev[0], cur_stream())
-                self._xin_clean = True
             a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
-            if a.tb_cnt and self.side is not None and self.async_tile_buckets:
-                # only the weight-gradient kernels read the buckets: build them beside the gathers
-                self._fork()
-                self._tb_forked = True
-                with torch.cuda.stream(self.side):
-                    self.tb = self._tile_buckets()
-            else:
-                self.tb = self._tile_buckets() if a.tb_cnt else None
-        self._xin_prev = (type(a).from_buffer_copy(a), owner) if self.sparse_clear else None
+            self.tb = self._tile_buckets() if a.tb_cnt else None
         self._xin_clean = False
 
     def _tile_buckets(self):
@@ -509,7 +506,7 @@ class Engine:
         s = cur_stream()
         call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
              self.Bp, s)
-        self._xin_prev, self._xin_clean = None, False      # xin written densely
+        self._xin_clean = False      # xin written densely
         self._grow_buckets(B * N)
         self.tb = None
         self.tseg = None
@@ -547,7 +544,7 @@ class Engine:
         s = cur_stream()
         Bp, L = self.Bp, len(self.H)
         keep = self.keep if training else 1.0
-        stream_id = (self.step_count * 16) if training else 0
+        stream_id = ((self.step_count * self.dp_world + self.dp_rank) * 16) if training else 0
         # layer 0: split-K over the (k x Np)-wide input
         Hp0 = self.Hp[0]
         sstride = Bp * Hp0
@@ -557,7 +554,7 @@ class Engine:
             with self.phase("enc_gemm"):
                 self._gemm(self.xin, 0, self.pad_dims[0], *self._wop(0), 1, Hp0, Bp, Hp0, self.pad_dims[0],
                            _lib.EPI_SLAB, splits=self.splits0, out=self.slabs, ld_out=Hp0, split_stride=sstride,
-                           b_nt=int(self.nt_operands), b_blocked=self._wblk(0))
+                           b_blocked=self._wblk(0))
         src, nsplit = self.slabs, self.splits0
         if self.gt is not None and self.comm is None:
             pass                      # fused bias/activation/dropout already applied by the row reduce
@@ -734,7 +731,7 @@ class Engine:
         with self.phase("dec_bwd_gemm"):
             self._gemm(self.d_out, 0, self.Np, *self._wop(L), 1, HpL, Bp, HpL, self.Np, _lib.EPI_SLAB,
                        splits=self.splitsL, out=self.slabs, ld_out=HpL, split_stride=sstride,
-                       b_nt=int(self.nt_operands), b_blocked=self._wblk(L))
+                       b_blocked=self._wblk(L))
         db_last = self.db_h[L - 1]
         src, nsplit = self.slabs, self.splitsL
         if fused and L == 1 and self.comm is None and self.side is not None:
@@ -767,6 +764,7 @@ class Engine:
         self._bias_update(L, self.db_out_part, Bp // TILE, self.Np, self.Np, grads_out, op)
         with self.phase("dW_out"):
             self._weight_update(L, self.d_out, self.Np, self.h[L - 1], HpL, self.Np, HpL, gscale, grads_out, op)
+        self._grad_ready(L, grads_out)
         parts_last = Bp // 4
         for i in range(L - 1, 0, -1):
             # delta of hidden layer i-1 through W_i (before W_i changes)
@@ -778,11 +776,13 @@ class Engine:
             self._bias_update(i, self.db_h[i], parts_last, self.Hp[i], self.Hp[i], grads_out, op)
             self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
                                 self.Hp[i], gscale, grads_out, op)
+            self._grad_ready(i, grads_out)
             parts_last = Bp // TILE
         self._bias_update(0, self.db_h[0], parts_last, self.Hp[0], self.Hp[0], grads_out, op)
         with self.phase("dW_in"):
             self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0],
                                 self.Hp[0], gscale, grads_out, op)
+        self._grad_ready(0, grads_out)
         if fused:
             self.opt.iterations += 1
 
@@ -810,15 +810,13 @@ class Engine:
                        ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
         else:
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
-                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), **sp)
+                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), h_dtype=self._grad_dt(grads_out[2 * i]),
+                       **sp)
 
     def _backward_gather(self, grads_out, op, gscale):
         """backward after the row-gather decoder: the last hidden delta already exists (single GPU) or
         its partial sum does (feature parallel: all-reduce, then activation/dropout)"""
         s = cur_stream()
-        if self._tb_forked:           # the tile buckets were built on the side stream
-            self._join()
-            self._tb_forked = False
         L, Bp = len(self.H), self.Bp
         HpL = self.Hp[L - 1]
         fused = grads_out is None
@@ -872,18 +870,9 @@ class Engine:
                 sp, n_sp, rs, n_rs, M, dst = self._stats_pending
                 jobs.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
                 self._stats_pending = None
-            if self.side is not None and self.split_dw_streams_1gpu:
-                # the two persistent dW kernels on two streams: the second one's workgroups take the CUs
-                # the first one's last tiles leave idle
-                self._fork()
-                with torch.cuda.stream(self.side):
-                    with self.phase("dW_out"):
-                        self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op,
-                                                   self.db_out_col, jobs=jobs)
-            else:
-                with self.phase("dW_out"):
-                    self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
-                                               jobs=jobs)
+            with self.phase("dW_out"):
+                self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
+                                           jobs=jobs)
             with self.phase("dW_in"):
                 self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
             self.opt.iterations += 1
@@ -907,6 +896,7 @@ class Engine:
                 self._weight_update_sparse(L, delta, self.h[L - 1], HpL, HpL, gscale, grads_out, op,
                                            self.db_out_col)
             self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
+        self._grad_ready(L, grads_out)
         for i in range(L - 1, 0, -1):
             self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
                        self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
@@ -916,10 +906,12 @@ class Engine:
             self._bias_update(i, db_last, parts_last, self.Hp[i], self.Hp[i], grads_out, op)
             self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
                                 self.Hp[i], gscale, grads_out, op)
+            self._grad_ready(i, grads_out)
             db_last, parts_last = self.db_h[i - 1], Bp // TILE
         self._bias_update(0, db_last, parts_last, self.Hp[0], self.Hp[0], grads_out, op)
         with self.phase("dW_in"):
             self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
+        self._grad_ready(0, grads_out)
         if fused:
             self.opt.iterations += 1
 
@@ -943,11 +935,22 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o, p_shadow=self.Wsh[i], a_nt=int(self.nt_operands and i in (0, len(self.W) - 1)),
-                       shadow_blocked=self._wblk(i))
+                       ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i))
         else:
             self._gemm(A, 1, lda, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
-                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale))
+                       opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), h_dtype=self._grad_dt(grads_out[2 * i]))
+
+    @staticmethod
+    def _grad_dt(g):
+        if g.dtype == torch.bfloat16:
+            return _lib.DT_BF16
+        if g.dtype != torch.float32:
+            raise ValueError("weight gradients are written in fp32 or bf16")
+        return _lib.DT_F32
+
+    def _grad_ready(self, i, grads_out):
+        if grads_out is not None and self.grad_hook is not None:
+            self.grad_hook(i)
 
     def apply_grads(self, grads, scale=1.0):
         """Elementwise optimizer over all parameters (after a data-parallel all-reduce)."""
@@ -971,6 +974,8 @@ class Engine:
 
     # ---------------------------------------------------------------- steps
     def train_step(self, grads_out=None):
+        if self.l2:
+            self._l2_penalty()
         self.forward(training=True)
         self.output_loss(with_grad=True)
         self.backward_update(grads_out)
@@ -978,6 +983,8 @@ class Engine:
         self.step_count += 1
 
     def eval_step(self):
+        if self.l2:
+            self._l2_penalty()     # Keras' test loss includes the regularisers too
         self.forward(training=False)
         self.output_loss(with_grad=False)
         self._join()
@@ -986,9 +993,16 @@ class Engine:
         """host copy of the per-step stats recorded since the last call: [steps, 4 + Bp]."""
         self._flush_stats()
         st = self.stats_hist[: self.n_stats]
+        pen = self.pen_hist[: self.n_stats]
         if self.comm is not None and self.n_stats:
             st = st.clone()
             self.comm(st)          # SSE / SAE / counts / row SSE are sums over the column shards
+            sh = pen[:, 0].clone()
+            self.comm(sh)
+            pen = torch.stack([sh, pen[:, 1]], 1)
         out = st.cpu().numpy().astype(np.float64)
+        # column 3 (0 from the loss epilogues) carries the step's l2 penalty
+        out[:, 3] = pen.double().sum(1).cpu().numpy()
+        self.pen_hist[: self.n_stats].zero_()
         self.n_stats = 0
         return out

@@ -55,17 +55,25 @@ class Model(object):
         self.metric_names = []
         self.rating_range = float(rating_range)
         self.stop_training = False
-        self.rank, self.world, self.bucket = 0, 1, None
+        self.rank, self.world, self.dp = 0, 1, None
+        # feature parallelism (engine built with shard / comm): (rank, world) for per-shard checkpoints
+        self.fp = None
 
-    def enable_data_parallel(self, rank, world):
-        """Row data parallelism (parallel.py): call after torch.distributed is initialised."""
-        from .parallel import GradBucket
+    def enable_data_parallel(self, rank, world, mode="sharded", grad_dtype="float32"):
+        """Row data parallelism (parallel.DataParallel): call on every rank after torch.distributed is
+        initialised and the model is compiled; rank 0's weights are broadcast."""
+        from .parallel import DataParallel
+        if self.engine.comm is not None:
+            raise ValueError("data parallelism over a feature-parallel (column-sharded) engine is not supported")
         self.rank, self.world = int(rank), int(world)
-        self.bucket = GradBucket(self.engine) if world > 1 else None
+        self.dp = DataParallel(self.engine, rank, world, mode=mode, grad_dtype=grad_dtype) if world > 1 else None
+
+    def enable_feature_parallel(self, rank, world):
+        """record the column-shard layout (the engine was built with shard=/comm=) for checkpoints"""
+        self.fp = (int(rank), int(world))
 
     def _train_one(self, gen):
         """One optimizer step; under data parallelism rank r takes the r-th of the next `world` batches."""
-        from .parallel import dp_train_step
         if self.world > 1 and isinstance(gen, BatchGenerator):
             idx = [gen.next_batch_index() for _ in range(self.world)]
             if idx[-1] is None:
@@ -74,7 +82,10 @@ class Model(object):
             self._load(None, gen, idx[self.rank])
         else:
             self._pull(gen)
-        dp_train_step(self.engine, self.bucket, self.world)
+        if self.dp is not None:
+            self.dp.step()
+        else:
+            self.engine.train_step()
 
     # ------------------------------------------------------------------ compile
     def compile(self, optimizer, loss="mean_squared_error", metrics=None, rating_range=None):
@@ -97,7 +108,8 @@ class Model(object):
         out = {k: [] for k in self.metrics_names}
         for row in st:
             sse, sae, cnt = row[0], row[1], row[2]
-            out["loss"].append(sse / (B * e.N_total))
+            # Keras' total loss = MSE + the kernels' l2 penalty (row[3], 0 without l2); metrics have none
+            out["loss"].append(sse / (B * e.N_total) + row[3])
             for name in self.metric_names:
                 out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N_total, self.rating_range))
         return {k: float(np.mean(v)) if v else float("nan") for k, v in out.items()}
@@ -122,7 +134,7 @@ class Model(object):
         e = self.engine
         if gen is not None:
             args = gen.scatter_args(bi, engine_args=e.scatter_args())
-            e.load_batch(args, gen.targets(bi, e.N), owner=gen, gather=gen.gather_tables(bi))
+            e.load_batch(args, gen.targets(bi, e.N), gather=gen.gather_tables(bi))
             return gen.target_count(bi)
         x, y = item[0], item[1]
         blocks, out_mask = self._split_inputs(x)
@@ -284,10 +296,23 @@ class Model(object):
     def set_weights(self, weights):
         self.engine.set_weights(weights)
 
+    def shard_path(self, path):
+        """feature parallelism: every rank checkpoints its own column shard"""
+        if self.fp is None:
+            return path
+        return "%s.shard%dof%d" % (path, self.fp[0], self.fp[1])
+
     def save(self, path):
-        """Weights (Keras layout) + optimizer state in a safetensors file (replaces the h5 of train.py:169)."""
+        """Weights (Keras layout) + optimizer state in a safetensors file (replaces the h5 of train.py:169).
+        Collective under data parallelism (the sharded optimizer slots are gathered first; rank 0 writes)
+        and under feature parallelism (every rank writes its shard, Model.shard_path)."""
         from safetensors.numpy import save_file
         e = self.engine
+        if self.dp is not None:
+            self.dp.gather_slots()
+            if self.rank != 0:
+                return
+        path = self.shard_path(path)
         tensors = {}
         for i, w in enumerate(e.get_weights()):
             tensors["param/%d" % i] = np.ascontiguousarray(w)
@@ -304,7 +329,7 @@ class Model(object):
 
     def load(self, path, with_optimizer=True):
         from safetensors.numpy import load_file
-        t = load_file(path)
+        t = load_file(self.shard_path(path))
         n = len([k for k in t if k.startswith("param/")])
         self.set_weights([t["param/%d" % i] for i in range(n)])
         e = self.engine
@@ -317,6 +342,23 @@ class Model(object):
                     if s is not None:
                         s.copy_(torch.as_tensor(t["opt/b%d/%d" % (i, j)]))
             self.optimizer.iterations = int(t["opt/iterations"][0])
+
+
+class _Donor(object):
+    """weights of a saved model (Model.save safetensors) in the Keras order, for the transfer helpers"""
+
+    def __init__(self, weights):
+        self.weights = weights
+
+    def get_weights(self):
+        return self.weights
+
+
+def load_donor(path):
+    """the donor model of train.py:136-145 (keras.models.load_model there; a Model.save file here)"""
+    from safetensors.numpy import load_file
+    t = load_file(path)
+    return _Donor([t["param/%d" % i] for i in range(len([k for k in t if k.startswith("param/")]))])
 
 
 class omni_model(object):

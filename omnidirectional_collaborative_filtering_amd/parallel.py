@@ -1,11 +1,10 @@
-"""Row (user/item-batch) data parallelism over torch.distributed (backend 'nccl' = RCCL on ROCm).
+"""Multi-GPU layouts over torch.distributed (backend 'nccl' = RCCL on ROCm), one process per GPU.
 
-One process per GPU.  Rank r takes batches r, r+G, r+2G, ... of the shared epoch permutation, so
-G ranks process a global batch of G*B rows per step.  Keras' MSE is a mean over B*N, hence the
-gradient of the concatenated G*B-row batch is the AVERAGE of the G local gradients -- exactly
-what ``grad_sync`` computes (one flat fp32 bucket, one all-reduce), after which every rank
-applies the same elementwise optimizer (``Engine.apply_grads``) and the replicas stay identical.
-With G = 1 nothing here runs: the optimizer is fused into the weight-gradient GEMM epilogues.
+Row data parallelism (``DataParallel``): rank r takes batches r, r+G, r+2G, ... of the shared epoch
+permutation, so G ranks process a global batch of G*B rows per step.  Keras' MSE is a mean over B*N,
+hence the gradient of the concatenated G*B-row batch is the AVERAGE of the G local gradients; after
+the exchange every rank holds the same parameters.  With G = 1 nothing here runs: the optimizer is
+fused into the weight-gradient kernels.  Feature (column) parallelism: see the second half.
 """
 from __future__ import annotations
 
@@ -57,13 +56,189 @@ def grad_sync(bucket, world):
 
 
 def dp_train_step(engine, bucket, world):
-    """forward + backward (raw grads) -> all-reduce -> averaged optimizer step."""
+    """forward + backward (raw grads) -> all-reduce -> averaged optimizer step (mode 'allreduce')."""
     if world == 1:
         engine.train_step()
         return
     engine.train_step(grads_out=bucket.views)
     grad_sync(bucket, world)
     engine.apply_grads(bucket.views, scale=1.0 / world)
+
+
+def _staged(backend, t):
+    """gloo moves CUDA tensors through host copies for all_reduce only; the tensor collectives below
+    get explicit host staging there (rehearsals on one GPU), device tensors directly over RCCL"""
+    return backend == "gloo" and t.is_cuda
+
+
+class ShardedSync:
+    """Reduce-scatter / sharded update / all-gather of a list of parameter tensors (SURVEY 8(e)'s
+    data-parallel mitigations): for tensor j, rank r owns elements [r n/G, (r+1) n/G) of its flat view.
+      start(j)         : reduce-scatter of grads[j] (sum; fp32 or bf16) into this rank's shard buffer,
+                         asynchronous -- issued as soon as the engine has written that gradient, so the
+                         output layer's exchange overlaps the input layer's weight-gradient kernel;
+      finish(update)   : for every started tensor in order: wait, update(j, lo, hi, g_shard_fp32) (the
+                         optimizer on this rank's 1/G of the parameters and slots), then an asynchronous
+                         all-gather of the updated parameter shard into the full tensor; waits for all.
+    Traffic per step: (G-1)/G of the gradient bytes (bf16: half) + (G-1)/G of the fp32 parameters,
+    the same as one all-reduce, with the HBM-bound optimizer pass cut to 1/G per rank."""
+
+    def __init__(self, params, grads, rank, world, group=None):
+        self.params, self.grads = params, grads
+        self.rank, self.world, self.group = rank, world, group
+        self.backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
+        for p, g in zip(params, grads):
+            if p.numel() % world or (p.numel() // world) % 4:
+                raise ValueError("tensor of %d elements does not split into %d 16-B aligned shards" % (p.numel(), world))
+            if g.numel() != p.numel():
+                raise ValueError("gradient / parameter size mismatch")
+        self.shard = [torch.empty(g.numel() // world, dtype=g.dtype, device=g.device) for g in grads]
+        self.shard32 = [s if s.dtype == torch.float32 else torch.empty(s.numel(), device=s.device) for s in self.shard]
+        self._started = []
+
+    def bounds(self, j):
+        n = self.params[j].numel() // self.world
+        return self.rank * n, (self.rank + 1) * n
+
+    def start(self, j):
+        g = self.grads[j].view(-1)
+        out = self.shard[j]
+        if _staged(self.backend, g):
+            gh, oh = g.cpu(), torch.empty(out.numel(), dtype=out.dtype)
+            dist.reduce_scatter_tensor(oh, gh, op=dist.ReduceOp.SUM, group=self.group)
+            out.copy_(oh)
+            work = None
+        else:
+            work = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._started.append((j, work))
+
+    def finish(self, update):
+        gathers = []
+        for j, work in self._started:
+            if work is not None:
+                work.wait()
+            g32 = self.shard32[j]
+            if g32 is not self.shard[j]:
+                g32.copy_(self.shard[j])
+            lo, hi = self.bounds(j)
+            update(j, lo, hi, g32)
+            flat = self.params[j].view(-1)
+            mine = flat[lo:hi]
+            if _staged(self.backend, flat):
+                fh = torch.empty(flat.numel(), dtype=flat.dtype)
+                dist.all_gather_into_tensor(fh, mine.cpu(), group=self.group)
+                flat.copy_(fh)
+            else:
+                gathers.append(dist.all_gather_into_tensor(flat, mine, group=self.group, async_op=True))
+        for w in gathers:
+            w.wait()
+        self._started = []
+
+    def gather_tensors(self, tensors):
+        """all-gather every rank's shard of same-shaped companions of the parameters (optimizer slots,
+        before a checkpoint)"""
+        for j, t in enumerate(tensors):
+            if t is None:
+                continue
+            flat = t.view(-1)
+            lo, hi = self.bounds(j)
+            if _staged(self.backend, flat):
+                fh = torch.empty(flat.numel(), dtype=flat.dtype)
+                dist.all_gather_into_tensor(fh, flat[lo:hi].cpu(), group=self.group)
+                flat.copy_(fh)
+            else:
+                dist.all_gather_into_tensor(flat, flat[lo:hi].clone(), group=self.group)
+
+
+class DataParallel:
+    """Row (user/item-batch) data parallelism of one Engine replica per rank -- the north_star's
+    "user-batch data parallelism with RCCL gradient all-reduce", with SURVEY 8(e)'s mitigations.
+
+    mode 'sharded' (default): the engine writes raw per-layer gradients (EPI_GRAD; bf16 with
+      grad_dtype='bfloat16'); each layer's reduce-scatter starts as soon as that layer's gradient is
+      written (the output layer's overlaps the input layer's weight-gradient kernel); every rank updates
+      its 1/G of every parameter tensor and its slots (ocf_opt_step) and all-gathers the parameters.
+    mode 'allreduce': one flat fp32 bucket, one all-reduce, the full optimizer on every rank.
+    Both start from rank 0's weights (broadcast here), and the engine mixes the rank into the Philox
+    stream of its dropout masks so the G local batches draw independent masks like one global batch."""
+
+    def __init__(self, engine, rank, world, mode="sharded", grad_dtype="float32", group=None):
+        if mode not in ("sharded", "allreduce"):
+            raise ValueError("mode must be 'sharded' or 'allreduce'")
+        if grad_dtype not in ("float32", "bfloat16"):
+            raise ValueError("grad_dtype must be float32 or bfloat16")
+        if grad_dtype == "bfloat16" and mode != "sharded":
+            raise ValueError("bf16 gradients need mode='sharded'")
+        self.engine, self.rank, self.world, self.group = engine, int(rank), int(world), group
+        self.mode, self.grad_dtype = mode, grad_dtype
+        engine.dp_rank, engine.dp_world = self.rank, self.world
+        self.broadcast_params()
+        params = [t for w, b in zip(engine.W, engine.b) for t in (w, b)]
+        if mode == "allreduce":
+            self.bucket = GradBucket(engine)
+            self.views = self.bucket.views
+            self.sync = None
+        else:
+            gdt = torch.bfloat16 if grad_dtype == "bfloat16" else torch.float32
+            self.views = []
+            for w, b in zip(engine.W, engine.b):
+                self.views += [torch.zeros(w.shape, device=engine.dev, dtype=gdt),
+                               torch.zeros(b.shape, device=engine.dev, dtype=torch.float32)]
+            self.sync = ShardedSync(params, self.views, self.rank, self.world, group)
+
+    def broadcast_params(self):
+        e = self.engine
+        if self.world > 1:
+            for t in [x for w, b in zip(e.W, e.b) for x in (w, b)]:
+                if _staged(dist.get_backend(self.group), t):
+                    h = t.cpu()
+                    dist.broadcast(h, 0, group=self.group)
+                    t.copy_(h)
+                else:
+                    dist.broadcast(t, 0, group=self.group)
+        e._refresh_shadows()
+
+    def step(self):
+        e = self.engine
+        if self.mode == "allreduce":
+            e.train_step(grads_out=self.views)
+            grad_sync(self.bucket, self.world)
+            e.apply_grads(self.views, scale=1.0 / self.world)
+            return
+        sync = self.sync
+        e.grad_hook = lambda i: (sync.start(2 * i), sync.start(2 * i + 1))
+        try:
+            e.train_step(grads_out=self.views)
+        finally:
+            e.grad_hook = None
+        scale = 1.0 / self.world
+        opw = e.opt.step_params(scale, e.l2)     # l2 regularises kernels only
+        opb = e.opt.step_params(scale, 0.0)
+
+        def update(j, lo, hi, g):
+            i = j // 2
+            if not e.trainable[i]:
+                return
+            p = e.W[i] if j % 2 == 0 else e.b[i]
+            sw, sb = e.slots[i]
+            s = sw if j % 2 == 0 else sb
+            f = lambda t: None if t is None else t.view(-1)[lo:hi].data_ptr()
+            from . import _lib
+            _lib.call("ocf_opt_step", f(p), g.data_ptr(), f(s[0]), f(s[1]), hi - lo, opw if j % 2 == 0 else opb,
+                      torch.cuda.current_stream().cuda_stream)
+        sync.finish(update)
+        e._refresh_shadows()
+        e.opt.iterations += 1
+
+    def gather_slots(self):
+        """every rank's optimizer-slot shards -> full slots on every rank (sharded mode; before save)"""
+        if self.sync is None:
+            return
+        e = self.engine
+        for k in range(2):
+            ts = [t for sw, sb in e.slots for t in (sw[k], sb[k])]
+            if any(t is not None for t in ts):
+                self.sync.gather_tensors(ts)
 
 
 def shard_batches(num_batches, rank, world):

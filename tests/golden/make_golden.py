@@ -30,6 +30,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 TOY = os.path.join(HERE, "toy")
+TOY_U = os.path.join(HERE, "toy_u")     # the same ratings in the U-AutoRec orientation
 
 B = 8
 
@@ -92,7 +93,35 @@ def make_toy_dataset(path, n_rows=43, n_cols=29, density=0.35, seed=11):
             "rating_range": 4.5, "nonsequentialusers": True}
     with open(os.path.join(path, "metadata.json"), "w") as f:
         json.dump(meta, f)
-    return meta
+    # U orientation (reverse_user_item_data=False, data_reader.py:20-23,46-49): rows = users,
+    # columns = items in unique_items_list order (permuted: column order != raw-id order)
+    rng_u = np.random.RandomState(seed + 1)
+
+    def build_u(idx):
+        d = {}
+        for i in idx:
+            r, c, v = ratings[i]
+            d.setdefault(col_key(c), []).append([row_key(r), v])
+        return d
+    train_u, valid_u, test_u = build_u(tr), build_u(va), build_u(te)
+    test_in_u = build_u(np.concatenate([tr, va]))
+    items = sorted({row_key(r) for r, _, _ in ratings})
+    files_u = {
+        "ratingsByUser_dicts_train": train_u,
+        "ratingsByUser_dicts_valid": [{k: train_u.get(k) for k in valid_u}, valid_u],
+        "ratingsByUser_dicts_test": [{k: test_in_u.get(k) for k in test_u}, test_u],
+        "unique_items_list": [items[i] for i in rng_u.permutation(len(items))],
+        "unique_users_list": sorted({col_key(c) for _, c, _ in ratings}),
+    }
+    os.makedirs(TOY_U, exist_ok=True)
+    for k, v in files_u.items():
+        with open(os.path.join(TOY_U, k + ".json"), "w") as f:
+            json.dump(v, f)
+    meta_u = {"num_items": len(items), "num_users": len(files_u["unique_users_list"]), "rating_range": 4.5,
+              "nonsequentialusers": True}
+    with open(os.path.join(TOY_U, "metadata.json"), "w") as f:
+        json.dump(meta_u, f)
+    return meta, meta_u
 
 
 def import_reference():
@@ -105,11 +134,15 @@ def import_reference():
     return ref_dr
 
 
-def ref_reader(ref_dr, meta):
-    # train.py:71-76 swaps num_items/num_users for I-AutoRec
-    rd = ref_dr.data_reader(meta["num_users"], meta["num_items"], TOY + "/", nonsequentialusers=True,
-                            use_json=True, eval_mode="fixed_split", useTimestamps=False,
-                            reverse_user_item_data=True)
+def ref_reader(ref_dr, meta, u=False):
+    if u:      # U orientation: train.py passes num_items / num_users unswapped (train.py:71-76)
+        rd = ref_dr.data_reader(meta["num_items"], meta["num_users"], TOY_U + "/", nonsequentialusers=True,
+                                use_json=True, eval_mode="fixed_split", useTimestamps=False,
+                                reverse_user_item_data=False)
+    else:      # train.py:71-76 swaps num_items/num_users for I-AutoRec
+        rd = ref_dr.data_reader(meta["num_users"], meta["num_items"], TOY + "/", nonsequentialusers=True,
+                                use_json=True, eval_mode="fixed_split", useTimestamps=False,
+                                reverse_user_item_data=True)
     rd.train_set = list(rd.train_set)
     rd.val_set = list(rd.val_set)
     rd.test_set = list(rd.test_set)
@@ -125,17 +158,14 @@ def drain(gen, n, with_count=False):
     return out
 
 
-def main():
-    meta = make_toy_dataset(TOY)
-    ref_dr = import_reference()
-    sys.path.insert(0, REPO)
+def run_configs(ref_dr, meta, u):
     from oracle.batch_oracle import ReaderOracle
-
     store = {}
     for ci, (name, sp, pt, aux_type, auxv) in enumerate(TRAIN_CONFIGS):
         for impl in ("ref", "oracle"):
             np.random.seed(1234 + ci)
-            rd = ref_reader(ref_dr, meta) if impl == "ref" else ReaderOracle.from_dir(TOY)
+            rd = ref_reader(ref_dr, meta, u) if impl == "ref" else \
+                ReaderOracle.from_dir(TOY_U if u else TOY, reverse_user_item_data=not u)
             ntr = rd.train_set_size if impl == "ref" else len(rd.train_keys)
             nva = rd.val_set_size if impl == "ref" else len(rd.valid_keys)
             nte = rd.test_set_size if impl == "ref" else len(rd.test_keys)
@@ -168,10 +198,21 @@ def main():
                 if len(ri) == 3:
                     assert ri[2] == oi[2]
                     store["%s/%s/%d/count" % (name, tag, bi)] = np.asarray(ri[2])
-        print("config %-12s ok (%d train batches)" % (name, ntr // B))
-    np.savez_compressed(os.path.join(HERE, "batches.npz"), **store)
+        print("%s config %-12s ok (%d train batches)" % ("U" if u else "I", name, ntr // B))
+    return store
+
+
+def main():
+    meta, meta_u = make_toy_dataset(TOY)
+    ref_dr = import_reference()
+    sys.path.insert(0, REPO)
+    np.savez_compressed(os.path.join(HERE, "batches.npz"), **run_configs(ref_dr, meta, False))
+    store_u = run_configs(ref_dr, meta_u, True)
+    np.savez_compressed(os.path.join(HERE, "batches_u.npz"), **store_u)
+    store = store_u
     cfg = {"B": B, "train_configs": TRAIN_CONFIGS, "seed_base": 1234,
            "sequence": ["train1", "valid", "test", "train2"], "meta": meta,
+           "u": {"dir": "toy_u", "npz": "batches_u.npz", "meta": meta_u, "reverse_user_item_data": False},
            "generator": "reference data_reader.py via tests/golden/make_golden.py"}
     with open(os.path.join(HERE, "batches_config.json"), "w") as f:
         json.dump(cfg, f, indent=1)

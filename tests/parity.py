@@ -82,7 +82,7 @@ def sparse_batch(csr, rows, N, aux=-1.0):
 
 def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_type=None, causal=False,
                gather=True, sparse_dw=None, dropout=None, data=None, n_rows=None, lr=None, eval_rmse=True,
-               envelope=False, model_hook=None, sparse_oracle=False, eval_batches=None):
+               envelope=False, model_hook=None, sparse_oracle=False, eval_batches=None, l2=None):
     """`steps` training steps through fit_generator (one call per step, so the engine's Philox
     dropout masks engine.mask[l][:B, :H] can be read back after each and fed to the oracle as Keras'
     Dropout draw, model.py:72-73), then the oracle on the same rows (the generator exposes its epoch
@@ -96,7 +96,7 @@ def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_
     np.random.seed(77)
     rd = data_reader(N, n_rows or data.train.n_rows, dataset=data, eval_mode="fixed_split")
     om = omni_model(layers, H, N, B, dense_activation=act, use_causal_info=causal, compute_dtype=compute_dtype,
-                    seed=11, dropout_probability=dropout)
+                    seed=11, dropout_probability=dropout, l2_weight_regulatization=l2)
     m = om.model
     om.engine.use_sparse = gather
     if sparse_dw is not None:
@@ -115,7 +115,7 @@ def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_
     w_gpu = m.get_weights()
     live_rows_used = bool(om.engine._rtag_live)        # (the eval batches below reset it)
     k = 1 + int(causal)
-    ora = OmniOracle([k * N] + [H] * layers + [N], activation=act, dropout=dropout,
+    ora = OmniOracle([k * N] + [H] * layers + [N], activation=act, dropout=dropout, l2=l2,
                      dtype=np.float64).set_params(w0[0::2], w0[1::2])
     opt = oracle_opt(opt_name, lr)
     u = UNIT_ROUNDOFF[compute_dtype]

@@ -15,14 +15,51 @@ def _data(rows=600, cols=200, nnz=9000, seed=2):
 
 
 @pytest.mark.gpu
-def test_trainer_end_to_end(gpu, tmp_path):
+def test_trainer_end_to_end_vs_oracle(gpu, tmp_path):
+    """train.py driver on BASELINE configs[0] (ML-100K-shaped I-AutoRec, 1 x 500 sigmoid, dropout 0.2,
+    Adagrad 0.005, batch 128, exact fp32): the early-stopping decisions replayed from its validation
+    history (train.py:147-177), a checkpoint for exactly the improving epochs (never the first), the
+    tested model = the best checkpoint (train.py:181-199), and compute_full_RMSE (train.py:225-255)
+    equal to the oracle's on that checkpoint's weights over the same test batches (1e-5)"""
+    import os
+    from safetensors.numpy import load_file
     from omnidirectional_collaborative_filtering_amd import train
+    from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
     cfg = dict(train.DEFAULTS)
-    cfg.update(synthetic="ml100k", max_epochs=3, batch_size=128, num_hidden_units=64, patience=5,
-               model_save_path=str(tmp_path), compute_dtype="float16", seed=4)
+    cfg.update(synthetic="ml100k", max_epochs=4, batch_size=128, num_hidden_units=500, patience=0,
+               model_save_path=str(tmp_path), compute_dtype="float32", seed=4)
     out = train.run(cfg)
-    assert np.isfinite(out["manual_test_RMSE"]) and 0.3 < out["manual_test_RMSE"] < 5.0
-    assert out["epochs_run"] == 3
+    st = train.EarlyStopper(0)
+    saved, epochs = [], 0
+    for i, v in enumerate(out["val_history"]):
+        a = st.update(i, [v])
+        epochs = i + 1
+        if a == "save":
+            saved.append(i + 1)
+        if a == "stop":
+            break
+    assert out["epochs_run"] == epochs and out["best_epoch"] == st.best_epoch + 1
+    files = sorted(f for f in os.listdir(str(tmp_path)) if f.endswith(".safetensors"))
+    assert len(files) == len(saved) and all(("_epoch_%d_" % e) in f for e, f in zip(sorted(saved), files))
+    assert 1 not in saved
+    if not saved:
+        assert out["tested_checkpoint"] is None
+        return
+    assert "_epoch_%d_" % out["best_epoch"] in out["tested_checkpoint"]
+    t = load_file(out["tested_checkpoint"])
+    w = [t["param/%d" % j] for j in range(4)]
+    data = synthetic_fixed_split("ml100k", seed=0)
+    N = data.num_cols
+    ora = OmniOracle([N, 500, N], activation="sigmoid").set_params(w[0::2], w[1::2])
+    sse, cnt = 0.0, 0
+    for rows in out["manual_test_rows"]:
+        _, _, x, _, _ = scatter_rows_numpy(data.test_in.row_ptr, data.test_in.col, data.test_in.val, rows, N, aux=-1.0)
+        _, mo, _, tt, _ = scatter_rows_numpy(data.test_tgt.row_ptr, data.test_tgt.col, data.test_tgt.val, rows, N,
+                                             aux=-1.0)
+        y, _ = ora.forward(x, mo)
+        sse += float(((y - tt) ** 2).sum())
+        cnt += int(data.test_tgt.row_lengths()[rows].sum())
+    assert abs(out["manual_test_RMSE"] - np.sqrt(sse / cnt)) <= 1e-5
 
 
 @pytest.mark.gpu

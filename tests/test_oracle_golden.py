@@ -23,19 +23,31 @@ def gold():
     return np.load(os.path.join(GOLD, "batches.npz"))
 
 
+@pytest.fixture(scope="module")
+def gold_u():
+    return np.load(os.path.join(GOLD, _cfg()["u"]["npz"]))
+
+
 def _drain(gen, n):
     out = [next(gen) for _ in range(n)]
     assert next(gen) is None
     return out
 
 
+@pytest.mark.parametrize("orient", ["I", "U"])
 @pytest.mark.parametrize("ci", range(5))
-def test_oracle_reproduces_reference(gold, ci):
+def test_oracle_reproduces_reference(gold, gold_u, ci, orient):
+    """I: ratingsByItem_* + unique_users_list (I-AutoRec); U: ratingsByUser_* + unique_items_list
+    (reverse_user_item_data=False, data_reader.py:20-23,46-49)"""
     cfg = _cfg()
     name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
     B = cfg["B"]
     np.random.seed(cfg["seed_base"] + ci)
-    rd = ReaderOracle.from_dir(TOY)
+    if orient == "U":
+        gold = gold_u
+        rd = ReaderOracle.from_dir(os.path.join(GOLD, cfg["u"]["dir"]), reverse_user_item_data=False)
+    else:
+        rd = ReaderOracle.from_dir(TOY)
     seq = [("train1", rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through=pt), len(rd.train_keys)),
            ("valid", rd.data_gen(B, sp, "valid", True, aux_type, auxv, return_target_count=True), len(rd.valid_keys)),
            ("test", rd.data_gen(B, sp, "test", True, aux_type, auxv, return_target_count=True), len(rd.test_keys)),
@@ -67,16 +79,23 @@ def test_uniform_and_stream_concatenation():
     assert np.array_equal(y, np.random.random_sample(10))
 
 
+@pytest.mark.parametrize("orient", ["I", "U"])
 @pytest.mark.parametrize("ci", range(5))
-def test_product_epoch_plan_matches_reference(gold, ci):
+def test_product_epoch_plan_matches_reference(gold, gold_u, ci, orient):
     """BatchGenerator.plan (host) + the vectorised scatter reproduce the reference train batches."""
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     cfg = _cfg()
     name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
     B = cfg["B"]
-    meta = cfg["meta"]
     np.random.seed(cfg["seed_base"] + ci)
-    rd = data_reader(meta["num_users"], meta["num_items"], TOY, eval_mode="fixed_split", reverse_user_item_data=True)
+    if orient == "U":
+        gold, meta = gold_u, cfg["u"]["meta"]
+        rd = data_reader(meta["num_items"], meta["num_users"], os.path.join(GOLD, cfg["u"]["dir"]),
+                         eval_mode="fixed_split", reverse_user_item_data=False)
+    else:
+        meta = cfg["meta"]
+        rd = data_reader(meta["num_users"], meta["num_items"], TOY, eval_mode="fixed_split",
+                         reverse_user_item_data=True)
     gen = rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through_input_training=pt)
     tr = rd.data.train
     rows, boff, _, keep = gen.plan(tr.row_lengths())

@@ -61,3 +61,14 @@ def test_low_precision_dropout(gpu, cd, tol, gather):
     dropout 0.2, Adagrad, row skipping on the gather path)"""
     res = run_parity(cd, "adagrad", 1, "sigmoid", dropout=0.2, gather=gather, envelope=True)
     assert_low_precision(res, tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather", [True, False])
+def test_fp32_l2_regulariser(gpu, gather):
+    """l2_weight_regulatization (model.py:66,82 W_regularizer=l2): the update sees g + 2 l2 W and the
+    logged loss carries l2 * sum(W^2) of every kernel (Keras' total loss), both against the oracle;
+    row skipping is off (a zero-gradient row still decays under l2)"""
+    res = run_parity("float32", "adagrad", 1, "sigmoid", l2=1e-3, gather=gather)
+    assert not res.om.engine._rtag_live
+    assert_fp32(res)
