@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--fp32-steps", type=int, default=10,
+                    help="N=1, 16-bit runs: also time this many steps of the exact-fp32 parity mode "
+                         "(compute_dtype float32; reported as fp32_parity_mode, not the headline)")
     ap.add_argument("--phase-timers", type=int, default=1)
     ap.add_argument("--rmse", type=int, default=1)
     ap.add_argument("--emulate-shards", type=int, default=0,
@@ -108,20 +111,36 @@ def optim(name, lr):
             "adam": lambda: O.Adam(lr=lr), "sgd": lambda: O.SGD(lr=lr)}[name]()
 
 
-def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps):
-    """The oracle restatement on the host cores (bounded sample): per-rating Python assembler
-    (data_reader.py:95-200, one core) + NumPy fp32 model step (Keras math, BLAS threads)."""
+# BASELINE.json configs by workload name: (index, dataset shape label)
+CONFIGS = {"ml100k": (0, "ML-100K", "1,682 x 943"), "ml1m": (1, "ML-1M", "3,706 x 6,040"),
+           "ml20m": (2, "ML-20M", "26,744 x 138,493"), "netflix": (3, "Netflix", "17,770 x 480,189")}
+REF_ASM_MS_PER_128 = {"ml20m": 233.9, "ml1m": 41.7}   # the reference's own assembler, 1 core
+
+
+def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps, config):
+    """The oracle restatement on the host cores (bounded sample): the reference's batch assembler
+    restated with its own data structures (ReaderOracle: dict of rows -> [[column id string, rating]],
+    column ids through the id dict, per-rating scalar stores into float64 zeros; data_reader.py:95-200,
+    one core) + a NumPy fp32 dense model step (Keras math, Adagrad; BLAS threads)."""
     from threadpoolctl import threadpool_info
-    from oracle.batch_oracle import train_batch_loop_csr
+    from oracle.batch_oracle import ReaderOracle
     from oracle.model_oracle import AdagradOracle, OmniOracle
     tr = data.train
     t_asm = t_mod = 0.0
     nnz = 0
     ora = OmniOracle([N, H, N], activation="sigmoid", dtype=np.float32).set_params(w0[0::2], w0[1::2])
     opt = AdagradOracle(lr=lr)
+    # the sampled rows in the reference's JSON-dict form (only these rows: the full dict of 20M
+    # ratings would be minutes of host setup for a bounded sample)
+    rows_all = np.unique(np.concatenate([np.asarray(r) for r in rows_batches[:n_steps]]))
+    rdict = {str(r): [[str(int(c)), float(v)] for c, v in zip(tr.col[tr.row_ptr[r]:tr.row_ptr[r + 1]],
+                                                               tr.val[tr.row_ptr[r]:tr.row_ptr[r + 1]])]
+             for r in rows_all}
+    ro = ReaderOracle([str(c) for c in range(N)], rdict)
     for rows in rows_batches[:n_steps]:
+        keys = [str(r) for r in rows]
         t0 = time.perf_counter()
-        m_in, m_out, x, t, m_miss = train_batch_loop_csr(tr.row_ptr, tr.col, tr.val, rows, N)
+        m_in, m_out, x, t, m_miss = ro.train_batch(keys, len(keys), 0, (1.0, 1.0), -1.0, True)
         t1 = time.perf_counter()
         loss, _, gW, gb = ora.loss_and_grads(x, m_out, t)
         ora.set_flat(opt.step(ora.params(), [g for pair in zip(gW, gb) for g in pair]))
@@ -130,10 +149,41 @@ def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps):
         t_mod += t2 - t1
         nnz += int(tr.row_lengths()[rows].sum())
     threads = max([d.get("num_threads", 1) for d in threadpool_info()] + [1])
-    return {"value": nnz / (t_asm + t_mod), "unit": "ratings/s", "cores": int(threads), "kind": "port",
-            "sample": "%d ML-20M-shaped train steps (B=%d): per-rating Python assembler %.2fs/step on 1 core + "
-                      "NumPy fp32 dense model step (Adagrad) %.2fs/step on %d BLAS threads"
-                      % (n_steps, len(rows_batches[0]), t_asm / n_steps, t_mod / n_steps, threads)}
+    B = len(rows_batches[0])
+    out = {"value": nnz / (t_asm + t_mod), "unit": "ratings/s", "cores": int(threads), "kind": "port",
+           "sample": "%d %s-shaped train steps (B=%d): the reference's dict-of-lists assembler restated, %.2fs/step "
+                     "on 1 core + NumPy fp32 dense model step (Adagrad) %.2fs/step on %d BLAS threads"
+                     % (n_steps, CONFIGS[config][1], B, t_asm / n_steps, t_mod / n_steps, threads),
+           "assembler_ms_per_128_rows": round(t_asm / n_steps * 1e3 * 128 / B, 1)}
+    if config in REF_ASM_MS_PER_128:
+        out["assembler_cross_check"] = ("the reference's own assembler measured %.1f ms per 128-row batch in the "
+                                        "survey container (BASELINE.md)" % REF_ASM_MS_PER_128[config])
+    return out
+
+
+def fp32_mode(args, data, rd, n_rows, dev, steps):
+    """ms/step of the exact-fp32 parity mode (compute_dtype float32, v_mfma_f32_32x32x2_f32; the mode the
+    1e-5 parity bar is tested in) on the same workload, N=1"""
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    om = omni_model(1, args.hidden, data.num_cols, args.batch, dense_activation="sigmoid", use_causal_info=False,
+                    dropout_probability=args.dropout or None, compute_dtype="float32", seed=7, device=dev)
+    m = om.model
+    m.compile(optim(args.optimizer, 0.005 if args.optimizer == "adagrad" else 0.001), "mean_squared_error")
+    gen = rd.data_gen(args.batch, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    gen._start()
+    nb = gen.num_batches
+    for i in range(3):
+        m._load(None, gen, i % nb)
+        om.engine.train_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        m._load(None, gen, (3 + i) % nb)
+        om.engine.train_step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    om.engine.take_stats()
+    return {"ms_per_step": round(ms, 4), "steps": steps, "compute": "float32 (exact fp32 MFMA)"}
 
 
 def main():
@@ -325,8 +375,11 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": {"float16": "f16", "bfloat16": "bf16",
                                                           "float32": "f32"}[args.dtype],
-        "data": "synthetic ML-20M-shaped fixed split (26,744 x 138,493, 20.0M ratings, seed 0); random-init weights",
-        "config": {"workload": "ml20m I-AutoRec train step (BASELINE configs[2])", "rows": n_rows, "N": N,
+        "data": "synthetic %s-shaped fixed split (%s, %.1fM ratings, seed 0); random-init weights"
+                % (CONFIGS[args.config][1], CONFIGS[args.config][2],
+                   (data_full.train.nnz + data_full.valid_tgt.nnz + data_full.test_tgt.nnz) / 1e6),
+        "config": {"workload": "%s I-AutoRec train step (BASELINE configs[%d])" % (args.config, CONFIGS[args.config][0]),
+                   "rows": n_rows, "N": N,
                    "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
                    "activation": "sigmoid", "dropout": args.dropout, "compute": args.dtype + " MFMA, fp32 accumulate",
                    "parallelism": ("feature%d" % world) if fp else ("dp%d" % world)},
@@ -345,10 +398,12 @@ def main():
         "setup_s": round(setup_s, 1),
         "host_issue_ms_per_step": round(host_ms, 4),
     }
+    if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
+        line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)
     if world == 1 and args.cpu_baseline:
         rows_b = [gen.rows_host[bi] for bi in batches[: args.cpu_steps]]
         try:
-            line["cpu_baseline"] = cpu_baseline(data, rows_b, N, H, w0, lr, args.cpu_steps)
+            line["cpu_baseline"] = cpu_baseline(data, rows_b, N, H, w0, lr, args.cpu_steps, args.config)
         except Exception as e:  # the baseline is reported, never the measured value
             line["cpu_baseline"] = {"error": repr(e)}
     print(json.dumps(line), flush=True)

@@ -537,14 +537,14 @@ __global__ void __launch_bounds__(256) tb_count_kernel(OcfTileBucketArgs a) {
 }
 
 // Row lists of tile t (ocf.h OcfTileBucketArgs row_ptr / row_ent), from the tile's buckets just
-// written by this workgroup (entries in (K-step, batch row, column) order): a counting sort by column
-// whose rank inside a column is the number of earlier same-column entries (chunks of 256 in order,
-// an LDS scan inside a chunk), so every column's list is in batch-row order without atomics deciding
-// the order.
+// written by this workgroup (entries in (K-step, batch row, column) order): a stable counting sort by
+// column.  Per chunk of 256 entries an entry's rank among the earlier same-column entries is counted
+// inside its wave by lane reads (no LDS traffic) plus the same-column counts of the earlier waves, so
+// every column's list is in batch-row order without atomics deciding the order.
 __device__ void tb_rows(const OcfTileBucketArgs& a, int t, int tile_base) {
   __shared__ int cnt_m[128], base_m[128], kofs[65];
-  __shared__ uint8_t mch[256];
-  const int tid = threadIdx.x;
+  __shared__ int wcnt[4][128];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nk = a.nk, before = t * nk;
   if (tid < 128) cnt_m[tid] = 0;
   if (tid <= nk) kofs[tid] = 0;
@@ -581,18 +581,31 @@ __device__ void tb_rows(const OcfTileBucketArgs& a, int t, int tile_base) {
     if (i < n) {
       e = ent[i];
       m = e.y >> 8;
-      mch[tid] = (uint8_t)m;
+    }
+    int r = 0, tot = 0;                 // same-column entries of this wave: before this lane / all
+    for (int j = 0; j < 64; ++j) {
+      const int mj = __builtin_amdgcn_readlane(m, j);
+      const int eq = mj == m ? 1 : 0;
+      tot += eq;
+      r += j < lane ? eq : 0;
+    }
+    wcnt[w][tid & 127] = 0;
+    wcnt[w][(tid & 127) ^ 64] = 0;
+    __syncthreads();
+    if (m >= 0) wcnt[w][m] = tot;       // every lane of the column writes the same count
+    __syncthreads();
+    if (m >= 0) {
+      for (int v = 0; v < w; ++v) r += wcnt[v][m];
+      int lo = 0, hi = nk - 1;          // the entry's K-step: the bucket holding position i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (kofs[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      rent[base_m[m] + r] = make_int2(e.x, lo * 64 + (e.y & 255));
     }
     __syncthreads();
-    if (i < n) {
-      int r = 0;
-      for (int j = 0; j < tid; ++j) r += mch[j] == m;
-      int kt = 0;                         // the entry's K-step: the bucket holding position i
-      while (kt + 1 < nk && kofs[kt + 1] <= i) ++kt;
-      rent[base_m[m] + r] = make_int2(e.x, kt * 64 + (e.y & 255));
-    }
-    __syncthreads();
-    if (i < n) atomicAdd(&base_m[m], 1);   // the chunk's entries of m precede the next chunk's
+    if (tid < 128) base_m[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
     __syncthreads();
   }
 }

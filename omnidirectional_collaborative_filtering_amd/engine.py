@@ -230,18 +230,22 @@ class Engine:
         self.gt = None
         self.sparse_ok = self.k == 1 and self.Hp[0] <= 512 and self.Hp[-1] <= 512
         self.use_sparse = True
-        # dW_out / dW_in operand A: built in LDS from the entries (sparse A, ocf.h a_sparse; no dense
-        # [B][N] arrays, no memsets) or the dense d_out / xin.  The sparse fill pays a chain of dependent
-        # index loads per K-step, so it wins only for short K loops: ML-20M, 1 GPU (K = 256): 0.774 vs
-        # 0.811 ms/step; with the bucketed role-split kernel, rank 0 of a feature-parallel job: 2-way
-        # (K = 512) 0.453 vs 0.509, 4-way (K = 1,024) 0.42 vs 0.38, 8-way (K = 2,048) 0.46 vs 0.375.
-        self.sparse_dw = Bp <= 512
+        # dW_out / dW_in operand A: the batch entries (sparse A, ocf.h a_sparse; no dense [B][N] arrays,
+        # no memsets: row lists for the row-stream kernel, or LDS-filled tiles for the MFMA kernels) or
+        # the dense d_out / xin.  With the MFMA kernels the sparse fill pays a chain of dependent index
+        # loads per K-step and lost beyond K = 512 (8-way feature-parallel rank step 0.46 vs 0.375 ms);
+        # the row-stream kernel (16-bit compute) has no K-loop and wins up to K = 2,048 (below).
+        self.sparse_dw = Bp <= (2048 if self.cdt != _lib.DT_F32 else 512)
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         # ... and as row lists (the buckets' transpose) for the row-stream kernel (ocf_rows_dw.h): one
         # wave per live weight row streams whole parameter / slot rows and forms the row's gradient from
         # its ~2 entries, no MFMA over the mostly-zero batch operand.  ML-20M step 0.50 -> 0.44 ms
         # (dW 200 -> 150-165 us per launch).  16-bit compute only (the library falls back otherwise).
         self.dw_rows = self.cdt != _lib.DT_F32
+
+        # with it, sparse operands pay off up to K = 2,048 (the 8-way feature-parallel global batch):
+        # emulated rank steps 4-way 0.353 -> 0.308 ms, 8-way 0.317 -> 0.294 ms vs the dense-operand
+        # generic kernel
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)

@@ -22,10 +22,10 @@ grep '^{' "$O/bench.log" | tail -1 > "$O/bench.json"
 cat "$O/bench.json"
 cd /tmp
 export TMPDIR=/tmp
-BARGS="--steps 20 --warmup 5 --cpu-baseline 0 --rmse 0"
+BARGS="--steps 20 --warmup 5 --cpu-baseline 0 --rmse 0 --fp32-steps 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ks" -o ks -- \
   python3 "$R/bench.py" $BARGS "$@" > "$O/ks.log" 2>&1
-BARGS_PMC="--steps 10 --warmup 2 --cpu-baseline 0 --rmse 0 --phase-timers 0"
+BARGS_PMC="--steps 10 --warmup 2 --cpu-baseline 0 --rmse 0 --phase-timers 0 --fp32-steps 0"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pf" -o f -- \
   python3 "$R/bench.py" $BARGS_PMC "$@" > "$O/pf.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pw" -o w -- \
