@@ -107,6 +107,10 @@ typedef struct OcfScatterArgs {
    * columns so tagged are a superset of the weight rows with a nonzero gradient this step
    * (OcfGemmArgs row_tag); the caller cycles rtag through 1..255 so no clearing pass is needed */
   uint8_t* rtag_in; uint8_t* rtag_out; int rtag;
+  /* (nullable, mode 0) the batch's per-column entry counts and entry keys for ocf_row_lists:
+   * col_cnt[c] += 1 and ecb[e] = c | b << 19 for every source-1 entry e (column c < 2^19, batch row
+   * b < 4096); the caller zeroes col_cnt once, ocf_row_lists leaves it zeroed for the next batch */
+  int32_t* col_cnt; int32_t* ecb;
 } OcfScatterArgs;
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
@@ -317,6 +321,23 @@ typedef struct OcfTileBucketArgs {
   int32_t* row_ptr; int32_t* row_ent;
 } OcfTileBucketArgs;
 int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
+
+/* ocf_row_lists -- the batch's entries grouped by column (the row lists of OcfGemmArgs sp_rowptr /
+ * sp_rowent) straight from the scatter's counts and keys, in parallel over the entries and columns
+ * whatever the number of column tiles: row_ptr = exclusive scan of col_cnt (which is zeroed for the
+ * next batch), each entry placed at its column's cursor, then every column's list sorted by entry
+ * index (= batch-row order; deterministic).  cursor: scratch of 2 n_cols + 128 ints whose first n_cols
+ * are zero on entry (and are left zero).
+ * With rtag_* / live_*, also the live-row records of ocf_sparse_tiles (OCF_LIVE_REC per 128 rows).
+ * Extension (no reference counterpart): feeds the row-stream weight-gradient kernel. */
+typedef struct OcfRowListArgs {
+  const int32_t* ecb; int64_t E;
+  int32_t* col_cnt; int32_t* cursor; int n_cols;
+  int32_t* row_ptr; int32_t* row_ent;
+  const uint8_t* rtag_in; const uint8_t* rtag_out; int rtag;
+  uint8_t* live_in; uint8_t* live_out;
+} OcfRowListArgs;
+int ocf_row_lists(const OcfRowListArgs* args, void* stream);
 
 /* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on

@@ -42,7 +42,14 @@ class OcfScatterArgs(ctypes.Structure):
         ("pos1", P),
         ("lboff1", P), ("lboff2", P), ("E1", I64), ("E2", I64), ("tflag1", P), ("tflag2", P),
         ("xin_clean", I32), ("xval1", P), ("tb_cnt", P), ("tb_nk", I32),
-        ("rtag_in", P), ("rtag_out", P), ("rtag", I32),
+        ("rtag_in", P), ("rtag_out", P), ("rtag", I32), ("col_cnt", P), ("ecb", P),
+    ]
+
+
+class OcfRowListArgs(ctypes.Structure):
+    _fields_ = [
+        ("ecb", P), ("E", I64), ("col_cnt", P), ("cursor", P), ("n_cols", I32), ("row_ptr", P), ("row_ent", P),
+        ("rtag_in", P), ("rtag_out", P), ("rtag", I32), ("live_in", P), ("live_out", P),
     ]
 
 
@@ -124,6 +131,7 @@ SIGNATURES = {
     "ocf_rows_reduce": (I32, [ctypes.POINTER(OcfRowsReduceArgs), P]),
     "ocf_colsum": (I32, [P, I32, I64, I32, I32, F32, P, P]),
     "ocf_sparse_tiles": (I32, [ctypes.POINTER(OcfTileBucketArgs), P]),
+    "ocf_row_lists": (I32, [ctypes.POINTER(OcfRowListArgs), P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),

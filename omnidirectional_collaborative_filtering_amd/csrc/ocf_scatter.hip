@@ -110,6 +110,10 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a,
     }
     if (a.xval1) a.xval1[e] = ((role & 1) && !later_in) ? v : 0.f;
     if (a.tb_cnt) atomicAdd(&a.tb_cnt[(c >> 7) * a.tb_nk + (b >> 6)], 1);   // ocf_sparse_tiles counts
+    if (a.col_cnt) {                                                         // ocf_row_lists counts / keys
+      atomicAdd(&a.col_cnt[c], 1);
+      a.ecb[e] = c | (b << 19);
+    }
     const bool live_tg = (role & 2) && !later_tg;
     if (role & 2) {
       if (a.Mout) a.Mout[o] = aux;
@@ -273,6 +277,8 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   OCF_CHECK(a.E1 >= 0 && a.E2 >= 0, "ocf_scatter_batch: negative entry counts");
   OCF_CHECK(a.E2 == 0 || (a.rows2 && a.lboff2), "ocf_scatter_batch: source 2 needs rows2 / lboff2");
   OCF_CHECK(a.E1 == 0 || (a.rows1 && (a.lboff1 || a.boff1)), "ocf_scatter_batch: source 1 needs rows1 / offsets");
+  OCF_CHECK(!a.col_cnt || (a.ecb && a.mode == 0 && a.B <= 4096 && a.N <= (1 << 19)),
+            "ocf_scatter_batch: col_cnt needs ecb, mode 0, B <= 4096 and N <= 2^19");
   OCF_CHECK(!(a.rtag_in || a.rtag_out) || (a.rtag >= 1 && a.rtag <= 255),
             "ocf_scatter_batch: row tags need 1 <= rtag <= 255");
   // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks)

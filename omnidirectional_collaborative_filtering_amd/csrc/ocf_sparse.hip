@@ -536,6 +536,18 @@ __global__ void __launch_bounds__(256) tb_count_kernel(OcfTileBucketArgs a) {
   if (lane == 0) a.cnt[id] = tot;
 }
 
+// live-row record of tile t (ocf.h OCF_LIVE_REC) from a tag array, by one wave: rank k of a live row =
+// live rows before it in the tile
+__device__ __forceinline__ void live_record(const uint8_t* tags, uint8_t* rec, int rtag, int lane) {
+  const bool l0 = tags[lane] == (uint8_t)rtag, l1 = tags[64 + lane] == (uint8_t)rtag;
+  const uint64_t b0 = __ballot(l0), b1 = __ballot(l1), below = (1ull << lane) - 1;
+  const int n0 = __popcll(b0);
+  const int k0 = __popcll(b0 & below), k1 = n0 + __popcll(b1 & below);
+  if (l0) rec[16 + (k0 & 7) * 16 + (k0 >> 3)] = (uint8_t)lane;
+  if (l1) rec[16 + (k1 & 7) * 16 + (k1 >> 3)] = (uint8_t)(64 + lane);
+  if (lane == 0) *reinterpret_cast<int*>(rec) = n0 + __popcll(b1);
+}
+
 // Row lists of tile t (ocf.h OcfTileBucketArgs row_ptr / row_ent), from the tile's buckets just
 // written by this workgroup (entries in (K-step, batch row, column) order): a stable counting sort by
 // column.  Per chunk of 256 entries an entry's rank among the earlier same-column entries is counted
@@ -620,17 +632,9 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
   const int nb = a.gm * a.nk, before = t * a.nk;
   // live-row records of tile t (ocf.h OCF_LIVE_REC): wave 0 from the input tags, wave 1 from the
   // target tags; rank k of a live row = live rows before it in the tile
-  if (w < 2 && (w == 0 ? a.live_in : a.live_out)) {
-    const uint8_t* tg = (w == 0 ? a.rtag_in : a.rtag_out) + (int64_t)t * 128;
-    uint8_t* rec = (w == 0 ? a.live_in : a.live_out) + (int64_t)t * OCF_LIVE_REC;
-    const bool l0 = tg[lane] == (uint8_t)a.rtag, l1 = tg[64 + lane] == (uint8_t)a.rtag;
-    const uint64_t b0 = __ballot(l0), b1 = __ballot(l1), below = (1ull << lane) - 1;
-    const int n0 = __popcll(b0);
-    const int k0 = __popcll(b0 & below), k1 = n0 + __popcll(b1 & below);
-    if (l0) rec[16 + (k0 & 7) * 16 + (k0 >> 3)] = (uint8_t)lane;
-    if (l1) rec[16 + (k1 & 7) * 16 + (k1 >> 3)] = (uint8_t)(64 + lane);
-    if (lane == 0) *reinterpret_cast<int*>(rec) = n0 + __popcll(b1);
-  }
+  if (w < 2 && (w == 0 ? a.live_in : a.live_out))
+    live_record((w == 0 ? a.rtag_in : a.rtag_out) + (int64_t)t * 128,
+                (w == 0 ? a.live_in : a.live_out) + (int64_t)t * OCF_LIVE_REC, a.rtag, lane);
   int s = 0;
   for (int i = tid; i < before; i += 256) s += a.cnt[i];
   red[tid] = s;
@@ -674,7 +678,132 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
   if (a.row_ptr) tb_rows(a, t, tile_base);
 }
 
+// ---- row lists straight from the scatter's per-column counts (ocf_row_lists) ------------------------
+// row_ptr = exclusive scan of col_cnt in blocks of RL_CHUNK columns: rl_scan_kernel scans each block
+// locally (coalesced int4 loads, wave scans + the block's wave totals) into lp[] and the block total
+// into bsum[]; the later kernels add the block offsets, each computing the (<= 128) offsets in LDS
+constexpr int RL_CHUNK = 4096;
+constexpr int RL_REG = 32;      // lists up to this long are sorted in registers (K = 2,048 rows: ~11 per column)
+__global__ void __launch_bounds__(1024) rl_scan_kernel(OcfRowListArgs a) {
+  __shared__ int wtot[16];
+  const int n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* lp = a.cursor + n;
+  int* bsum = a.cursor + 2 * n;
+  const int i0 = blockIdx.x * RL_CHUNK + 4 * tid;
+  int4 v = make_int4(0, 0, 0, 0);
+  if (i0 < n) {                          // n % 128 == 0: a thread's 4 columns are all in range or none
+    v = *reinterpret_cast<const int4*>(a.col_cnt + i0);
+    *reinterpret_cast<int4*>(a.col_cnt + i0) = make_int4(0, 0, 0, 0);   // zeroed for the next batch
+  }
+  const int ts = v.x + v.y + v.z + v.w;
+  const int incl = wave_incl_scan(ts, lane);
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  int off = 0;
+  for (int k = 0; k < w; ++k) off += wtot[k];
+  const int ex = off + incl - ts;
+  if (i0 < n) *reinterpret_cast<int4*>(lp + i0) = make_int4(ex, ex + v.x, ex + v.x + v.y, ex + v.x + v.y + v.z);
+  if (tid == 1023) bsum[blockIdx.x] = off + incl;
+}
+
+// exclusive prefix of the block totals into LDS (one wave, nb <= 128 blocks); returns the grand total
+__device__ __forceinline__ int rl_block_offsets(const OcfRowListArgs& a, int* sboff) {
+  const int nb = (a.n_cols + RL_CHUNK - 1) / RL_CHUNK;
+  const int* bsum = a.cursor + 2 * a.n_cols;
+  __shared__ int tot;
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    const int v0 = 2 * l < nb ? bsum[2 * l] : 0, v1 = 2 * l + 1 < nb ? bsum[2 * l + 1] : 0;
+    const int incl = wave_incl_scan(v0 + v1, l);
+    sboff[2 * l] = incl - v0 - v1;
+    sboff[2 * l + 1] = incl - v1;
+    if (l == 63) tot = incl;
+  }
+  __syncthreads();
+  return tot;
+}
+
+// one thread per entry: its column's next slot (unordered; rl_sort_kernel orders each list)
+__global__ void __launch_bounds__(256) rl_fill_kernel(OcfRowListArgs a) {
+  __shared__ int sboff[128];
+  rl_block_offsets(a, sboff);
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E) return;
+  const int v = a.ecb[e];
+  const int c = v & ((1 << 19) - 1), b = v >> 19;
+  const int slot = a.cursor[a.n_cols + c] + sboff[c / RL_CHUNK] + atomicAdd(&a.cursor[c], 1);
+  reinterpret_cast<int2*>(a.row_ent)[slot] = make_int2((int)e, b);
+}
+
+// one thread per column of a 128-column tile: insertion sort of its list by entry index (entry indices
+// grow with the batch row: the list ends in batch-row order, whatever order the fill left), cursor
+// reset; waves 0 / 1 write the tile's live-row records
+__global__ void __launch_bounds__(128) rl_sort_kernel(OcfRowListArgs a) {
+  const int t = blockIdx.x, tid = threadIdx.x, m = t * 128 + tid;
+  const int lane = tid & 63, w = tid >> 6;
+  if (w == 0 && a.live_in) live_record(a.rtag_in + (int64_t)t * 128, a.live_in + (int64_t)t * OCF_LIVE_REC, a.rtag, lane);
+  if (w == 1 && a.live_out)
+    live_record(a.rtag_out + (int64_t)t * 128, a.live_out + (int64_t)t * OCF_LIVE_REC, a.rtag, lane);
+  __shared__ int sboff[128];
+  const int total = rl_block_offsets(a, sboff);
+  const int* lp = a.cursor + a.n_cols;
+  const int lo = lp[m] + sboff[m / RL_CHUNK];
+  const int hi = m + 1 < a.n_cols ? lp[m + 1] + sboff[(m + 1) / RL_CHUNK] : total;
+  a.row_ptr[m] = lo;
+  if (m + 1 == a.n_cols) a.row_ptr[a.n_cols] = total;
+  a.cursor[m] = 0;
+  int2* ent = reinterpret_cast<int2*>(a.row_ent);
+  const int n = hi - lo;
+  if (n <= RL_REG) {
+    // short list (the common case): independent loads, an odd-even transposition sort in registers on
+    // (entry index, batch row) packed into one 64-bit key, independent stores
+    uint64_t k[RL_REG];
+#pragma unroll
+    for (int i = 0; i < RL_REG; ++i) {
+      const int2 x = i < n ? ent[lo + i] : make_int2(0x7fffffff, 0);
+      k[i] = ((uint64_t)(uint32_t)x.x << 32) | (uint32_t)x.y;
+    }
+#pragma unroll
+    for (int p = 0; p < RL_REG; ++p)
+#pragma unroll
+      for (int i = p & 1; i + 1 < RL_REG; i += 2) {
+        const uint64_t lo_k = k[i] < k[i + 1] ? k[i] : k[i + 1], hi_k = k[i] < k[i + 1] ? k[i + 1] : k[i];
+        k[i] = lo_k;
+        k[i + 1] = hi_k;
+      }
+#pragma unroll
+    for (int i = 0; i < RL_REG; ++i)
+      if (i < n) ent[lo + i] = make_int2((int)(k[i] >> 32), (int)(uint32_t)k[i]);
+    return;
+  }
+  for (int i = lo + 1; i < hi; ++i) {    // long list: insertion sort in place
+    const int2 x = ent[i];
+    int j = i - 1;
+    for (; j >= lo; --j) {
+      const int2 y = ent[j];
+      if (y.x <= x.x) break;
+      ent[j + 1] = y;
+    }
+    ent[j + 1] = x;
+  }
+}
+
 }  // namespace ocf
+
+extern "C" int ocf_row_lists(const OcfRowListArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfRowListArgs& a = *args;
+  OCF_CHECK(a.ecb && a.col_cnt && a.cursor && a.row_ptr && a.row_ent, "ocf_row_lists: null pointer");
+  OCF_CHECK(a.n_cols > 0 && a.n_cols % 128 == 0 && a.n_cols <= (1 << 19), "ocf_row_lists: 0 < n_cols <= 2^19, % 128");
+  OCF_CHECK((!a.live_in || a.rtag_in) && (!a.live_out || a.rtag_out), "ocf_row_lists: live records need row tags");
+  OCF_CHECK(!(a.live_in || a.live_out) || (a.rtag >= 1 && a.rtag <= 255), "ocf_row_lists: 1 <= rtag <= 255");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(rl_scan_kernel, dim3((a.n_cols + RL_CHUNK - 1) / RL_CHUNK), dim3(1024), 0, s, a);
+  if (a.E > 0) hipLaunchKernelGGL(rl_fill_kernel, dim3((unsigned)((a.E + 255) / 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(rl_sort_kernel, dim3(a.n_cols / 128), dim3(128), 0, s, a);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
 
 extern "C" int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream) {
   OCF_TRY_BEGIN

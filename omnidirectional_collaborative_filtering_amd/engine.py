@@ -436,19 +436,26 @@ class Engine:
         self.tseg = seg
         self.gt = None
         self._enc_fused = None
-        self._enc_fused = None
         a.tb_cnt, a.tb_nk = None, 0
+        a.col_cnt = a.ecb = None
+        lists = False
         a.rtag_in = a.rtag_out = None
         self._rtag_live = False
         if gather is not None and self.sparse_ok and self.use_sparse:
             xval = self._buf("xval", int(a.E1))
             a.xval1 = ptr(xval)
             if self.sparse_dw and self.dw_buckets and targets["flag"] == 1:   # train split: inputs = targets
-                # tile-bucket counts from the scatter (ocf_sparse_tiles then skips its count pass);
-                # two counter sets alternate so the fill pass can zero the next batch's
-                gm, nk = self.Np // TILE, self.Bp // 64
-                self._tb_par ^= 1
-                a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
+                if self.dw_rows:
+                    # per-column counts and entry keys from the scatter -> row lists (ocf_row_lists)
+                    a.col_cnt = ptr(self._buf("col_cnt", self.Np, torch.int32))
+                    a.ecb = ptr(self._buf("ecb", int(a.E1), torch.int32))
+                    lists = True
+                else:
+                    # tile-bucket counts from the scatter (ocf_sparse_tiles then skips its count pass);
+                    # two counter sets alternate so the fill pass can zero the next batch's
+                    gm, nk = self.Np // TILE, self.Bp // 64
+                    self._tb_par ^= 1
+                    a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
                 if self.row_skip:
                     self._rtag_val = self._rtag_val % 255 + 1
                     a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
@@ -459,8 +466,24 @@ class Engine:
         with self.phase("scatter"):
             a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
-            self.tb = self._tile_buckets() if a.tb_cnt else None
+            self.tb = self._row_lists(int(a.E1)) if lists else (self._tile_buckets() if a.tb_cnt else None)
         self._xin_clean = False
+
+    def _row_lists(self, E):
+        """the batch's entries grouped by weight row (ocf_row_lists, from the scatter's per-column counts)
+        for the row-stream weight-gradient kernel; shared by dW_out (deltas) and dW_in (inputs)"""
+        a = _lib.OcfRowListArgs()
+        a.ecb, a.E = ptr(self._buf("ecb", E, torch.int32)), E
+        a.col_cnt, a.cursor = ptr(self._buf("col_cnt", self.Np, torch.int32)), ptr(self._buf("rl_cur", 2 * self.Np + 128, torch.int32))
+        a.n_cols = self.Np
+        rptr = self._buf("tb_rowptr", self.Np + 1, torch.int32)
+        rent = self._buf("tb_rowent", 2 * max(E, 1), torch.int32)
+        a.row_ptr, a.row_ent = ptr(rptr), ptr(rent)
+        if self._rtag_live:
+            a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
+            a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
+        call("ocf_row_lists", a, cur_stream())
+        return dict(sp_rowptr=rptr, sp_rowent=rent)
 
     def _tile_buckets(self):
         """the batch's entries bucketed by (user tile, K-step) for the persistent weight-gradient
@@ -479,11 +502,6 @@ class Engine:
         a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
         a.counted, a.cnt_clear = 1, ptr(nxt)
         out = dict(sp_bptr=bptr, sp_ent=ent)
-        if self.dw_rows:
-            rptr = self._buf("tb_rowptr", self.Np + 1, torch.int32)
-            rent = self._buf("tb_rowent", 2 * self.gt["E"], torch.int32)
-            a.row_ptr, a.row_ent = ptr(rptr), ptr(rent)
-            out.update(sp_rowptr=rptr, sp_rowent=rent)
         if self._rtag_live:
             a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
             a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])

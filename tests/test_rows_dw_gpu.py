@@ -157,3 +157,45 @@ def test_rows_kernel_matches_mfma_kernels_and_bias_job(gpu):
               cur_stream())
     torch.cuda.synchronize()
     assert torch.equal(b1, b2) and torch.equal(a1, a2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ncols,E,B", [(256, 3000, 256), (6144, 69000, 256), (1024, 40000, 2048),
+                                       (138496, 191000, 256)])
+def test_ocf_row_lists_match_numpy(gpu, ncols, E, B):
+    """ocf_row_lists (the row lists from the scatter's per-column counts and keys): per column, the
+    batch entries in entry order (= batch-row order), row_ptr the exclusive scan of the counts, the
+    counts left zeroed and the cursor scratch left zeroed; the live records as ocf_sparse_tiles'"""
+    rng = np.random.RandomState(ncols + E)
+    b = np.sort(rng.randint(0, B, E))                       # entries in batch-row order (flat order)
+    c = rng.randint(0, ncols, E)
+    ecb = torch.as_tensor((c | (b << 19)).astype(np.int32), device="cuda")
+    cnt = torch.as_tensor(np.bincount(c, minlength=ncols).astype(np.int32), device="cuda")
+    cur = torch.zeros(2 * ncols + 128, dtype=torch.int32, device="cuda")
+    rptr = torch.full((ncols + 1,), -3, dtype=torch.int32, device="cuda")
+    rent = torch.full((E, 2), -9, dtype=torch.int32, device="cuda")
+    tag = 7
+    tags = np.zeros(ncols, np.uint8)
+    tags[np.unique(c)] = tag
+    tags_d = torch.as_tensor(tags, device="cuda")
+    rec = torch.zeros(ncols // 128 * _lib.LIVE_REC, dtype=torch.uint8, device="cuda")
+    a = _lib.OcfRowListArgs()
+    a.ecb, a.E, a.col_cnt, a.cursor, a.n_cols = ecb.data_ptr(), E, cnt.data_ptr(), cur.data_ptr(), ncols
+    a.row_ptr, a.row_ent = rptr.data_ptr(), rent.data_ptr()
+    a.rtag_in, a.rtag_out, a.rtag, a.live_in, a.live_out = tags_d.data_ptr(), tags_d.data_ptr(), tag, rec.data_ptr(), None
+    _lib.call("ocf_row_lists", a, cur_stream())
+    torch.cuda.synchronize()
+    want_ptr = np.concatenate([[0], np.cumsum(np.bincount(c, minlength=ncols))])
+    np.testing.assert_array_equal(rptr.cpu().numpy(), want_ptr)
+    ent = rent.cpu().numpy()
+    order = np.argsort(c, kind="stable")                   # per column, entry order
+    np.testing.assert_array_equal(ent[:, 0], order)
+    np.testing.assert_array_equal(ent[:, 1], b[order])
+    assert not cnt.any() and not cur[:ncols].any()
+    r = rec.cpu().numpy().reshape(-1, _lib.LIVE_REC)
+    for t in range(ncols // 128):
+        live = np.nonzero(tags[t * 128:(t + 1) * 128] == tag)[0]
+        L = int(r[t, :4].view(np.int32)[0])
+        assert L == len(live)
+        got = [r[t, 16 + (k % 8) * 16 + k // 8] for k in range(L)]
+        np.testing.assert_array_equal(got, live)
