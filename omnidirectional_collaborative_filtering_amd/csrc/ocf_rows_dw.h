@@ -77,11 +77,13 @@ template <> struct RsVec<2> {
 
 // A workgroup takes one of PARTS equal parts of a tile's live rows and each wave walks its
 // rows (ranks kb + wave + 4 i) one per iteration, with the index chain run ahead of the data:
-//   A (row i+3): record byte -> row m;             B (row i+2): row pointers, p / slot loads (HBM);
-//   C (row i+1): the first RS_E0 entries;          D (row i+1): their values and B pieces (L2);
+//   A (row i+4): record byte -> row m;     B (row i+3): row pointers;
+//   C (row i+2): the first RS_E0 entries;  D (row i+1): p / slot loads (HBM), entry values, B pieces;
 //   E (row i):   gradient, update, stores.
-// Scalar loads return out of order (a use waits for every outstanding one), so each iteration
-// advances every row by one stage and the chain never waits on the HBM loads or they on it.
+// Scalar loads return out of order (a use waits for every outstanding one), so each stage consumes
+// only what the previous iteration loaded and the consumers are issued first: the one scalar wait per
+// iteration covers loads a whole iteration old.  Against the p / slot loads one stage earlier (B):
+// 75 vs 113 VGPRs (6 vs 4 waves per SIMD), dW_in 144.5 vs 157.5 us.
 // PARTS = 8 (about 11 rows per wave at ML-20M): 2 and 4 parts 177 / 165 us, 6-12 within noise.
 template <int CW, int NCH, int E0, bool ADAM> struct RpRow {
   using F = typename RsVec<CW>::F;
@@ -135,10 +137,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
     r.lv = i < nr;
     r.m = m0 + __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * (i < nr ? i : 0)));
   };
-  auto stB = [&](Row& r) {
-    if (!r.lv) return;
-    r.lo = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m]);
-    r.n = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m + 1]) - r.lo;
+  auto ld_pa = [&](Row& r) {
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const uint32_t o = off(r.m, j);
@@ -146,6 +145,11 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
       r.a[j] = V::ld(r1, ra.s1, o);
       if constexpr (ADAM) r.b[j] = V::ld(r2, ra.s2, o);
     }
+  };
+  auto stB = [&](Row& r) {
+    if (!r.lv) return;
+    r.lo = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m]);
+    r.n = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m + 1]) - r.lo;
   };
   auto stC = [&](Row& r) {
     if (!r.lv) return;
@@ -155,6 +159,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
   };
   auto stD = [&](Row& r) {
     if (!r.lv) return;
+    ld_pa(r);
 #pragma unroll
     for (int e = 0; e < E0; ++e) {
       r.v[e] = 0.f;
@@ -238,25 +243,30 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
       if (jobs.cb_p) jobs.colsum_bias<KIND>(r.m, v, r.bias);
     }
   };
-  // prologue: row 0 through D, row 1 through B, row 2 through A
-  Row r0, r1s, r2s;
+  // every stage consumes only what the previous iteration loaded, and the consumers come first: the
+  // one scalar wait per iteration (at E's first use) covers loads a whole iteration old
+  Row r0, r1s, r2s, r3s;
   stA(r0, 0);
   stA(r1s, 1);
-  stB(r0);
   stA(r2s, 2);
+  stA(r3s, 3);
+  stB(r0);
   stB(r1s);
+  stB(r2s);
   stC(r0);
+  stC(r1s);
   stD(r0);
   for (int i = 0; i < nr; ++i) {
-    Row r3;
-    stA(r3, i + 3);
-    stB(r2s);
-    stC(r1s);
-    stD(r1s);
     stE(r0);
+    stD(r1s);
+    stC(r2s);
+    stB(r3s);
+    Row r4;
+    stA(r4, i + 4);
     r0 = r1s;
     r1s = r2s;
-    r2s = r3;
+    r2s = r3s;
+    r3s = r4;
   }
 }
 }  // namespace ocf
