@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="ml20m")
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--skew", type=float, default=0.0,
+                    help="synthetic item / user popularity ~ rank^-skew (0: uniform; 0.5: ML-20M-like heavy "
+                         "tail with duplicates removed, so somewhat fewer ratings)")
     ap.add_argument("--hidden", type=int, default=500)
     ap.add_argument("--dtype", default="float16")
     ap.add_argument("--optimizer", default="adagrad")
@@ -77,6 +80,9 @@ def parse():
     ap.add_argument("--fuse-enc", type=int, default=1,
                     help="single GPU, one hidden layer: the decoder gather applies the hidden layer's bias / "
                          "activation / dropout to the encoder partials itself (0: separate row-reduce launch)")
+    ap.add_argument("--epoch-lists", type=int, default=1,
+                    help="weight-gradient row lists built per epoch by the generator (ocf_epoch_row_lists; the "
+                         "timed region includes building them for the timed batches) instead of per step")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -200,7 +206,7 @@ def main():
     from omnidirectional_collaborative_filtering_amd.model import omni_model
 
     t0 = time.time()
-    data_full = synthetic_fixed_split(args.config, seed=0)
+    data_full = synthetic_fixed_split(args.config, seed=0, skew=args.skew)
     N = data_full.num_cols
     n_rows = data_full.train.n_rows
     fp = world > 1 and args.parallel == "feature"
@@ -235,6 +241,7 @@ def main():
     eng.fold_jobs = bool(args.fold_jobs)
     eng.split_dw_streams = bool(args.split_dw)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
+    eng.epoch_row_lists = bool(args.epoch_lists)
     if args.dw_rows >= 0:
         eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
@@ -275,6 +282,11 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     nnz = 0
+    epoch_lists = eng.epoch_row_lists and eng.dw_rows and eng.sparse_dw and eng.use_sparse
+    if epoch_lists:
+        # the timed batches' row lists, built inside the timed region (one launch sequence, as at the
+        # start of every training epoch)
+        gen.prepare_row_lists(eng.Np, [batches[(args.warmup + i) % len(batches)] for i in range(args.steps)])
     # the dominant kernel's HIP events on every TIMER_EVERY-th timed step: each event record idles the
     # stream ~6 us (measured: 0 vs 5.8 us launch gaps with and without), so sampling keeps the timing
     # overhead at ~0.5 % of the step while still averaging over the whole timed region
@@ -375,9 +387,10 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": {"float16": "f16", "bfloat16": "bf16",
                                                           "float32": "f32"}[args.dtype],
-        "data": "synthetic %s-shaped fixed split (%s, %.1fM ratings, seed 0); random-init weights"
+        "data": "synthetic %s-shaped fixed split (%s, %.1fM ratings, seed 0, %s); random-init weights"
                 % (CONFIGS[args.config][1], CONFIGS[args.config][2],
-                   (data_full.train.nnz + data_full.valid_tgt.nnz + data_full.test_tgt.nnz) / 1e6),
+                   (data_full.train.nnz + data_full.valid_tgt.nnz + data_full.test_tgt.nnz) / 1e6,
+                   "popularity ~ rank^-%g" % args.skew if args.skew > 0 else "uniform popularity"),
         "config": {"workload": "%s I-AutoRec train step (BASELINE configs[%d])" % (args.config, CONFIGS[args.config][0]),
                    "rows": n_rows, "N": N,
                    "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
@@ -397,6 +410,9 @@ def main():
                        "every %d-th step)" % (args.warmup, dom, TIMER_EVERY),
         "setup_s": round(setup_s, 1),
         "host_issue_ms_per_step": round(host_ms, 4),
+        "row_lists": ("per epoch: ocf_epoch_row_lists for the %d timed batches inside the timed region"
+                      % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
+                     if epoch_lists else "per step (ocf_row_lists)" if eng.dw_rows else "n/a",
     }
     if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
         line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)

@@ -326,8 +326,9 @@ int ocf_sparse_tiles(const OcfTileBucketArgs* args, void* stream);
  * sp_rowent) straight from the scatter's counts and keys, in parallel over the entries and columns
  * whatever the number of column tiles: row_ptr = exclusive scan of col_cnt (which is zeroed for the
  * next batch), each entry placed at its column's cursor, then every column's list sorted by entry
- * index (= batch-row order; deterministic).  cursor: scratch of 2 n_cols + 128 ints whose first n_cols
- * are zero on entry (and are left zero).
+ * index (= batch-row order; deterministic).  cursor: scratch of 3 n_cols + 256 ints whose first n_cols
+ * are zero on entry (and are left zero).  Lists longer than 32 entries (a column present in that many
+ * batch rows; at most one entry per batch row, so <= 4,096) are sorted by a workgroup each in LDS.
  * With rtag_* / live_*, also the live-row records of ocf_sparse_tiles (OCF_LIVE_REC per 128 rows).
  * Extension (no reference counterpart): feeds the row-stream weight-gradient kernel. */
 typedef struct OcfRowListArgs {
@@ -338,6 +339,31 @@ typedef struct OcfRowListArgs {
   uint8_t* live_in; uint8_t* live_out;
 } OcfRowListArgs;
 int ocf_row_lists(const OcfRowListArgs* args, void* stream);
+
+/* ocf_epoch_row_lists -- the row lists of ocf_row_lists for many batches of an epoch plan at once
+ * (one launch sequence per epoch instead of three small launches per step), built from the plan's
+ * tables rather than a scatter: for each selected batch s (epoch batch sel[s]) and column m,
+ *   row_ent[ebase[s] + row_ptr[s][m] .. ebase[s] + row_ptr[s][m+1]) = (batch-local entry, batch row)
+ * of every source entry of the batch in column m, in entry (= batch-row) order, row_ptr[s] the exclusive
+ * scan of the column counts (row_ptr[s][n_cols] = the batch's entry count), and with live non-null
+ * the OCF_LIVE_REC records of the columns holding at least one entry (a superset of the columns with
+ * a nonzero gradient: an Adagrad l2 = 0 update at g = 0 is the identity, so the row skip stays exact).
+ * B <= 4,096; a batch's entries < 2^31.  cnt: scratch of n_sel * n_cols + 1 + 2 * (entries / 1025 + 1)
+ * ints (counts, then the queue of lists over 1,024 entries).  n_cols % 128 == 0.
+ * Extension (no reference counterpart): the data_reader.py:326-419 batch loop's structure, per epoch. */
+typedef struct OcfEpochRowListArgs {
+  int n_sel; int B; int n_cols;
+  const int32_t* rows;                   /* [nb][B] CSR row of each batch row */
+  const int64_t* rp; const int32_t* col; /* source CSR */
+  const int64_t* lboff;                  /* [nb][B + 1] batch-local entry offsets */
+  const int32_t* sel;                    /* [n_sel] epoch batch index of each slot */
+  const int64_t* ebase;                  /* [n_sel + 1] slot offsets into row_ent (entries) */
+  int32_t* cnt;
+  int32_t* row_ptr;                      /* [n_sel][n_cols + 1] */
+  int32_t* row_ent;                      /* [ebase[n_sel]][2] */
+  uint8_t* live;                         /* [n_sel][n_cols / 128][OCF_LIVE_REC] or null */
+} OcfEpochRowListArgs;
+int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream);
 
 /* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on

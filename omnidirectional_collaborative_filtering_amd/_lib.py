@@ -53,6 +53,13 @@ class OcfRowListArgs(ctypes.Structure):
     ]
 
 
+class OcfEpochRowListArgs(ctypes.Structure):
+    _fields_ = [
+        ("n_sel", I32), ("B", I32), ("n_cols", I32), ("rows", P), ("rp", P), ("col", P), ("lboff", P),
+        ("sel", P), ("ebase", P), ("cnt", P), ("row_ptr", P), ("row_ent", P), ("live", P),
+    ]
+
+
 class OcfGatherArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("col", P), ("val", P), ("lboff", P), ("xval", P), ("flag", P),
@@ -132,6 +139,7 @@ SIGNATURES = {
     "ocf_colsum": (I32, [P, I32, I64, I32, I32, F32, P, P]),
     "ocf_sparse_tiles": (I32, [ctypes.POINTER(OcfTileBucketArgs), P]),
     "ocf_row_lists": (I32, [ctypes.POINTER(OcfRowListArgs), P]),
+    "ocf_epoch_row_lists": (I32, [ctypes.POINTER(OcfEpochRowListArgs), P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),

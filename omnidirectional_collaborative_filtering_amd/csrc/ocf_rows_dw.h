@@ -111,6 +111,9 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
     for (int j = blockIdx.x * 4 + wave; j < nj; j += gridDim.x * 4) jobs.run<KIND>(j, lane);
   }
   const int t = blockIdx.x / PARTS, part = blockIdx.x % PARTS;
+  // workgroups past the last tile exist only for the jobs (a small M with many jobs): no rows, no
+  // record (reading one past the last tile's would name rows of a neighbouring table)
+  if (t >= ra.M / 128) return;
   const int m0 = t * 128;
   const uint8_t* rec = ra.live ? ra.live + (int64_t)t * OCF_LIVE_REC : nullptr;
   const int L = rec ? *reinterpret_cast<const int*>(rec) : (ra.M - m0 < 128 ? ra.M - m0 : 128);

@@ -17,6 +17,7 @@
 // owns one entry at a time and each lane holds PPL 16-byte pieces of the row (pieces l, l+16, ...:
 // every load instruction of a group reads 256 contiguous bytes).  Chunk partials are reduced in a
 // fixed order per row by ocf_rows_reduce, which also applies the layer epilogue.
+#include <algorithm>
 #include <cstdlib>
 
 #include "ocf_epilogues.h"
@@ -684,12 +685,14 @@ __global__ void __launch_bounds__(256) tb_fill_kernel(OcfTileBucketArgs a) {
 // into bsum[]; the later kernels add the block offsets, each computing the (<= 128) offsets in LDS
 constexpr int RL_CHUNK = 4096;
 constexpr int RL_REG = 32;      // lists up to this long are sorted in registers (K = 2,048 rows: ~11 per column)
+constexpr int RL_LONG_BLOCKS = 128;   // workgroups of rl_sort_long_kernel (most batches queue no list)
 __global__ void __launch_bounds__(1024) rl_scan_kernel(OcfRowListArgs a) {
   __shared__ int wtot[16];
   const int n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   int* lp = a.cursor + n;
   int* bsum = a.cursor + 2 * n;
   const int i0 = blockIdx.x * RL_CHUNK + 4 * tid;
+  if (blockIdx.x == 0 && tid == 0) a.cursor[2 * n + 128] = 0;   // this batch's long-list queue (rl_sort)
   int4 v = make_int4(0, 0, 0, 0);
   if (i0 < n) {                          // n % 128 == 0: a thread's 4 columns are all in range or none
     v = *reinterpret_cast<const int4*>(a.col_cnt + i0);
@@ -735,6 +738,27 @@ __global__ void __launch_bounds__(256) rl_fill_kernel(OcfRowListArgs a) {
   reinterpret_cast<int2*>(a.row_ent)[slot] = make_int2((int)e, b);
 }
 
+// short list (the common case): independent loads, an odd-even transposition sort in registers on the
+// entry index (unique; the batch row rides along), independent stores
+template <int S>
+__device__ __forceinline__ void rl_reg_sort(int2* ent, int n) {
+  int2 k[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) k[i] = i < n ? ent[i] : make_int2(0x7fffffff, 0);
+#pragma unroll
+  for (int p = 0; p < S; ++p)
+#pragma unroll
+    for (int i = p & 1; i + 1 < S; i += 2) {
+      const bool sw = k[i + 1].x < k[i].x;
+      const int2 a = k[i], b = k[i + 1];
+      k[i] = sw ? b : a;
+      k[i + 1] = sw ? a : b;
+    }
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (i < n) ent[i] = k[i];
+}
+
 // one thread per column of a 128-column tile: insertion sort of its list by entry index (entry indices
 // grow with the batch row: the list ends in batch-row order, whatever order the fill left), cursor
 // reset; waves 0 / 1 write the tile's live-row records
@@ -754,41 +778,281 @@ __global__ void __launch_bounds__(128) rl_sort_kernel(OcfRowListArgs a) {
   a.cursor[m] = 0;
   int2* ent = reinterpret_cast<int2*>(a.row_ent);
   const int n = hi - lo;
+  // the sorting network's size follows the wave's longest short list (an S-entry network costs S^2 / 2
+  // compare-exchanges whatever n is: 32 entries for every column took 22 us at ML-20M, ~1.4 per column)
+  int nm = n <= RL_REG ? n : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nm = max(nm, __shfl_xor(nm, off, 64));
+  if (n <= 1) return;                    // empty or single-entry lists are in order as filled
   if (n <= RL_REG) {
-    // short list (the common case): independent loads, an odd-even transposition sort in registers on
-    // (entry index, batch row) packed into one 64-bit key, independent stores
-    uint64_t k[RL_REG];
-#pragma unroll
-    for (int i = 0; i < RL_REG; ++i) {
-      const int2 x = i < n ? ent[lo + i] : make_int2(0x7fffffff, 0);
-      k[i] = ((uint64_t)(uint32_t)x.x << 32) | (uint32_t)x.y;
-    }
-#pragma unroll
-    for (int p = 0; p < RL_REG; ++p)
-#pragma unroll
-      for (int i = p & 1; i + 1 < RL_REG; i += 2) {
-        const uint64_t lo_k = k[i] < k[i + 1] ? k[i] : k[i + 1], hi_k = k[i] < k[i + 1] ? k[i + 1] : k[i];
-        k[i] = lo_k;
-        k[i + 1] = hi_k;
-      }
-#pragma unroll
-    for (int i = 0; i < RL_REG; ++i)
-      if (i < n) ent[lo + i] = make_int2((int)(k[i] >> 32), (int)(uint32_t)k[i]);
+    if (nm <= 4) rl_reg_sort<4>(ent + lo, n);
+    else if (nm <= 8) rl_reg_sort<8>(ent + lo, n);
+    else if (nm <= 16) rl_reg_sort<16>(ent + lo, n);
+    else rl_reg_sort<RL_REG>(ent + lo, n);
     return;
   }
-  for (int i = lo + 1; i < hi; ++i) {    // long list: insertion sort in place
-    const int2 x = ent[i];
-    int j = i - 1;
-    for (; j >= lo; --j) {
-      const int2 y = ent[j];
-      if (y.x <= x.x) break;
-      ent[j + 1] = y;
+  // long list (a column present in more than RL_REG batch rows): queued for rl_sort_long_kernel
+  int* q = a.cursor + 2 * a.n_cols + 128;
+  q[1 + atomicAdd(q, 1)] = m;
+}
+
+// Bitonic sort of x[0, n) by .x in a workgroup of NT threads (LDS), all-ascending form: each merge
+// stage first compares i with i ^ (k - 1), then with i ^ j; a partner at or past n is a virtual +inf
+// that never moves, so no padding is needed.  Every thread of the workgroup must call it.
+template <int NT>
+__device__ void wg_bitonic(int2* x, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += NT) {
+        const int ij = j == (k >> 1) ? (i ^ (k - 1)) : (i ^ j);
+        if (ij > i && ij < n) {
+          const int2 a = x[i], b = x[ij];
+          if (a.x > b.x) {
+            x[i] = b;
+            x[ij] = a;
+          }
+        }
+      }
+      __syncthreads();
     }
-    ent[j + 1] = x;
+}
+
+// one workgroup per queued long list: bitonic sort in LDS (a list holds at most one entry per batch
+// row, <= RL_MAX_LIST); the queue length is read after rl_sort_kernel has finished
+constexpr int RL_MAX_LIST = 4096;
+__global__ void __launch_bounds__(256) rl_sort_long_kernel(OcfRowListArgs a) {
+  __shared__ int2 buf[RL_MAX_LIST];
+  const int* q = a.cursor + 2 * a.n_cols + 128;
+  const int nq = q[0];
+  int2* ent = reinterpret_cast<int2*>(a.row_ent);
+  for (int qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    const int m = q[1 + qi];
+    const int lo = a.row_ptr[m], n = a.row_ptr[m + 1] - lo;
+    for (int i = threadIdx.x; i < n; i += 256) buf[i] = ent[lo + i];
+    __syncthreads();
+    wg_bitonic<256>(buf, n);
+    for (int i = threadIdx.x; i < n; i += 256) ent[lo + i] = buf[i];
+    __syncthreads();
+  }
+}
+
+// ---- epoch row lists (ocf_epoch_row_lists): the same lists for many batches, from the plan's tables ----
+// Counting and placement are privatised per (batch, block of columns): the workgroup's waves walk the
+// batch's rows (a wave per row, lanes over its entries) and count / place the entries of the block's
+// columns with LDS atomics (global atomics on per-column counters ran at ~40 G/s: 355 + 429 us for an
+// ML-20M epoch).  The column block is as wide as the LDS allows next to the batch's row table.
+constexpr int ERL_THREADS = 1024;
+constexpr int ERL_MAXB = 4096;
+constexpr int ERL_LDS = 160 * 1024;
+
+// columns per workgroup for batches of B rows: the rest of the LDS after the CSR starts and row offsets
+inline int erl_block_cols(int B) {
+  const int64_t rest = ERL_LDS - (int64_t)B * 8 - (int64_t)(B + 1) * 4 - 64;
+  return (int)std::min<int64_t>(32768, rest / 4 / 128 * 128);
+}
+inline size_t erl_lds_bytes(int B) { return (size_t)erl_block_cols(B) * 4 + (size_t)B * 8 + (size_t)(B + 1) * 4; }
+
+struct ErlLds {
+  int* cnt; int64_t* src; int* off;
+};
+__device__ __forceinline__ ErlLds erl_lds(int B) {
+  extern __shared__ int64_t erl_dyn[];
+  ErlLds l;
+  l.src = erl_dyn;
+  l.off = reinterpret_cast<int*>(erl_dyn + B);
+  l.cnt = l.off + B + 1;
+  return l;
+}
+// stage batch s's CSR starts and batch-local row offsets in LDS
+__device__ __forceinline__ void erl_stage(const OcfEpochRowListArgs& a, int s, const ErlLds& l) {
+  const int bi = a.sel[s];
+  const int64_t* lb = a.lboff + (int64_t)bi * (a.B + 1);
+  for (int b = threadIdx.x; b <= a.B; b += ERL_THREADS) {
+    l.off[b] = (int)lb[b];
+    if (b < a.B) {
+      const int r = a.rows[(int64_t)bi * a.B + b];
+      l.src[b] = r >= 0 ? a.rp[r] : 0;
+    }
+  }
+}
+
+// per (column block, batch): the block's column counts
+__global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListArgs a, int cb) {
+  const ErlLds l = erl_lds(a.B);
+  const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
+  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) l.cnt[i] = 0;
+  erl_stage(a, s, l);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int b = w; b < a.B; b += ERL_THREADS / 64) {
+    const int n = l.off[b + 1] - l.off[b];
+    const int* col = a.col + l.src[b];
+    for (int j = lane; j < n; j += 64) {
+      const int c = col[j] - c0;
+      if (c >= 0 && c < nc) atomicAdd(&l.cnt[c], 1);
+    }
+  }
+  __syncthreads();
+  int* g = a.cnt + (int64_t)s * a.n_cols + c0;
+  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) g[i] = l.cnt[i];
+}
+
+// per batch: exclusive scan of its column counts (4,096 columns per pass, running carry), counts zeroed
+// for the fill's cursors
+__global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
+  __shared__ int wtot[16];
+  __shared__ int carry_s;
+  const int s = blockIdx.x, n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int* cnt = a.cnt + (int64_t)s * n;
+  int* rp = a.row_ptr + (int64_t)s * (n + 1);
+  if (s == 0 && tid == 0) a.cnt[(int64_t)a.n_sel * n] = 0;   // erl_sort's long-list queue
+  int carry = 0;
+  for (int base = 0; base < n; base += 4096) {
+    const int i0 = base + 4 * tid;
+    int4 v = make_int4(0, 0, 0, 0);
+    if (i0 < n) v = *reinterpret_cast<const int4*>(cnt + i0);   // n % 128 == 0: all 4 columns in range or none
+    const int ts = v.x + v.y + v.z + v.w;
+    const int incl = wave_incl_scan(ts, lane);
+    if (lane == 63) wtot[w] = incl;
+    __syncthreads();
+    int off = carry;
+    for (int k = 0; k < w; ++k) off += wtot[k];
+    const int ex = off + incl - ts;
+    if (i0 < n) {
+      rp[i0] = ex;
+      rp[i0 + 1] = ex + v.x;
+      rp[i0 + 2] = ex + v.x + v.y;
+      rp[i0 + 3] = ex + v.x + v.y + v.z;
+    }
+    if (tid == 1023) carry_s = off + incl;
+    __syncthreads();
+    carry = carry_s;
+  }
+  if (tid == 0) rp[n] = carry;
+}
+
+// per (column block, batch): every entry of the block's columns at its column's next slot (LDS cursors;
+// unordered within a column, erl_sort_kernel orders each list)
+__global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListArgs a, int cb) {
+  const ErlLds l = erl_lds(a.B);
+  const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
+  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) l.cnt[i] = 0;
+  erl_stage(a, s, l);
+  __syncthreads();
+  const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
+  int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int b = w; b < a.B; b += ERL_THREADS / 64) {
+    const int e0 = l.off[b], n = l.off[b + 1] - e0;
+    const int* col = a.col + l.src[b];
+    for (int j = lane; j < n; j += 64) {
+      const int c = col[j];
+      if (c >= c0 && c < c0 + nc) ent[rp[c] + atomicAdd(&l.cnt[c - c0], 1)] = make_int2(e0 + j, b);
+    }
+  }
+}
+
+// per (batch, 128-column tile): the tile's live record, every list sorted by entry
+// index -- short lists in registers (rl_reg_sort), up to ERL_MID entries by the workgroup in LDS, longer
+// ones (a column in more than ERL_MID batch rows) queued for erl_sort_long_kernel
+constexpr int ERL_MID = 1024;
+constexpr int ERL_LONG_MAX = 4096;
+__global__ void __launch_bounds__(128) erl_sort_kernel(OcfEpochRowListArgs a) {
+  __shared__ int2 buf[ERL_MID];
+  __shared__ int nlong, n0s;
+  __shared__ int longs[128];
+  const int t = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n_cols = a.n_cols, m = t * 128 + tid;
+  const int* rp = a.row_ptr + (int64_t)s * (n_cols + 1);
+  int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+  const int lo = rp[m], n = rp[m + 1] - lo;
+  if (tid == 0) nlong = 0;
+  const uint64_t bal = __ballot(n > 0);
+  if (w == 0 && lane == 0) n0s = __popcll(bal);
+  __syncthreads();
+  if (a.live) {
+    uint8_t* rec = a.live + ((int64_t)s * (n_cols / 128) + t) * OCF_LIVE_REC;
+    const int k = (w ? n0s : 0) + __popcll(bal & ((1ull << lane) - 1));
+    if (n > 0) rec[16 + (k & 7) * 16 + (k >> 3)] = (uint8_t)tid;
+    if (w == 1 && lane == 0) *reinterpret_cast<int*>(rec) = n0s + __popcll(bal);
+  }
+  int nm = n <= RL_REG ? n : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nm = max(nm, __shfl_xor(nm, off, 64));
+  if (n > 1 && n <= RL_REG) {
+    if (nm <= 4) rl_reg_sort<4>(ent + lo, n);
+    else if (nm <= 8) rl_reg_sort<8>(ent + lo, n);
+    else if (nm <= 16) rl_reg_sort<16>(ent + lo, n);
+    else rl_reg_sort<RL_REG>(ent + lo, n);
+  } else if (n > ERL_MID) {
+    int* q = a.cnt + (int64_t)a.n_sel * n_cols;      // long-list queue after the counters
+    const int qi = atomicAdd(q, 1);
+    q[1 + 2 * qi] = s;
+    q[2 + 2 * qi] = m;
+  } else if (n > RL_REG) {
+    longs[atomicAdd(&nlong, 1)] = tid;
+  }
+  __syncthreads();
+  for (int q = 0; q < nlong; ++q) {        // workgroup-uniform loop over the tile's mid-length lists
+    const int mq = t * 128 + longs[q];
+    const int lq = rp[mq], nq = rp[mq + 1] - lq;
+    for (int i = tid; i < nq; i += 128) buf[i] = ent[lq + i];
+    __syncthreads();
+    wg_bitonic<128>(buf, nq);
+    for (int i = tid; i < nq; i += 128) ent[lq + i] = buf[i];
+    __syncthreads();
+  }
+}
+
+// one workgroup per queued list of more than ERL_MID entries (<= ERL_LONG_MAX: one per batch row)
+__global__ void __launch_bounds__(1024) erl_sort_long_kernel(OcfEpochRowListArgs a) {
+  __shared__ int2 buf[ERL_LONG_MAX];
+  const int* q = a.cnt + (int64_t)a.n_sel * a.n_cols;
+  const int nq = q[0];
+  for (int qi = blockIdx.x; qi < nq; qi += gridDim.x) {
+    const int s = q[1 + 2 * qi], m = q[2 + 2 * qi];
+    const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
+    int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+    const int lo = rp[m], n = rp[m + 1] - lo;
+    for (int i = threadIdx.x; i < n; i += 1024) buf[i] = ent[lo + i];
+    __syncthreads();
+    wg_bitonic<1024>(buf, n);
+    for (int i = threadIdx.x; i < n; i += 1024) ent[lo + i] = buf[i];
+    __syncthreads();
   }
 }
 
 }  // namespace ocf
+
+extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfEpochRowListArgs& a = *args;
+  OCF_CHECK(a.rows && a.rp && a.col && a.lboff && a.sel && a.ebase && a.cnt && a.row_ptr && a.row_ent,
+            "ocf_epoch_row_lists: null pointer");
+  OCF_CHECK(a.n_cols > 0 && a.n_cols % 128 == 0, "ocf_epoch_row_lists: n_cols > 0, % 128");
+  OCF_CHECK(a.B > 0 && a.B <= ERL_MAXB, "ocf_epoch_row_lists: 0 < B <= 4096 (one entry per batch row and column)");
+  OCF_CHECK(a.n_sel >= 0 && a.n_sel <= 65535, "ocf_epoch_row_lists: 0 <= n_sel <= 65535");
+  if (a.n_sel == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int cb = erl_block_cols(a.B), ncb = (a.n_cols + cb - 1) / cb;
+  const size_t lds = erl_lds_bytes(a.B);
+  static const bool lds_attr = [] {   // dynamic LDS above 64 KiB (gfx950: up to 160 KiB per workgroup)
+    return hipFuncSetAttribute((const void*)erl_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ERL_LDS) ==
+               hipSuccess &&
+           hipFuncSetAttribute((const void*)erl_fill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, ERL_LDS) ==
+               hipSuccess;
+  }();
+  OCF_CHECK(lds_attr, "ocf_epoch_row_lists: cannot raise the dynamic LDS limit");
+  hipLaunchKernelGGL(erl_count_kernel, dim3(ncb, a.n_sel), dim3(ERL_THREADS), lds, s, a, cb);
+  hipLaunchKernelGGL(erl_scan_kernel, dim3(a.n_sel), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel), dim3(ERL_THREADS), lds, s, a, cb);
+  hipLaunchKernelGGL(erl_sort_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(erl_sort_long_kernel, dim3(64), dim3(1024), 0, s, a);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
 
 extern "C" int ocf_row_lists(const OcfRowListArgs* args, void* stream) {
   OCF_TRY_BEGIN
@@ -801,6 +1065,7 @@ extern "C" int ocf_row_lists(const OcfRowListArgs* args, void* stream) {
   hipLaunchKernelGGL(rl_scan_kernel, dim3((a.n_cols + RL_CHUNK - 1) / RL_CHUNK), dim3(1024), 0, s, a);
   if (a.E > 0) hipLaunchKernelGGL(rl_fill_kernel, dim3((unsigned)((a.E + 255) / 256)), dim3(256), 0, s, a);
   hipLaunchKernelGGL(rl_sort_kernel, dim3(a.n_cols / 128), dim3(128), 0, s, a);
+  hipLaunchKernelGGL(rl_sort_long_kernel, dim3(RL_LONG_BLOCKS), dim3(256), 0, s, a);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

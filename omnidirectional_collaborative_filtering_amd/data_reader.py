@@ -218,7 +218,9 @@ class BatchGenerator(object):
         j0 = k * chunk
         j1 = np.minimum(j0 + chunk, L[rep])
         t = lambda x: torch.as_tensor(np.ascontiguousarray(x, dtype=np.int32), device=dev)
-        return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase)
+        max_chunks = nc.reshape(nb, B).max(axis=1) if nb else np.zeros(0, np.int64)
+        return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase,
+                    max_chunks=max_chunks)
 
     def gather_tables(self, bi):
         """pointer sets for the row-gather kernels of batch bi: 'enc' (source-1 inputs) and 'dec'
@@ -233,8 +235,61 @@ class BatchGenerator(object):
                             val=ptr(src.val), lboff=lb.data_ptr() + 8 * bi * (B + 1),
                             ch_row=ch["ch_row"].data_ptr() + 4 * c0, ch_j0=ch["ch_j0"].data_ptr() + 4 * c0,
                             ch_j1=ch["ch_j1"].data_ptr() + 4 * c0, n_chunks=int(ch["cbase"][bi + 1]) - c0,
-                            row_cptr=ch["row_cptr"].data_ptr() + 4 * bi * (B + 1))
+                            row_cptr=ch["row_cptr"].data_ptr() + 4 * bi * (B + 1),
+                            max_chunks=int(ch["max_chunks"][bi]))
+        if self.split == "train":      # train batches: inputs = targets -> the weight-gradient row lists
+            out["row_lists"] = lambda n_cols, bi=bi: self.row_lists(bi, n_cols)
         return out
+
+    def prepare_row_lists(self, n_cols, batches=None):
+        """The row lists (per weight row: the batch entries in that column, in batch-row order) and
+        live-row records of the given epoch batches (default: every batch of the epoch), built on the
+        device by one ocf_epoch_row_lists launch sequence instead of per step.  n_cols = the engine's
+        padded column count."""
+        if not self.started:
+            self._start()
+        if self.split != "train":
+            raise ValueError("row lists are built for train batches (inputs = targets)")
+        nb = self.num_batches
+        sel = np.arange(nb, dtype=np.int64) if batches is None else np.unique(np.asarray(batches, dtype=np.int64))
+        if len(sel) and (sel[0] < 0 or sel[-1] >= nb):
+            raise ValueError("batch index out of range")
+        dev = self.rows_dev.device
+        ebase = np.zeros(len(sel) + 1, dtype=np.int64)
+        np.cumsum(self.nnz1[sel], out=ebase[1:])
+        E = int(ebase[-1])
+        # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
+        need = dict(cnt=(len(sel) * n_cols + 1 + 2 * (E // 1025 + 1), torch.int32),
+                    row_ptr=(len(sel) * (n_cols + 1), torch.int32), row_ent=(2 * max(E, 1), torch.int32),
+                    live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8))
+        bufs = getattr(self, "_rl_bufs", None) or {}
+        for k, (n, dt) in need.items():
+            if k not in bufs or bufs[k].numel() < n:
+                bufs[k] = torch.empty(n, dtype=dt, device=dev)
+        self._rl_bufs = bufs
+        keep = dict(sel=torch.as_tensor(sel.astype(np.int32), device=dev), ebase=torch.as_tensor(ebase, device=dev),
+                    row_ptr=bufs["row_ptr"], row_ent=bufs["row_ent"], live=bufs["live"])
+        a = _lib.OcfEpochRowListArgs()
+        a.n_sel, a.B, a.n_cols = len(sel), self.B, n_cols
+        a.rows, a.rp, a.col, a.lboff = ptr(self.rows_dev), ptr(self.src1.rp), ptr(self.src1.col), ptr(self.lboff1_dev)
+        a.sel, a.ebase = ptr(keep["sel"]), ptr(keep["ebase"])
+        a.cnt, a.row_ptr, a.row_ent, a.live = ptr(bufs["cnt"]), ptr(bufs["row_ptr"]), ptr(bufs["row_ent"]), \
+            ptr(bufs["live"])
+        _lib.call("ocf_epoch_row_lists", a, cur_stream())
+        keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
+        self._rl = keep
+
+    def row_lists(self, bi, n_cols):
+        """device pointers of batch bi's row lists (sp_rowptr / sp_rowent of the row-stream weight-gradient
+        kernel) and live records; the whole epoch's are built on first use"""
+        rl = getattr(self, "_rl", None)
+        if rl is None or rl["n_cols"] != n_cols or bi not in rl["slot"]:
+            self.prepare_row_lists(n_cols)
+            rl = self._rl
+        s = rl["slot"][bi]
+        return dict(row_ptr=rl["row_ptr"].data_ptr() + 4 * s * (n_cols + 1),
+                    row_ent=rl["row_ent"].data_ptr() + 8 * int(rl["ebase_host"][s]),
+                    live=rl["live"].data_ptr() + s * (n_cols // 128) * _lib.LIVE_REC)
 
     @staticmethod
     def _local_offsets(lens, rows):

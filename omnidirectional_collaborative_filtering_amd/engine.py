@@ -22,6 +22,7 @@ keeps f16 operands far from underflow.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -30,6 +31,11 @@ from . import _lib
 from ._lib import OcfGemmArgs, OcfScatterArgs, call
 
 TILE = 128
+# the decoder gather re-reduces a row's encoder chunk partials in every one of that row's chunks
+# (O(chunks^2) per row): past this many chunks in a batch row, a separate ocf_rows_reduce runs instead
+# (skewed ML-20M-shaped batch, rows up to ~170 chunks: fused 128 us vs 135 us for the two gathers;
+# a Netflix-sized row of 900 chunks would re-read 1.6 GB of partials)
+FUSE_MAX_CHUNKS = int(os.environ.get("OCF_FUSE_MAX_CHUNKS", 256))
 DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
           "bfloat16": (_lib.DT_BF16, torch.bfloat16)}
 DTYPE_ALIASES = {"f32": "float32", "fp32": "float32", "f16": "float16", "fp16": "float16", "half": "float16",
@@ -288,6 +294,10 @@ class Engine:
         # boundaries to the main chain.  Joined at the end of every step.
         self.side = torch.cuda.Stream(device=d) if d.type == "cuda" else None
         self._side_busy = False
+        # generator batches: the row lists come from the generator's per-epoch build (BatchGenerator.
+        # prepare_row_lists) instead of the per-step ocf_row_lists launches
+        self.epoch_row_lists = os.environ.get("OCF_EPOCH_LISTS", "1") != "0"
+        self._live_ptrs = None
         if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
             self.hpre = torch.zeros(Bp, self.Hp[0], device=d, dtype=torch.float32)
             self.dhpre = torch.zeros(Bp, self.Hp[-1], device=d, dtype=torch.float32)
@@ -439,13 +449,22 @@ class Engine:
         a.tb_cnt, a.tb_nk = None, 0
         a.col_cnt = a.ecb = None
         lists = False
+        epoch_lists = None
         a.rtag_in = a.rtag_out = None
         self._rtag_live = False
+        self._live_ptrs = None
         if gather is not None and self.sparse_ok and self.use_sparse:
             xval = self._buf("xval", int(a.E1))
             a.xval1 = ptr(xval)
             if self.sparse_dw and self.dw_buckets and targets["flag"] == 1:   # train split: inputs = targets
-                if self.dw_rows:
+                rl = gather.get("row_lists") if self.epoch_row_lists else None
+                if self.dw_rows and rl is not None:
+                    # the epoch's row lists and live records, built once per epoch by the generator
+                    # (ocf_epoch_row_lists): no per-step counting, keys or tags
+                    t = rl(self.Np)
+                    epoch_lists = dict(sp_rowptr=t["row_ptr"], sp_rowent=t["row_ent"])
+                    self._live_ptrs = (t["live"], t["live"]) if self.row_skip else None
+                elif self.dw_rows:
                     # per-column counts and entry keys from the scatter -> row lists (ocf_row_lists)
                     a.col_cnt = ptr(self._buf("col_cnt", self.Np, torch.int32))
                     a.ecb = ptr(self._buf("ecb", int(a.E1), torch.int32))
@@ -456,9 +475,12 @@ class Engine:
                     gm, nk = self.Np // TILE, self.Bp // 64
                     self._tb_par ^= 1
                     a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
-                if self.row_skip:
+                if self.row_skip and epoch_lists is None:
                     self._rtag_val = self._rtag_val % 255 + 1
                     a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
+                    self._rtag_live = True
+                    self._live_ptrs = (ptr(self.live_rec[0]), ptr(self.live_rec[1]))
+                elif self._live_ptrs is not None:
                     self._rtag_live = True
             if self.sparse_dw:
                 a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
@@ -466,7 +488,10 @@ class Engine:
         with self.phase("scatter"):
             a.xin_clean = int(self._xin_clean)
             call("ocf_scatter_batch", a, cur_stream())
-            self.tb = self._row_lists(int(a.E1)) if lists else (self._tile_buckets() if a.tb_cnt else None)
+            if epoch_lists is not None:
+                self.tb = epoch_lists
+            else:
+                self.tb = self._row_lists(int(a.E1)) if lists else (self._tile_buckets() if a.tb_cnt else None)
         self._xin_clean = False
 
     def _row_lists(self, E):
@@ -474,7 +499,7 @@ class Engine:
         for the row-stream weight-gradient kernel; shared by dW_out (deltas) and dW_in (inputs)"""
         a = _lib.OcfRowListArgs()
         a.ecb, a.E = ptr(self._buf("ecb", E, torch.int32)), E
-        a.col_cnt, a.cursor = ptr(self._buf("col_cnt", self.Np, torch.int32)), ptr(self._buf("rl_cur", 2 * self.Np + 128, torch.int32))
+        a.col_cnt, a.cursor = ptr(self._buf("col_cnt", self.Np, torch.int32)), ptr(self._buf("rl_cur", 3 * self.Np + 256, torch.int32))
         a.n_cols = self.Np
         rptr = self._buf("tb_rowptr", self.Np + 1, torch.int32)
         rent = self._buf("tb_rowent", 2 * max(E, 1), torch.int32)
@@ -628,7 +653,8 @@ class Engine:
             g = self._gather_args(tab, 0, part, Hp0)
             g.xval = ptr(self.gt["xval"])
             call("ocf_gather_encoder", g, cur_stream())
-            if self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue:
+            if (self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue
+                    and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS):
                 # the decoder gather applies bias / activation / dropout to these partials itself
                 self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id)
                 return
@@ -827,7 +853,7 @@ class Engine:
             sw, _ = self.slots[i]
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             if self._rtag_live and self.sparse_dw and op.kind == _lib.OPT_ADAGRAD and op.l2 == 0:
-                sp.update(row_live=self.live_rec[0 if i == 0 else 1])
+                sp.update(row_live=self._live_ptrs[0 if i == 0 else 1])
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
                        ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
         else:

@@ -160,18 +160,36 @@ def test_rows_kernel_matches_mfma_kernels_and_bias_job(gpu):
 
 
 @pytest.mark.gpu
+def _skewed_entries(rng, ncols, B):
+    """unique (batch row, column) pairs, column popularity ~ rank^-1 (lists from 1 to all B rows), in
+    flat (batch row, column) order"""
+    k = np.minimum(B, (B * 1.3 / np.arange(1, ncols + 1)).astype(np.int64) + 1)
+    c = np.repeat(rng.permutation(ncols), k)
+    b = np.concatenate([rng.choice(B, int(x), replace=False) for x in k])
+    o = np.lexsort((c, b))
+    return b[o], c[o]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ncols,E,B", [(256, 3000, 256), (6144, 69000, 256), (1024, 40000, 2048),
-                                       (138496, 191000, 256)])
+                                       (138496, 191000, 256), (2048, 0, 4096), (1024, 0, 1000)])
 def test_ocf_row_lists_match_numpy(gpu, ncols, E, B):
     """ocf_row_lists (the row lists from the scatter's per-column counts and keys): per column, the
     batch entries in entry order (= batch-row order), row_ptr the exclusive scan of the counts, the
-    counts left zeroed and the cursor scratch left zeroed; the live records as ocf_sparse_tiles'"""
+    counts left zeroed and the cursor scratch left zeroed; the live records as ocf_sparse_tiles'.
+    E = 0: skewed columns (lists up to every batch row: the long-list LDS sort, twice to check its
+    queue is reset)"""
     rng = np.random.RandomState(ncols + E)
-    b = np.sort(rng.randint(0, B, E))                       # entries in batch-row order (flat order)
-    c = rng.randint(0, ncols, E)
+    if E:
+        b = np.sort(rng.randint(0, B, E))                   # entries in batch-row order (flat order)
+        c = rng.randint(0, ncols, E)
+    else:
+        b, c = _skewed_entries(rng, ncols, B)
+        E = len(b)
+        assert np.bincount(c).max() == B
     ecb = torch.as_tensor((c | (b << 19)).astype(np.int32), device="cuda")
     cnt = torch.as_tensor(np.bincount(c, minlength=ncols).astype(np.int32), device="cuda")
-    cur = torch.zeros(2 * ncols + 128, dtype=torch.int32, device="cuda")
+    cur = torch.zeros(3 * ncols + 256, dtype=torch.int32, device="cuda")
     rptr = torch.full((ncols + 1,), -3, dtype=torch.int32, device="cuda")
     rent = torch.full((E, 2), -9, dtype=torch.int32, device="cuda")
     tag = 7
@@ -183,7 +201,11 @@ def test_ocf_row_lists_match_numpy(gpu, ncols, E, B):
     a.ecb, a.E, a.col_cnt, a.cursor, a.n_cols = ecb.data_ptr(), E, cnt.data_ptr(), cur.data_ptr(), ncols
     a.row_ptr, a.row_ent = rptr.data_ptr(), rent.data_ptr()
     a.rtag_in, a.rtag_out, a.rtag, a.live_in, a.live_out = tags_d.data_ptr(), tags_d.data_ptr(), tag, rec.data_ptr(), None
-    _lib.call("ocf_row_lists", a, cur_stream())
+    for rep in range(2):
+        if rep:
+            cnt.copy_(torch.as_tensor(np.bincount(c, minlength=ncols).astype(np.int32)))
+            rent.fill_(-9)
+        _lib.call("ocf_row_lists", a, cur_stream())
     torch.cuda.synchronize()
     want_ptr = np.concatenate([[0], np.cumsum(np.bincount(c, minlength=ncols))])
     np.testing.assert_array_equal(rptr.cpu().numpy(), want_ptr)
@@ -199,3 +221,91 @@ def test_ocf_row_lists_match_numpy(gpu, ncols, E, B):
         assert L == len(live)
         got = [r[t, 16 + (k % 8) * 16 + k // 8] for k in range(L)]
         np.testing.assert_array_equal(got, live)
+
+
+def _gen_for(rows, cols, nnz, B, skew, seed, sparsity=(1.0, 1.0), pass_through=True):
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=seed, skew=skew)
+    data = split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(seed))
+    np.random.seed(seed)
+    rd = data_reader(cols, rows, dataset=data, eval_mode="fixed_split")
+    return rd, rd.data_gen(B, list(sparsity), "train", True, None, -1, pass_through_input_training=pass_through)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols,nnz,B,skew,sel", [
+    (900, 4000, 30000, 128, 0.0, None),          # every batch of the epoch, short lists
+    (3000, 1024, 400000, 512, 1.0, [1, 0, 3]),   # a subset, out of order; lists up to ~500 (LDS bitonic)
+    (5000, 1024, 1500000, 2048, 1.0, None),      # lists over 1,024 entries (long-list queue)
+])
+def test_epoch_row_lists_match_numpy(gpu, rows, cols, nnz, B, skew, sel):
+    """ocf_epoch_row_lists (BatchGenerator.prepare_row_lists): per selected batch and column, the batch's
+    entries in entry (= batch-row) order, row_ptr the exclusive scan of the column counts, the live
+    records = the columns holding an entry; a second build into the same tables agrees"""
+    rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=rows + B)
+    gen._start()
+    Np = (cols + 127) // 128 * 128
+    for rep in range(2):
+        gen.prepare_row_lists(Np, sel)
+        torch.cuda.synchronize()
+        rl = gen._rl
+        csr = gen.src1.host
+        longest = 0
+        for bi in (sel if sel is not None else range(gen.num_batches)):
+            s = rl["slot"][bi]
+            rws = gen.rows_host[bi]
+            lens = np.diff(csr.row_ptr)[rws]
+            lb = np.concatenate([[0], np.cumsum(lens)])
+            e = np.arange(lb[-1])
+            b = np.repeat(np.arange(B), lens)
+            c = csr.col[np.concatenate([np.arange(csr.row_ptr[r], csr.row_ptr[r + 1]) for r in rws])]
+            cnt = np.bincount(c, minlength=Np)
+            longest = max(longest, cnt.max())
+            rp = rl["row_ptr"][s * (Np + 1):(s + 1) * (Np + 1)].cpu().numpy()
+            np.testing.assert_array_equal(rp, np.concatenate([[0], np.cumsum(cnt)]))
+            e0 = int(rl["ebase_host"][s])
+            ent = rl["row_ent"].view(-1, 2)[e0:e0 + len(e)].cpu().numpy()
+            o = np.argsort(c, kind="stable")
+            np.testing.assert_array_equal(ent[:, 0], e[o])
+            np.testing.assert_array_equal(ent[:, 1], b[o])
+            rec = rl["live"].view(-1, Np // 128, _lib.LIVE_REC)[s].cpu().numpy()
+            for t in range(Np // 128):
+                live = np.nonzero(cnt[t * 128:(t + 1) * 128])[0]
+                L = int(rec[t, :4].view(np.int32)[0])
+                assert L == len(live)
+                np.testing.assert_array_equal([rec[t, 16 + (k % 8) * 16 + k // 8] for k in range(L)], live)
+    if B == 2048:
+        assert longest > 1024
+    elif B == 512:
+        assert longest > 32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd,sparsity,pt", [("float16", (1.0, 1.0), True), ("bfloat16", (0.5, 0.9), False)])
+def test_engine_epoch_lists_bit_identical(gpu, cd, sparsity, pt):
+    """Generator training with the epoch row lists (and their structural live records) against the per-step
+    ocf_row_lists (and the scatter's row tags): identical weights, slots and shadows -- also under input
+    corruption, where the epoch records add columns whose every input was dropped (an identity update)."""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B = 900, 4000, 40000, 128
+    out = []
+    for epoch in (False, True):
+        rd, gen = _gen_for(rows, cols, nnz, B, 0.5, seed=11, sparsity=sparsity, pass_through=pt)
+        om = om_ = omni_model(1, 200, cols, B, dense_activation="sigmoid", use_causal_info=False,
+                              dropout_probability=0.2, compute_dtype=cd, seed=4)
+        eng = om.engine
+        eng.epoch_row_lists = epoch
+        m = om.model
+        m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        loss = m.fit_generator(gen, 5, epochs=1, verbose=0).history["loss"][0]
+        assert eng._rtag_live and (getattr(gen, "_rl", None) is not None) == epoch
+        torch.cuda.synchronize()
+        out.append(([loss], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                    [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                    [t.clone() for t in eng.Wsh if t is not None]))
+        del om_
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
