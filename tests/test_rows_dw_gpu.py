@@ -309,3 +309,52 @@ def test_engine_epoch_lists_bit_identical(gpu, cd, sparsity, pt):
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_rows_job_only_workgroups_stay_in_bounds(gpu):
+    """A small weight (M = 128: 8 row workgroups) with more folded jobs than those hold (the step's stats
+    over 512 rows: 513 jobs -> 129 workgroups): the workgroups past the last tile run only their jobs --
+    no live record read past the table (here the next table's valid record), no colsum zeroing past M,
+    no parameter row past M."""
+    M, N, K, krows = 128, 128, 256, 200
+    sp, _ = _sparse_batch(M, K, krows, seed=21)
+    _, _, rptr, rent = _row_lists(sp, M, K)
+    rng = np.random.RandomState(3)
+    state = [torch.as_tensor(rng.uniform(-0.1, 0.1, (M + 256) * N).astype(np.float32), device="cuda"),
+             torch.as_tensor(rng.uniform(0.1, 1.0, (M + 256) * N).astype(np.float32), device="cuda"),
+             torch.zeros((M + 256) * N, device="cuda")]
+    Bm = torch.as_tensor(rng.uniform(-1, 1, (K, N)), device="cuda").to(torch.float16)
+    # two tiles of records: ours, then a neighbour's with every row live
+    rec = torch.zeros(2 * _lib.LIVE_REC, dtype=torch.uint8, device="cuda")
+    live = torch.nonzero(rptr[1:M + 1] > rptr[:M]).flatten().cpu().numpy()
+    r = np.zeros((2, _lib.LIVE_REC), np.uint8)
+    for t, rows in ((0, live), (1, np.arange(128))):
+        r[t, :4] = np.array([len(rows)], np.int32).view(np.uint8)
+        for k, m in enumerate(rows):
+            r[t, 16 + (k % 8) * 16 + k // 8] = m
+    rec.copy_(torch.as_tensor(r.reshape(-1)))
+    js_M = 512
+    cs_guard = torch.full((M + 1024,), -7.0, device="cuda")
+    jobs = dict(js_sp=torch.zeros(8 * 4, device="cuda"), js_nparts=8, js_rs=torch.zeros(2 * js_M, device="cuda"),
+                js_ntiles=2, js_M=js_M, js_out=torch.zeros(4 + js_M, device="cuda"))
+    spr = dict(sp, sp_rowptr=rptr, sp_rowent=rent)
+    spr["row_live"] = rec
+    P0 = [t.clone() for t in state]
+    a = _lib.OcfGemmArgs()
+    cd = _lib.DT_F16
+    a.compute_dtype = cd
+    a.A, a.a_dtype, a.a_col, a.lda = Bm.data_ptr(), cd, 1, M
+    a.B, a.b_dtype, a.b_col, a.ldb = Bm.data_ptr(), cd, 1, N
+    a.M, a.N, a.K, a.splits, a.epi = M, N, K, 1, _lib.EPI_OPTIM
+    a.p, a.ld_out, a.s1 = state[0].data_ptr(), N, state[1].data_ptr()
+    a.opt = OPTS["adagrad"](1.0)
+    a.sp_colsum = cs_guard.data_ptr()
+    a.a_sparse = 1
+    for k, v in list(spr.items()) + list(jobs.items()):
+        setattr(a, k, v.data_ptr() if torch.is_tensor(v) else v)
+    _lib.call("ocf_gemm", a, cur_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(cs_guard[M:], torch.full((1024,), -7.0, device="cuda"))
+    assert torch.equal(state[0][M * N:], P0[0][M * N:]) and torch.equal(state[1][M * N:], P0[1][M * N:])
+    assert not torch.equal(state[0][:M * N], P0[0][:M * N])

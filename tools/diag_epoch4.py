@@ -1,3 +1,6 @@
+# Memory-corruption check for one generator training step: snapshots the generator's device tables, runs the
+# step with a synchronize + comparison after every libocf call, and names the first call that changed one.
+#   python tools/diag_epoch4.py   (on the GPU box)
 import sys, numpy as np, torch
 sys.path.insert(0, '.')
 from tests.parity import dataset, our_opt
