@@ -240,8 +240,9 @@ class Engine:
         # no memsets: row lists for the row-stream kernel, or LDS-filled tiles for the MFMA kernels) or
         # the dense d_out / xin.  With the MFMA kernels the sparse fill pays a chain of dependent index
         # loads per K-step and lost beyond K = 512 (8-way feature-parallel rank step 0.46 vs 0.375 ms);
-        # the row-stream kernel (16-bit compute) has no K-loop and wins up to K = 2,048 (below).
-        self.sparse_dw = Bp <= (2048 if self.cdt != _lib.DT_F32 else 512)
+        # the row-stream kernel (16-bit compute) has no K-loop and wins up to K = 4,096, the row lists'
+        # limit (ML-20M at B = 4,096: 2.14 vs 3.31 ms/step with the dense-operand MFMA GEMMs).
+        self.sparse_dw = Bp <= (4096 if self.cdt != _lib.DT_F32 else 512)
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         # ... and as row lists (the buckets' transpose) for the row-stream kernel (ocf_rows_dw.h): one
         # wave per live weight row streams whole parameter / slot rows and forms the row's gradient from
