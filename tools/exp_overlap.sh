@@ -1,3 +1,4 @@
+# (historical: the --prefetch / --overlap-dw-out switches were removed with the experiment)
 # dW_out on the side stream beside the next batch's load + encoder (bench --prefetch / --overlap-dw-out)
 set -e -o pipefail
 O=gpurun_out/overlap; mkdir -p $O
