@@ -96,13 +96,11 @@ void jobs_after(const OcfGemmArgs& g, hipStream_t s) {
 }
 
 // EPI_OPTIM over a sparse batch operand given as row lists: the row-stream kernel (ocf_rows_dw.h),
-// one wave per weight row.  Takes 16-bit compute, Adagrad / RMSprop / Adam with their slots, N a
+// one wave per weight row.  Takes 16-bit or fp32 compute, Adagrad / RMSprop / Adam with their slots, N a
 // multiple of 128 up to 512 and a row-major shadow; anything else returns false (the tile kernels).
 template <typename CT>
 bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
-  if constexpr (sizeof(CT) != 2) {
-    return false;   // a lane's B elements are one 4- or 8-B load of 16-bit values
-  } else {
+  {   // a lane's B elements are one 4-, 8- or 16-B load (16-bit or fp32 compute)
     const bool kind_ok = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
                          (g.opt.kind == OCF_OPT_ADAM && g.s2);
     if (!(kind_ok && g.s1 && g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N && g.M % 128 == 0))

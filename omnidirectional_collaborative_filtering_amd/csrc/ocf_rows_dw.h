@@ -42,10 +42,16 @@ struct RowsDwArgs {
   float* colsum; float colsum_scale;
 };
 
+// CW consecutive B-operand elements of type CT as one load (4, 8 or 16 bytes)
+template <int BYTES> struct RsBits;
+template <> struct RsBits<4> { using T = uint32_t; };
+template <> struct RsBits<8> { using T = uint2; };
+template <> struct RsBits<16> { using T = uint4; };
+template <typename CT, int CW> using RsH = typename RsBits<CW * (int)sizeof(CT)>::T;
+
 template <int CW> struct RsVec;
 template <> struct RsVec<4> {
   using F = float4;
-  using H = uint2;     // four 16-bit values
   static __device__ __forceinline__ F ld(__amdgpu_buffer_rsrc_t r, const float* base, uint32_t o) {
     return ld_pol16<OCF_OPT_LD_POL>(r, base, o);
   }
@@ -56,7 +62,6 @@ template <> struct RsVec<4> {
 };
 template <> struct RsVec<2> {
   using F = float2;
-  using H = uint32_t;  // two 16-bit values
   static __device__ __forceinline__ F ld(__amdgpu_buffer_rsrc_t r, const float* base, uint32_t o) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     const u2 u = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, OCF_OPT_LD_POL);
@@ -85,9 +90,9 @@ template <> struct RsVec<2> {
 // iteration covers loads a whole iteration old.  Against the p / slot loads one stage earlier (B):
 // 75 vs 113 VGPRs (6 vs 4 waves per SIMD), dW_in 144.5 vs 157.5 us.
 // PARTS = 8 (about 11 rows per wave at ML-20M): 2 and 4 parts 177 / 165 us, 6-12 within noise.
-template <int CW, int NCH, int E0, bool ADAM> struct RpRow {
+template <typename CT, int CW, int NCH, int E0, bool ADAM> struct RpRow {
   using F = typename RsVec<CW>::F;
-  using H = typename RsVec<CW>::H;
+  using H = RsH<CT, CW>;
   int m, lo, n;
   bool lv;
   int2 e[E0];
@@ -101,10 +106,10 @@ template <typename CT, int KIND, int CW, int NCH, int PARTS>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
   using V = RsVec<CW>;
   using F = typename V::F;
-  using H = typename V::H;
+  using H = RsH<CT, CW>;
   constexpr bool ADAM = KIND == OCF_OPT_ADAM;
   constexpr int E0 = RS_E0;
-  using Row = RpRow<CW, NCH, E0, ADAM>;
+  using Row = RpRow<CT, CW, NCH, E0, ADAM>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   {  // folded small jobs (hidden-bias update from the decoder's partials, the step's stats): one per wave
     const int nj = jobs.count();
@@ -237,7 +242,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
         for (int i = 0; i < CW; ++i) hh[i] = CvtT<CT>::to(pf[i]);
         H w;
         __builtin_memcpy(&w, hh, sizeof(w));
-        *reinterpret_cast<H*>(reinterpret_cast<char*>(ra.shadow) + ((int64_t)r.m * ra.ld + col(j)) * 2) = w;
+        *reinterpret_cast<H*>(reinterpret_cast<char*>(ra.shadow) + ((int64_t)r.m * ra.ld + col(j)) * sizeof(CT)) = w;
       }
     }
     if (ra.colsum && lane == 0) {   // output-bias gradient (column sum of the entries) and its update

@@ -240,15 +240,18 @@ class Engine:
         # no memsets: row lists for the row-stream kernel, or LDS-filled tiles for the MFMA kernels) or
         # the dense d_out / xin.  With the MFMA kernels the sparse fill pays a chain of dependent index
         # loads per K-step and lost beyond K = 512 (8-way feature-parallel rank step 0.46 vs 0.375 ms);
-        # the row-stream kernel (16-bit compute) has no K-loop and wins up to K = 4,096, the row lists'
-        # limit (ML-20M at B = 4,096: 2.14 vs 3.31 ms/step with the dense-operand MFMA GEMMs).
-        self.sparse_dw = Bp <= (4096 if self.cdt != _lib.DT_F32 else 512)
+        # the row-stream kernel has no K-loop and wins up to K = 4,096, the row lists' limit (ML-20M at
+        # B = 4,096: 2.14 vs 3.31 ms/step with the dense-operand MFMA GEMMs); it takes first / last layers
+        # of up to 512 hidden units
+        rows_ok = max(self.Hp[0], self.Hp[-1]) <= 512
+        self.sparse_dw = Bp <= (4096 if rows_ok else 2048 if self.cdt != _lib.DT_F32 else 512)
         self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
         # ... and as row lists (the buckets' transpose) for the row-stream kernel (ocf_rows_dw.h): one
         # wave per live weight row streams whole parameter / slot rows and forms the row's gradient from
         # its ~2 entries, no MFMA over the mostly-zero batch operand.  ML-20M step 0.50 -> 0.44 ms
-        # (dW 200 -> 150-165 us per launch).  16-bit compute only (the library falls back otherwise).
-        self.dw_rows = self.cdt != _lib.DT_F32
+        # (dW 200 -> 150-165 us per launch).  16-bit and fp32 compute (fp32: the B rows of h / dh are
+        # fp32, no shadow; the exact-fp32 ML-20M step 1.27 ms on the generic MFMA kernel before).
+        self.dw_rows = rows_ok
 
         # with it, sparse operands pay off up to K = 2,048 (the 8-way feature-parallel global batch):
         # emulated rank steps 4-way 0.353 -> 0.308 ms, 8-way 0.317 -> 0.294 ms vs the dense-operand
