@@ -847,22 +847,24 @@ constexpr int ERL_THREADS = 1024;
 constexpr int ERL_MAXB = 4096;
 constexpr int ERL_LDS = 160 * 1024;
 
-// columns per workgroup for batches of B rows: the rest of the LDS after the CSR starts and row offsets
+// columns per workgroup for batches of B rows: the rest of the LDS after the CSR starts and row offsets,
+// at 16 bits per column (a column holds at most one entry per batch row, B <= 4,096: two counters share
+// a 32-bit word and an atomic add of 1 << 16 (c & 1) never carries into the neighbour)
 inline int erl_block_cols(int B) {
   const int64_t rest = ERL_LDS - (int64_t)B * 8 - (int64_t)(B + 1) * 4 - 64;
-  return (int)std::min<int64_t>(32768, rest / 4 / 128 * 128);
+  return (int)std::min<int64_t>(65536, rest / 2 / 128 * 128);
 }
-inline size_t erl_lds_bytes(int B) { return (size_t)erl_block_cols(B) * 4 + (size_t)B * 8 + (size_t)(B + 1) * 4; }
+inline size_t erl_lds_bytes(int B) { return (size_t)erl_block_cols(B) * 2 + (size_t)B * 8 + (size_t)(B + 1) * 4; }
 
 struct ErlLds {
-  int* cnt; int64_t* src; int* off;
+  uint32_t* cnt; int64_t* src; int* off;   // cnt: 16-bit counters, two per word
 };
 __device__ __forceinline__ ErlLds erl_lds(int B) {
   extern __shared__ int64_t erl_dyn[];
   ErlLds l;
   l.src = erl_dyn;
   l.off = reinterpret_cast<int*>(erl_dyn + B);
-  l.cnt = l.off + B + 1;
+  l.cnt = reinterpret_cast<uint32_t*>(l.off + B + 1);
   return l;
 }
 // stage batch s's CSR starts and batch-local row offsets in LDS
@@ -882,7 +884,7 @@ __device__ __forceinline__ void erl_stage(const OcfEpochRowListArgs& a, int s, c
 __global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListArgs a, int cb) {
   const ErlLds l = erl_lds(a.B);
   const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
-  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) l.cnt[i] = 0;
+  for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;   // nc % 128 == 0
   erl_stage(a, s, l);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -891,12 +893,12 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListA
     const int* col = a.col + l.src[b];
     for (int j = lane; j < n; j += 64) {
       const int c = col[j] - c0;
-      if (c >= 0 && c < nc) atomicAdd(&l.cnt[c], 1);
+      if (c >= 0 && c < nc) atomicAdd(&l.cnt[c >> 1], 1u << (16 * (c & 1)));
     }
   }
   __syncthreads();
   int* g = a.cnt + (int64_t)s * a.n_cols + c0;
-  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) g[i] = l.cnt[i];
+  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) g[i] = (int)((l.cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
 }
 
 // per batch: exclusive scan of its column counts (4,096 columns per pass, running carry), counts zeroed
@@ -938,7 +940,7 @@ __global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
 __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListArgs a, int cb) {
   const ErlLds l = erl_lds(a.B);
   const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
-  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) l.cnt[i] = 0;
+  for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;
   erl_stage(a, s, l);
   __syncthreads();
   const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
@@ -949,7 +951,11 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListAr
     const int* col = a.col + l.src[b];
     for (int j = lane; j < n; j += 64) {
       const int c = col[j];
-      if (c >= c0 && c < c0 + nc) ent[rp[c] + atomicAdd(&l.cnt[c - c0], 1)] = make_int2(e0 + j, b);
+      if (c >= c0 && c < c0 + nc) {
+        const int r = c - c0, sh = 16 * (r & 1);
+        const int pos = (int)((atomicAdd(&l.cnt[r >> 1], 1u << sh) >> sh) & 0xFFFFu);
+        ent[rp[c] + pos] = make_int2(e0 + j, b);
+      }
     }
   }
 }
