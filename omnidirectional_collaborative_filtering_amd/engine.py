@@ -368,10 +368,11 @@ class Engine:
         return s
 
     def _buf(self, name, n, dtype=torch.float32):
-        """grow-only device scratch"""
+        """grow-only device scratch, with 1/4 headroom: per-batch sizes (entries, chunks) vary by a few
+        percent, and every new maximum cost a zero-fill kernel inside the step"""
         t = self._gbuf.get(name)
         if t is None or t.numel() < n:
-            t = torch.zeros(max(n, 1 << 12), device=self.dev, dtype=dtype)
+            t = torch.zeros(max(n + n // 4, 1 << 12), device=self.dev, dtype=dtype)
             self._gbuf[name] = t
         return t
 
