@@ -51,7 +51,9 @@ def ptr(t):
 
 
 def cur_stream():
-    return torch.cuda.current_stream().cuda_stream
+    """the current HIP stream of the current device, as a raw pointer for the C ABI (the torch._C getters:
+    torch.cuda.current_stream() costs ~8 us of Python per call, ~9 calls per training step)"""
+    return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
 def glorot_uniform(rng, fan_in, fan_out):
@@ -584,10 +586,9 @@ class Engine:
         g.order = kw.pop("order", 0)
         g.epi = epi
         g.keep = 1.0
+        T = torch.Tensor
         for k, v in kw.items():
-            if torch.is_tensor(v):
-                v = ptr(v)
-            setattr(g, k, v)
+            setattr(g, k, v.data_ptr() if isinstance(v, T) else v)
         call("ocf_gemm", g, cur_stream())
 
     # ---------------------------------------------------------------- forward
