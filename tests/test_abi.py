@@ -43,7 +43,7 @@ STRUCTS = {
     "OcfOptParams": (_lib.OcfOptParams, ["kind", "lr", "gscale"]),
     "OcfScatterArgs": (_lib.OcfScatterArgs, ["keep1", "s0", "seed", "mode", "rows2", "aux", "ld", "xin_dtype",
                                              "feed", "tile_cnt", "n_tiles", "pos1", "lboff2", "E2", "tflag2", "xin_clean",
-                                             "xval1", "tb_cnt", "tb_nk", "rtag_in", "rtag_out", "rtag"]),
+                                             "xval1", "tb_cnt", "tb_nk", "rtag_in", "rtag_out", "rtag", "col_cnt", "ecb"]),
     "OcfGatherArgs": (_lib.OcfGatherArgs, ["rows", "n_chunks", "ldw", "w_blocked", "H", "part", "aux", "delta_e",
                                            "ld_d", "enc_part", "enc_cptr", "bias_h", "act", "keep", "seed",
                                            "stream", "a_out", "mask_out", "m_real", "n_real"]),
@@ -58,6 +58,10 @@ STRUCTS = {
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
                                                        "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",
                                                        "row_ptr", "row_ent"]),
+    "OcfRowListArgs": (_lib.OcfRowListArgs, ["ecb", "E", "col_cnt", "cursor", "n_cols", "row_ptr", "row_ent", "rtag_in",
+                                             "rtag_out", "rtag", "live_in", "live_out"]),
+    "OcfEpochRowListArgs": (_lib.OcfEpochRowListArgs, ["n_sel", "B", "n_cols", "rows", "rp", "col", "lboff", "sel",
+                                                       "ebase", "cnt", "row_ptr", "row_ent", "live"]),
 }
 
 
