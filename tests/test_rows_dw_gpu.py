@@ -282,24 +282,31 @@ def test_epoch_row_lists_match_numpy(gpu, rows, cols, nnz, B, skew, sel):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cd,sparsity,pt", [("float16", (1.0, 1.0), True), ("bfloat16", (0.5, 0.9), False)])
-def test_engine_epoch_lists_bit_identical(gpu, cd, sparsity, pt):
+@pytest.mark.parametrize("cd,sparsity,pt,shape", [
+    ("float16", (1.0, 1.0), True, (900, 4000, 40000, 128, 0.5)),
+    ("bfloat16", (0.5, 0.9), False, (900, 4000, 40000, 128, 0.5)),
+    ("float32", (1.0, 1.0), True, (900, 4000, 40000, 128, 0.5)),
+    # popular columns in most of 2,048 batch rows: lists sorted by the LDS bitonic and the long-list queue
+    ("float16", (1.0, 1.0), True, (5000, 1024, 1500000, 2048, 1.0)),
+])
+def test_engine_epoch_lists_bit_identical(gpu, cd, sparsity, pt, shape):
     """Generator training with the epoch row lists (and their structural live records) against the per-step
     ocf_row_lists (and the scatter's row tags): identical weights, slots and shadows -- also under input
-    corruption, where the epoch records add columns whose every input was dropped (an identity update)."""
+    corruption, where the epoch records add columns whose every input was dropped (an identity update),
+    and with lists longer than 1,024 entries."""
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     from omnidirectional_collaborative_filtering_amd.model import omni_model
-    rows, cols, nnz, B = 900, 4000, 40000, 128
+    rows, cols, nnz, B, skew = shape
     out = []
     for epoch in (False, True):
-        rd, gen = _gen_for(rows, cols, nnz, B, 0.5, seed=11, sparsity=sparsity, pass_through=pt)
+        rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=11, sparsity=sparsity, pass_through=pt)
         om = om_ = omni_model(1, 200, cols, B, dense_activation="sigmoid", use_causal_info=False,
                               dropout_probability=0.2, compute_dtype=cd, seed=4)
         eng = om.engine
         eng.epoch_row_lists = epoch
         m = om.model
         m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
-        loss = m.fit_generator(gen, 5, epochs=1, verbose=0).history["loss"][0]
+        loss = m.fit_generator(gen, min(5, gen.num_batches), epochs=1, verbose=0).history["loss"][0]
         assert eng._rtag_live and (getattr(gen, "_rl", None) is not None) == epoch
         torch.cuda.synchronize()
         out.append(([loss], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
