@@ -115,7 +115,10 @@ bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s
     ra.shadow = ep.shadow;
     ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
     const WsJobs jb = ws_jobs(g);
-    constexpr int PARTS = 8;
+    // workgroups per 128-row tile (each a twelfth of the tile's live rows): with the 75-VGPR pipeline
+    // (6 waves per SIMD) 12 parts measured best, ML-20M step 0.4243-0.4269 ms against 6 / 8 / 16 / 24 / 32
+    // parts 0.439-0.441 / 0.4332-0.4364 / 0.437 / 0.430 / 0.446
+    constexpr int PARTS = 12;
     const int grid = std::max(g.M / 128 * PARTS, (jb.count() + 3) / 4);
     // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
     auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {

@@ -89,7 +89,7 @@ template <> struct RsVec<2> {
 // only what the previous iteration loaded and the consumers are issued first: the one scalar wait per
 // iteration covers loads a whole iteration old.  Against the p / slot loads one stage earlier (B):
 // 75 vs 113 VGPRs (6 vs 4 waves per SIMD), dW_in 144.5 vs 157.5 us.
-// PARTS = 8 (about 11 rows per wave at ML-20M): 2 and 4 parts 177 / 165 us, 6-12 within noise.
+// PARTS = 12 (about 7 rows per wave at ML-20M; ocf_gemm.hip launch_rows has the sweep).
 template <typename CT, int CW, int NCH, int E0, bool ADAM> struct RpRow {
   using F = typename RsVec<CW>::F;
   using H = RsH<CT, CW>;
