@@ -258,6 +258,11 @@ typedef struct OcfGemmArgs {
    * in place by one wave per row -- no MFMA over the mostly-zero A; with Adagrad and l2 == 0 rows
    * without entries are skipped (identity update).  Requires N % 128 == 0, N <= 512. */
   const int32_t* sp_rowptr; const int32_t* sp_rowent;
+  /* (nullable, OPTIM with the row-stream or role-split kernel) a folded ocf_rows_reduce in mode
+   * OCF_REDUCE_GRAD_ACT: one job per batch row (a wave; the same per-element sums and epilogue), so the
+   * decoder's delta reduction rides in a weight-gradient launch that does not read its outputs (dW_out)
+   * and the launches that do (dW_in, its bias / stats jobs) follow.  The struct is copied at the call. */
+  const OcfRowsReduceArgs* jr;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

@@ -77,11 +77,18 @@ WsJobs ws_jobs(const OcfGemmArgs& g) {
   j.jb_s1 = g.jb_s1; j.jb_s2 = g.jb_s2; j.jb_op = g.jb_op;
   j.js_sp = g.js_sp; j.js_rs = g.js_rs; j.js_out = g.js_out; j.js_nparts = g.js_nparts; j.js_ntiles = g.js_ntiles;
   j.js_M = g.js_M;
+  if (g.jr) {
+    OCF_CHECK(g.jr->mode == OCF_REDUCE_GRAD_ACT && g.jr->part && g.jr->row_cptr && g.jr->h_out && g.jr->a_in,
+              "ocf_gemm: the folded row reduction (jr) takes OCF_REDUCE_GRAD_ACT with part, row_cptr, h_out, a_in");
+    j.jr = *g.jr;
+    j.jr_on = 1;
+  }
   return j;
 }
 
 // the folded jobs as separate launches (generic kernel path): before / after the GEMM
 void jobs_before(const OcfGemmArgs& g, hipStream_t s) {
+  if (g.jr) OCF_CHECK(ocf_rows_reduce(g.jr, s) == 0, ocf_last_error());
   if (g.jb_part)
     OCF_CHECK(ocf_bias_opt_from_partials(g.jb_p, g.jb_part, g.jb_parts, g.jb_ld, g.jb_n, g.jb_s1, g.jb_s2, nullptr,
                                          &g.jb_op, s) == 0, ocf_last_error());

@@ -203,9 +203,11 @@ struct WsJobs {
   const float* jb_part; int jb_parts, jb_n; int64_t jb_ld; float* jb_p; float* jb_s1; float* jb_s2;
   OcfOptParams jb_op;
   const float* js_sp; const float* js_rs; float* js_out; int js_nparts, js_ntiles, js_M;
+  OcfRowsReduceArgs jr; int jr_on;   // folded ocf_rows_reduce (GRAD_ACT): one job per batch row
 
   __host__ __device__ __forceinline__ int count() const {
-    int n = jb_part ? (jb_n + 63) / 64 : 0;
+    int n = jr_on ? jr.Bp : 0;
+    n += jb_part ? (jb_n + 63) / 64 : 0;
     if (js_sp) n += 1 + (js_rs ? js_M : 0);
     return n;
   }
@@ -269,8 +271,38 @@ struct WsJobs {
     for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
     if (lane == 0) js_out[4 + m] = r;
   }
+  // rows_reduce_kernel (OCF_REDUCE_GRAD_ACT) for batch row b by one wave: lane l plays the threads
+  // x = l, l + 64, ... of the 256-thread workgroup (the same sums, in the same chunk order)
+  __device__ __forceinline__ void reduce_row(int b, int lane) const {
+    const bool real = b < jr.B;
+    const int c0 = real ? jr.row_cptr[b] : 0, c1 = real ? jr.row_cptr[b + 1] : 0;
+    GradActParams p;
+    p.a = jr.a_in; p.mask = jr.mask_in; p.keep = jr.keep; p.act = jr.act; p.d_out = jr.h_out; p.d_dtype = jr.h_dtype;
+    p.ld = jr.H; p.db_part = nullptr; p.gscale = jr.gscale; p.m_real = jr.B; p.n_real = jr.n_real;
+    for (int x = lane; x < jr.H; x += 64) {
+      float v = 0.f;
+      for (int c = c0; c < c1; ++c) v += jr.part[(int64_t)c * jr.H + x];
+      const float d = grad_act_value(p, b, x, v);
+      store_ct(jr.h_out, jr.h_dtype, (int64_t)b * jr.H + x, d);
+      if (jr.db_part) jr.db_part[(int64_t)b * jr.H + x] = d * jr.gscale;
+    }
+    if (jr.chunk_stats && lane < 4) {
+      float v = 0.f;
+      if (lane < 3)
+        for (int c = c0; c < c1; ++c) v += jr.chunk_stats[(int64_t)c * 4 + lane];
+      jr.stats_part[(int64_t)b * 4 + lane] = v;
+      if (lane == 0 && jr.row_sse) jr.row_sse[b] = v;
+    }
+  }
   template <int KIND>
   __device__ __forceinline__ void run(int j, int lane) const {
+    if (jr_on) {
+      if (j < jr.Bp) {
+        reduce_row(j, lane);
+        return;
+      }
+      j -= jr.Bp;
+    }
     const int nbj = jb_part ? (jb_n + 63) / 64 : 0;
     if (j < nbj) bias_block<KIND>(j, lane);
     else if (j == nbj) stats_totals(lane);

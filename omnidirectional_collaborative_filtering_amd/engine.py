@@ -21,6 +21,7 @@ keeps f16 operands far from underflow.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 
@@ -303,6 +304,10 @@ class Engine:
         # generator batches: the row lists come from the generator's per-epoch build (BatchGenerator.
         # prepare_row_lists) instead of the per-step ocf_row_lists launches
         self.epoch_row_lists = os.environ.get("OCF_EPOCH_LISTS", "1") != "0"
+        # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
+        self.fold_reduce = os.environ.get("OCF_FOLD_REDUCE", "1") != "0"
+        self._reduce_job = None
+        self._fused_step = False
         self._live_ptrs = None
         if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
             self.hpre = torch.zeros(Bp, self.Hp[0], device=d, dtype=torch.float32)
@@ -708,7 +713,12 @@ class Engine:
             r = self._reduce_args(tab, part, HpL, _lib.REDUCE_RAW)
             r.out = ptr(self.dhpre if (with_grad and self.comm is not None) else self.dh_raw)
         r.chunk_stats, r.stats_part, r.row_sse = ptr(cst), ptr(self.stats_rows), ptr(self.row_sse_rows)
-        call("ocf_rows_reduce", r, cur_stream())
+        self._reduce_job = None
+        if (with_grad and self.comm is None and self._fused_step and self.fold_reduce and self._folds()
+                and self.trainable[0]):
+            self._reduce_job = r          # rides in the dW_out launch (OcfGemmArgs jr), see _backward_gather
+        else:
+            call("ocf_rows_reduce", r, cur_stream())
 
     def output_loss(self, with_grad):
         """Decoder (dense GEMM with the fused masked-MSE epilogue, or the row gather for sparse
@@ -910,25 +920,33 @@ class Engine:
         else:
             db_last, parts_last = self.db_rows, Bp
         if fused and self._folds():
-            # dW_out also: output-bias gradient (column sums of the deltas) and its update, the
-            # hidden-bias update from the decoder's row partials, the step's stats
-            jobs = {}
+            # dW_out also: output-bias gradient (column sums of the deltas) and its update, and -- when the
+            # decoder's row reduction rides here too (jr: it writes δh, the hidden-bias rows and the stats
+            # rows, which dW_out does not read) -- nothing else; the hidden-bias update from the δh rows
+            # and the step's stats then ride in dW_in, after it.  Without jr all of them ride in dW_out.
+            jobs_out, jobs_in = {}, {}
             if self.trainable[1]:
                 sb = self.slots[1][1]
-                jobs.update(cb_p=self.b[1], cb_s1=sb[0], cb_s2=sb[1], cb_op=self._bias_op)
+                jobs_out.update(cb_p=self.b[1], cb_s1=sb[0], cb_s2=sb[1], cb_op=self._bias_op)
+            late = jobs_out
+            if self._reduce_job is not None:
+                jobs_out.update(jr=ctypes.addressof(self._reduce_job))
+                late = jobs_in
             if self.trainable[0]:
                 sb = self.slots[0][1]
-                jobs.update(jb_part=db_last, jb_parts=parts_last, jb_ld=HpL, jb_n=HpL, jb_p=self.b[0], jb_s1=sb[0],
+                late.update(jb_part=db_last, jb_parts=parts_last, jb_ld=HpL, jb_n=HpL, jb_p=self.b[0], jb_s1=sb[0],
                             jb_s2=sb[1], jb_op=self._bias_op)
             if self._stats_pending is not None:
                 sp, n_sp, rs, n_rs, M, dst = self._stats_pending
-                jobs.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
+                late.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
                 self._stats_pending = None
             with self.phase("dW_out"):
                 self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
-                                           jobs=jobs)
+                                           jobs=jobs_out)
             with self.phase("dW_in"):
-                self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
+                self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op,
+                                           jobs=jobs_in)
+            self._reduce_job = None
             self.opt.iterations += 1
             return
         self._flush_stats()
@@ -1028,6 +1046,7 @@ class Engine:
 
     # ---------------------------------------------------------------- steps
     def train_step(self, grads_out=None):
+        self._fused_step = grads_out is None
         if self.l2:
             self._l2_penalty()
         self.forward(training=True)

@@ -365,3 +365,31 @@ def test_rows_job_only_workgroups_stay_in_bounds(gpu):
     assert torch.equal(cs_guard[M:], torch.full((1024,), -7.0, device="cuda"))
     assert torch.equal(state[0][M * N:], P0[0][M * N:]) and torch.equal(state[1][M * N:], P0[1][M * N:])
     assert not torch.equal(state[0][:M * N], P0[0][:M * N])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float16", "float32"])
+def test_engine_fold_reduce_bit_identical(gpu, cd):
+    """The decoder's δh row reduction as jobs of the dW_out launch (Engine.fold_reduce; the hidden-bias and
+    stats jobs then ride in dW_in) against its own ocf_rows_reduce launch: identical losses, weights, slots,
+    shadows and per-step stats."""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    out = []
+    for fold in (False, True):
+        rd, gen = _gen_for(900, 4000, 60000, 128, 0.5, seed=8)
+        om = om_ = omni_model(1, 200, 4000, 128, dense_activation="sigmoid", use_causal_info=False,
+                              dropout_probability=0.2, compute_dtype=cd, seed=4)
+        eng = om.engine
+        eng.fold_reduce = fold
+        m = om.model
+        m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        h = m.fit_generator(gen, 5, epochs=1, verbose=0).history
+        torch.cuda.synchronize()
+        out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                    [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                    [t.clone() for t in eng.Wsh if t is not None]))
+        del om_
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
