@@ -115,6 +115,19 @@ typedef struct OcfScatterArgs {
 
 int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
 
+/* ocf_epoch_scatter -- ocf_scatter_batch's per-entry outputs (xval1: live input value, tflag1: live target)
+ * for many train batches of an epoch plan in one launch: base is batch 0's OcfScatterArgs (mode 0, no
+ * dense / xin / bucket / count / tag outputs, E2 = 0); batch sel[s] uses base's rows1 / lboff1 / boff1
+ * offset by that batch, keep1 + keep_off[sel[s]], stream = stream_mul * (sel[s] + 1) (the per-step
+ * generator's seeds) and writes xval / tflag at ebase[s] .. ebase[s + 1]; max_e = max entries of a batch.
+ * Extension (no reference counterpart): the data_reader.py:95-200 batch assembly, per epoch. */
+typedef struct OcfEpochScatterArgs {
+  int n_sel; const int32_t* sel; const int64_t* ebase; int64_t max_e;
+  const int64_t* keep_off; uint64_t stream_mul;
+  float* xval; uint8_t* tflag;
+} OcfEpochScatterArgs;
+int ocf_epoch_scatter(const OcfScatterArgs* base, const OcfEpochScatterArgs* ep, void* stream);
+
 /*
  * Row-gather products for sparse batches (csrc/ocf_sparse.hip): the encoder sum over a batch row's
  * live input entries, and the decoder's per-target forward / loss / delta with the delta times W_out

@@ -53,6 +53,13 @@ class OcfRowListArgs(ctypes.Structure):
     ]
 
 
+class OcfEpochScatterArgs(ctypes.Structure):
+    _fields_ = [
+        ("n_sel", I32), ("sel", P), ("ebase", P), ("max_e", I64), ("keep_off", P), ("stream_mul", U64),
+        ("xval", P), ("tflag", P),
+    ]
+
+
 class OcfEpochRowListArgs(ctypes.Structure):
     _fields_ = [
         ("n_sel", I32), ("B", I32), ("n_cols", I32), ("rows", P), ("rp", P), ("col", P), ("lboff", P),
@@ -140,6 +147,7 @@ SIGNATURES = {
     "ocf_sparse_tiles": (I32, [ctypes.POINTER(OcfTileBucketArgs), P]),
     "ocf_row_lists": (I32, [ctypes.POINTER(OcfRowListArgs), P]),
     "ocf_epoch_row_lists": (I32, [ctypes.POINTER(OcfEpochRowListArgs), P]),
+    "ocf_epoch_scatter": (I32, [ctypes.POINTER(OcfScatterArgs), ctypes.POINTER(OcfEpochScatterArgs), P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),

@@ -67,15 +67,9 @@ __device__ __forceinline__ int find_row(const int64_t* off, int B, int64_t e) {
   return lo;
 }
 
-__global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a, int nblk1) {
-  extern __shared__ int64_t sh_off[];
-  const bool src2 = (int)blockIdx.x >= nblk1;
-  const int64_t* lboff = src2 ? a.lboff2 : (a.lboff1 ? a.lboff1 : a.boff1);
+// one batch entry e (of source 1 or 2) with the batch offsets staged in LDS
+__device__ __forceinline__ void scatter_entry(const ScatterArgs& a, const int64_t* sh_off, bool src2, int64_t e) {
   const int B = a.B;
-  for (int i = threadIdx.x; i <= B; i += SC_THREADS) sh_off[i] = lboff[i];
-  __syncthreads();
-  const int64_t e = (int64_t)(src2 ? (int)blockIdx.x - nblk1 : (int)blockIdx.x) * SC_THREADS + threadIdx.x;
-  if (e >= (src2 ? a.E2 : a.E1)) return;
   const int b = find_row(sh_off, B, e);
   const int64_t j = e - sh_off[b];
   const float aux = a.aux;
@@ -149,6 +143,39 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a,
   }
 }
 
+
+__global__ void __launch_bounds__(SC_THREADS) scatter_flat_kernel(ScatterArgs a, int nblk1) {
+  extern __shared__ int64_t sh_off[];
+  const bool src2 = (int)blockIdx.x >= nblk1;
+  const int64_t* lboff = src2 ? a.lboff2 : (a.lboff1 ? a.lboff1 : a.boff1);
+  for (int i = threadIdx.x; i <= a.B; i += SC_THREADS) sh_off[i] = lboff[i];
+  __syncthreads();
+  const int64_t e = (int64_t)(src2 ? (int)blockIdx.x - nblk1 : (int)blockIdx.x) * SC_THREADS + threadIdx.x;
+  if (e >= (src2 ? a.E2 : a.E1)) return;
+  scatter_entry(a, sh_off, src2, e);
+}
+
+// every selected batch of an epoch plan at once (ocf_epoch_scatter): base holds batch 0's pointers; slot s
+// (epoch batch sel[s]) offsets them and writes its entries' xval / live-target flags at ebase[s]
+__global__ void __launch_bounds__(SC_THREADS) scatter_epoch_kernel(ScatterArgs base, OcfEpochScatterArgs ep) {
+  extern __shared__ int64_t sh_off[];
+  const int s = blockIdx.y, bi = ep.sel[s];
+  ScatterArgs a = base;
+  a.rows1 = base.rows1 + (int64_t)bi * base.B;
+  a.lboff1 = base.lboff1 ? base.lboff1 + (int64_t)bi * (base.B + 1) : nullptr;
+  a.boff1 = base.boff1 ? base.boff1 + (int64_t)bi * (base.B + 1) : nullptr;
+  a.keep1 = base.keep1 ? base.keep1 + ep.keep_off[bi] : nullptr;
+  a.stream = ep.stream_mul * (uint64_t)(bi + 1);
+  a.E1 = ep.ebase[s + 1] - ep.ebase[s];
+  a.xval1 = ep.xval + ep.ebase[s];
+  a.tflag1 = ep.tflag + ep.ebase[s];
+  const int64_t* lboff = a.lboff1 ? a.lboff1 : a.boff1;
+  for (int i = threadIdx.x; i <= a.B; i += SC_THREADS) sh_off[i] = lboff[i];
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * SC_THREADS + threadIdx.x;
+  if (e >= a.E1) return;
+  scatter_entry(a, sh_off, false, e);
+}
 
 // exclusive scan of per-tile target counts -> bucket pointers; resets counts for next batch
 __global__ void __launch_bounds__(1024) bucket_scan_kernel(int* tile_cnt, int* bk_ptr, int* bk_cur, int n_tiles) {
@@ -261,6 +288,25 @@ __global__ void pack_input_kernel(const float* s0, const float* s1, const float*
 }  // namespace ocf
 
 using namespace ocf;
+
+extern "C" int ocf_epoch_scatter(const ScatterArgs* base, const OcfEpochScatterArgs* ep, void* stream) {
+  OCF_TRY_BEGIN
+  const ScatterArgs& a = *base;
+  const OcfEpochScatterArgs& e = *ep;
+  OCF_CHECK(a.mode == 0 && a.rows1 && a.rp1 && a.col1 && a.val1 && (a.lboff1 || a.boff1),
+            "ocf_epoch_scatter: a train-mode base with source-1 tables");
+  OCF_CHECK(!a.X && !a.Min && !a.Mout && !a.T && !a.Mmiss && !a.xin && !a.tile_cnt && !a.tb_cnt && !a.col_cnt &&
+                !a.rtag_in && !a.rtag_out && !a.E2,
+            "ocf_epoch_scatter: only the per-entry outputs (xval, live-target flags) are produced");
+  OCF_CHECK(e.sel && e.ebase && e.xval && e.tflag && (!a.keep1 || e.keep_off), "ocf_epoch_scatter: null pointer");
+  OCF_CHECK(e.n_sel >= 0 && e.n_sel <= 65535 && a.B >= 0 && a.B <= 16384, "ocf_epoch_scatter: sizes");
+  if (e.n_sel == 0 || e.max_e == 0) return 0;
+  const int nblk = (int)((e.max_e + SC_THREADS - 1) / SC_THREADS);
+  hipLaunchKernelGGL(scatter_epoch_kernel, dim3(nblk, e.n_sel), dim3(SC_THREADS), (size_t)(a.B + 1) * sizeof(int64_t),
+                     (hipStream_t)stream, a, e);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
 
 extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
   OCF_TRY_BEGIN

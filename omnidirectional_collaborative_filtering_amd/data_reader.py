@@ -261,7 +261,8 @@ class BatchGenerator(object):
         # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
         need = dict(cnt=(len(sel) * n_cols + 1 + 2 * (E // 1025 + 1), torch.int32),
                     row_ptr=(len(sel) * (n_cols + 1), torch.int32), row_ent=(2 * max(E, 1), torch.int32),
-                    live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8))
+                    live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
+                    xval=(max(E, 1), torch.float32), tflag=(max(E, 1), torch.uint8))
         bufs = getattr(self, "_rl_bufs", None) or {}
         for k, (n, dt) in need.items():
             if k not in bufs or bufs[k].numel() < n:
@@ -276,6 +277,19 @@ class BatchGenerator(object):
         a.cnt, a.row_ptr, a.row_ent, a.live = ptr(bufs["cnt"]), ptr(bufs["row_ptr"]), ptr(bufs["row_ent"]), \
             ptr(bufs["live"])
         _lib.call("ocf_epoch_row_lists", a, cur_stream())
+        # ... and the batches' per-entry scatter outputs (live input value, live-target flag): the per-step
+        # ocf_scatter_batch has nothing left to do for them
+        base = self.scatter_args(0)
+        es = _lib.OcfEpochScatterArgs()
+        if self.keep_dev is not None:
+            keep["keep_off"] = torch.as_tensor(np.ascontiguousarray(self.keep_off, dtype=np.int64), device=dev)
+            es.keep_off = ptr(keep["keep_off"])
+        es.n_sel, es.sel, es.ebase = len(sel), ptr(keep["sel"]), ptr(keep["ebase"])
+        es.max_e = int(self.nnz1[sel].max()) if len(sel) else 0
+        es.stream_mul = 2
+        es.xval, es.tflag = ptr(bufs["xval"]), ptr(bufs["tflag"])
+        _lib.call("ocf_epoch_scatter", base, es, cur_stream())
+        keep.update(xval=bufs["xval"], tflag=bufs["tflag"])
         keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
         self._rl = keep
 
@@ -287,9 +301,11 @@ class BatchGenerator(object):
             self.prepare_row_lists(n_cols)
             rl = self._rl
         s = rl["slot"][bi]
+        e0 = int(rl["ebase_host"][s])
         return dict(row_ptr=rl["row_ptr"].data_ptr() + 4 * s * (n_cols + 1),
-                    row_ent=rl["row_ent"].data_ptr() + 8 * int(rl["ebase_host"][s]),
-                    live=rl["live"].data_ptr() + s * (n_cols // 128) * _lib.LIVE_REC)
+                    row_ent=rl["row_ent"].data_ptr() + 8 * e0,
+                    live=rl["live"].data_ptr() + s * (n_cols // 128) * _lib.LIVE_REC,
+                    xval=rl["xval"].data_ptr() + 4 * e0, tflag=rl["tflag"].data_ptr() + e0)
 
     @staticmethod
     def _local_offsets(lens, rows):

@@ -304,6 +304,7 @@ class Engine:
         # generator batches: the row lists come from the generator's per-epoch build (BatchGenerator.
         # prepare_row_lists) instead of the per-step ocf_row_lists launches
         self.epoch_row_lists = os.environ.get("OCF_EPOCH_LISTS", "1") != "0"
+        self.epoch_scatter = os.environ.get("OCF_EPOCH_SCATTER", "1") != "0"   # ... and their scatter outputs
         # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
         self.fold_reduce = os.environ.get("OCF_FOLD_REDUCE", "1") != "0"
         self._reduce_job = None
@@ -462,6 +463,7 @@ class Engine:
         a.col_cnt = a.ecb = None
         lists = False
         epoch_lists = None
+        epoch_entries = None
         a.rtag_in = a.rtag_out = None
         self._rtag_live = False
         self._live_ptrs = None
@@ -476,6 +478,9 @@ class Engine:
                     t = rl(self.Np)
                     epoch_lists = dict(sp_rowptr=t["row_ptr"], sp_rowent=t["row_ent"])
                     self._live_ptrs = (t["live"], t["live"]) if self.row_skip else None
+                    # ... and the batch's scatter outputs (ocf_epoch_scatter): no per-step scatter
+                    if self.epoch_scatter:
+                        epoch_entries = dict(xval=t["xval"], flag=t["tflag"])
                 elif self.dw_rows:
                     # per-column counts and entry keys from the scatter -> row lists (ocf_row_lists)
                     a.col_cnt = ptr(self._buf("col_cnt", self.Np, torch.int32))
@@ -497,9 +502,12 @@ class Engine:
             if self.sparse_dw:
                 a.xin = None          # no dense layer-0 input: encoder and dW_in read the entries
             self.gt = dict(gather, xval=xval, aux=float(targets["t_aux"]), E=int(targets["E"]))
+            if epoch_entries is not None:
+                self.gt.update(epoch_entries)
         with self.phase("scatter"):
-            a.xin_clean = int(self._xin_clean)
-            call("ocf_scatter_batch", a, cur_stream())
+            if epoch_entries is None:
+                a.xin_clean = int(self._xin_clean)
+                call("ocf_scatter_batch", a, cur_stream())
             if epoch_lists is not None:
                 self.tb = epoch_lists
             else:
@@ -662,7 +670,8 @@ class Engine:
         part = self._buf("part_enc", tab["n_chunks"] * Hp0)
         with self.phase("enc_gemm"):
             g = self._gather_args(tab, 0, part, Hp0)
-            g.xval = ptr(self.gt["xval"])
+            xv = self.gt["xval"]
+            g.xval = xv if isinstance(xv, int) else ptr(xv)
             call("ocf_gather_encoder", g, cur_stream())
             if (self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue
                     and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS):
@@ -688,7 +697,7 @@ class Engine:
         part = self._buf("part_dec", tab["n_chunks"] * HpL)
         cst = self._buf("chunk_stats", tab["n_chunks"] * 4)
         g = self._gather_args(tab, L, part, HpL)
-        g.flag = ptr(self.tflag)
+        g.flag = self.gt.get("flag") or ptr(self.tflag)
         g.h, g.h_dtype, g.bias, g.aux = ptr(self.h[L - 1]), self.cdt, ptr(self.b[L]), self.gt["aux"]
         g.chunk_stats = ptr(cst)
         ef, self._enc_fused = self._enc_fused, None
