@@ -62,6 +62,8 @@ STRUCTS = {
                                              "rtag_out", "rtag", "live_in", "live_out"]),
     "OcfEpochRowListArgs": (_lib.OcfEpochRowListArgs, ["n_sel", "B", "n_cols", "rows", "rp", "col", "lboff", "sel",
                                                        "ebase", "cnt", "row_ptr", "row_ent", "live"]),
+    "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
+                                                       "xval", "tflag"]),
 }
 
 
