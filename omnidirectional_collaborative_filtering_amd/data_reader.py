@@ -279,7 +279,7 @@ class BatchGenerator(object):
         _lib.call("ocf_epoch_row_lists", a, cur_stream())
         # ... and the batches' per-entry scatter outputs (live input value, live-target flag): the per-step
         # ocf_scatter_batch has nothing left to do for them
-        base = self.scatter_args(0)
+        base = self.scatter_args(0) if nb else _lib.OcfScatterArgs()
         es = _lib.OcfEpochScatterArgs()
         if self.keep_dev is not None:
             keep["keep_off"] = torch.as_tensor(np.ascontiguousarray(self.keep_off, dtype=np.int64), device=dev)
@@ -288,7 +288,8 @@ class BatchGenerator(object):
         es.max_e = int(self.nnz1[sel].max()) if len(sel) else 0
         es.stream_mul = 2
         es.xval, es.tflag = ptr(bufs["xval"]), ptr(bufs["tflag"])
-        _lib.call("ocf_epoch_scatter", base, es, cur_stream())
+        if len(sel):
+            _lib.call("ocf_epoch_scatter", base, es, cur_stream())
         keep.update(xval=bufs["xval"], tflag=bufs["tflag"])
         keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
         self._rl = keep
