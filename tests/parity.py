@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 
 from oracle.batch_oracle import scatter_rows_numpy
-from oracle.model_oracle import AdagradOracle, AdamOracle, OmniOracle, RMSpropOracle
+from oracle.model_oracle import AdagradOracle, AdamOracle, OmniOracle, RMSpropOracle  # noqa: F401
 
 FP32_ABS = 1e-5
 UNIT_ROUNDOFF = {"float16": 2.0 ** -11, "bfloat16": 2.0 ** -8, "float32": 2.0 ** -24}
@@ -179,6 +179,122 @@ def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_
                   reader=rd, masks=masks)
 
 
+def replay_train_draws(lens, n_rows, B, sparsity, shuffle=True):
+    """The reference's own NumPy calls for one training generator, in its order (independent of the
+    product's restatement in BatchGenerator.plan): np.random.permutation of the row set
+    (data_reader.py:326-327), then per batch np.random.uniform for the row sparsities (:120) and one
+    np.random.choice([0, 1], p=[1-s, s]) per row (:130).  Returns (rows [nb][B], keep [nb] -> bool
+    per entry of the batch in CSR order)."""
+    order = np.random.permutation(n_rows) if shuffle else np.arange(n_rows)
+    nb = n_rows // B
+    rows, keeps = [], []
+    for bi in range(nb):
+        r = order[bi * B:(bi + 1) * B]
+        s = np.random.uniform(low=sparsity[0], high=sparsity[1], size=B)
+        k = [np.random.choice([0, 1], size=int(lens[x]), p=[1 - s[j], s[j]]) for j, x in enumerate(r)]
+        rows.append(r)
+        keeps.append(np.concatenate(k).astype(bool) if k else np.zeros(0, bool))
+    return rows, keeps
+
+
+def with_duplicates(rows, cols, nnz, dup_frac=0.03, half_stars=True, seed=0):
+    """synthetic ratings with the reference's own data hazards: a fraction of (row, col) pairs rated twice
+    with a different value (data_reader.py:158-166 resolves them last-write-wins, per array), some
+    ratings of exactly 0.0 (they still set the masks), and every row's list in random order (not
+    column order) -- as a fixed split (rating-level 80/10/10, TrainValidTestSplit.py:74-103)"""
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=half_stars, seed=seed)
+    g = np.random.RandomState(seed + 1)
+    d = g.choice(len(r), int(dup_frac * len(r)), replace=False)
+    r = np.concatenate([r, r[d]])
+    c = np.concatenate([c, c[d]])
+    v = np.concatenate([v, (g.randint(1, 11, len(d)) / 2.0).astype(np.float32)])
+    v[g.choice(len(v), max(1, len(v) // 500), replace=False)] = 0.0
+    p = g.permutation(len(r))
+    data = split_ratings(r[p], c[p], v[p], rows, cols, rng=np.random.RandomState(seed))
+    assert data.train.dup is not None, "the split must keep duplicate (row, col) pairs in train"
+    return data
+
+
+def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_dtype, dropout, seed, oracle_batch,
+                         eval_batches=4, envelope=False, lr=0.005):
+    """The DEFAULT training path (data_reader with rng='numpy' -> fit_generator, one hidden layer,
+    aux None = k=1 row gathers, the per-epoch row lists and scatter outputs, row-stream dW with
+    live-row skipping) on the reference's data semantics: reciprocal split with s<1, pass-through
+    on or off, duplicate (row, col) ratings, unsorted lists.  oracle_batch(bi, rows) -> (x, m_out, t)
+    is the oracle's dense batch (reference goldens or scatter_rows_numpy over the replayed draws).
+    Per step: loss and accurate_MSE (count_nonzero(T + y) denominators) vs the oracle; after the run
+    every weight, and compute_full_RMSE on the test split (train.py:243-255)."""
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    from omnidirectional_collaborative_filtering_amd.optimizers import Adagrad
+    from oracle.model_oracle import batch_metrics
+    N = rd.num_items
+    om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype=compute_dtype,
+                    seed=11, dropout_probability=dropout)
+    m = om.model
+    m.compile(Adagrad(lr=lr, epsilon=1e-8), "mean_squared_error", metrics=["accurate_MSE"])
+    w0 = m.get_weights()
+    np.random.seed(seed)
+    gen = rd.data_gen(B, sparsity, "train", True, None, aux, pass_through_input_training=pass_through)
+    assert gen.r.rng == "numpy"
+    steps = min(steps, gen.num_batches)
+    masks, gl, gm = [], [], []
+    for _ in range(steps):
+        hist = m.fit_generator(gen, 1, epochs=1, verbose=0)
+        gl.append(hist.history["loss"][0])
+        gm.append(hist.history["accurate_MSE"][0])
+        if dropout:
+            masks.append([om.engine.mask[0][:B, :H].cpu().numpy().astype(np.float64)])
+    e = om.engine
+    # the default path really ran: row gathers, the epoch's row lists + scatter outputs, live-row records
+    assert e.gt is not None and "xval" in e.gt and "flag" in e.gt, "epoch scatter outputs not used"
+    assert getattr(gen, "_rl", None) is not None and e.tb is not None and "sp_rowptr" in e.tb
+    assert e._rtag_live, "live-row records expected (Adagrad, l2 = 0)"
+    w_gpu = m.get_weights()
+    ora = OmniOracle([N, H, N], activation="sigmoid", dropout=dropout, dtype=np.float64).set_params(w0[0::2],
+                                                                                                   w0[1::2])
+    opt = AdagradOracle(lr=lr, epsilon=1e-8)
+    u = UNIT_ROUNDOFF[compute_dtype]
+    env = [np.zeros_like(p) for p in ora.params()] if envelope else None
+    rmax = [np.zeros_like(p) for p in ora.params()] if envelope else None
+    losses, mets = [], []
+    for bi in range(steps):
+        dm = masks[bi] if dropout else None
+        x, mo, t = oracle_batch(bi, gen.rows_host[bi])
+        loss, y, gW, gb = ora.loss_and_grads(x, mo, t, drop_masks=dm)
+        mets.append(batch_metrics(t, y, N, B, 1.0)["accurate_MSE"])
+        grads = [g for pair in zip(gW, gb) for g in pair]
+        if envelope:
+            GW, Gb = ora.grad_magnitudes(x, mo, t, drop_masks=dm, u=u)
+            for j, (g, G) in enumerate(zip(grads, [z for pair in zip(GW, Gb) for z in pair])):
+                rmax[j] = np.maximum(rmax[j], CHAIN_ROUNDINGS * u * G / np.maximum(np.abs(g), 1e-30))
+                env[j] += opt.lr * np.minimum(2.0, 3.0 * rmax[j])
+        losses.append(loss)
+        ora.set_flat(opt.step(ora.params(), grads))
+    # compute_full_RMSE over test batches; the oracle replays the test permutation itself
+    np.random.seed(seed + 1)
+    tgen = rd.data_gen(B, None, "test", True, None, aux, return_target_count=True)
+    nb = min(eval_batches, rd.test_set_size // B)
+    sse, cnt = m.evaluate_sse(tgen, nb)
+    np.random.seed(seed + 1)
+    order = np.random.permutation(rd.test_set_size)
+    data = rd.data
+    sse_o, cnt_o = 0.0, 0
+    for bi in range(nb):
+        rows = order[bi * B:(bi + 1) * B]
+        assert np.array_equal(rows, tgen.rows_host[bi])
+        _, _, xe, _, _ = scatter_rows_numpy(data.test_in.row_ptr, data.test_in.col, data.test_in.val, rows, N, aux=aux)
+        _, mo, _, te, _ = scatter_rows_numpy(data.test_tgt.row_ptr, data.test_tgt.col, data.test_tgt.val, rows, N,
+                                             aux=aux)
+        y, _ = ora.forward(xe, mo)
+        sse_o += float(((y - te) ** 2).sum())
+        cnt_o += int(data.test_tgt.row_lengths()[rows].sum())          # data_reader.py:268: every list entry
+    assert cnt == cnt_o, (cnt, cnt_o)
+    return Result(loss_g=float(np.mean(gl)), loss_o=float(np.mean(losses)), step_losses_g=gl, step_losses_o=losses,
+                  step_mse_g=gm, step_mse_o=mets, rmse_g=float(np.sqrt(sse / cnt)), rmse_o=float(np.sqrt(sse_o / cnt_o)),
+                  w=w_gpu, ora=ora, env=env, om=om, gen=gen, reader=rd, masks=masks)
+
+
 def _sparse_eval_sse(ora, data, rows, N):
     """compute_full_RMSE's squared error of one test batch (train.py:243-252) from the sparse
     forward: inputs from test_in, predictions only at the test_tgt entries (elsewhere y = T = 0)"""
@@ -195,6 +311,8 @@ def assert_fp32(res, loss_rel=FP32_ABS, rmse_abs=FP32_ABS, w_abs=FP32_ABS):
     """the exact-fp32 bar: per-step loss, test RMSE, and the max-abs error of every parameter"""
     for lg, lo in zip(res.step_losses_g, res.step_losses_o):
         assert abs(lg - lo) <= loss_rel * abs(lo), (lg, lo)
+    for mg, mo in zip(getattr(res, "step_mse_g", []), getattr(res, "step_mse_o", [])):
+        assert abs(mg - mo) <= loss_rel * abs(mo), ("accurate_MSE", mg, mo)
     if res.rmse_g is not None:
         assert abs(res.rmse_g - res.rmse_o) <= rmse_abs, (res.rmse_g, res.rmse_o)
     for name, err in res.max_param_err():
@@ -206,6 +324,8 @@ def assert_low_precision(res, tol):
     rounding envelope (+ FP32_ABS); returns the worst |error| / envelope ratio"""
     for lg, lo in zip(res.step_losses_g, res.step_losses_o):
         assert abs(lg - lo) <= tol * abs(lo), (lg, lo)
+    for mg, mo in zip(getattr(res, "step_mse_g", []), getattr(res, "step_mse_o", [])):
+        assert abs(mg - mo) <= tol * abs(mo), ("accurate_MSE", mg, mo)
     if res.rmse_g is not None:
         assert abs(res.rmse_g - res.rmse_o) <= tol * res.rmse_o, (res.rmse_g, res.rmse_o)
     worst = 0.0

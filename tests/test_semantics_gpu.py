@@ -1,0 +1,182 @@
+"""The default training path on the reference's OWN data semantics, against the oracle.
+
+Default path = what train.py runs (train.py:28,39,40,43,45-46): data_reader with the NumPy RNG
+(rng='numpy') -> fit_generator, one hidden layer, auxilliary_mask_type None, use_causal_info False
+(k = 1 row gathers), the per-epoch row lists and scatter outputs (ocf_epoch_row_lists +
+ocf_epoch_scatter), the row-stream weight-gradient kernel with live-row skipping, dropout 0.2
+(device Philox masks read back into the oracle).  Data semantics (data_reader.py:120-130,158-169):
+reciprocal per-rating input/target split with s < 1, pass-through on and off, duplicate (row, col)
+ratings resolved last-write-wins per array, a rating of exactly 0.0, per-row list order != column
+order.
+
+  * test_epoch_scatter_entries_vs_golden: the per-entry outputs the gather path consumes (live input
+    value xval, live-target flag) rebuild the reference's dense X / M_out / T bit for bit, for every
+    golden train batch (reference-generated, tests/golden/make_golden.py), I and U orientation;
+  * test_train_parity_golden_toy: training on the golden toy files, the oracle fed the REFERENCE's
+    own dense batches (tests/golden/batches.npz) -- the GPU draws its masks from the NumPy stream
+    exactly as data_reader.py does, so the two must see the same batches;
+  * test_train_parity_duplicates: an ML-1M-shaped (3,706 x 6,040) synthetic set with 3 % duplicate
+    pairs, 0.0 ratings and shuffled lists; the oracle replays the reference's np.random calls itself
+    (tests/parity.py replay_train_draws) and scatters with scatter_rows_numpy.
+
+Tolerances (tests/parity.py): fp32 -- per-step loss and accurate_MSE within 1e-5 relative, test
+RMSE within 1e-5, every weight within 1e-5 max-abs; f16 -- loss / accurate_MSE / RMSE within 2e-3
+relative, every weight inside its Adagrad rounding envelope."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.batch_oracle import scatter_rows_numpy
+from parity import (assert_fp32, assert_low_precision, replay_train_draws, run_semantics_parity,
+                    with_duplicates)
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _cfg():
+    with open(os.path.join(GOLD, "batches_config.json")) as f:
+        return json.load(f)
+
+
+def _toy_reader(orient):
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    cfg = _cfg()
+    if orient == "U":
+        meta = cfg["u"]["meta"]
+        rd = data_reader(meta["num_items"], meta["num_users"], os.path.join(GOLD, cfg["u"]["dir"]),
+                         nonsequentialusers=True, use_json=True, eval_mode="fixed_split", reverse_user_item_data=False)
+        gold = np.load(os.path.join(GOLD, cfg["u"]["npz"]))
+    else:
+        meta = cfg["meta"]
+        rd = data_reader(meta["num_users"], meta["num_items"], os.path.join(GOLD, "toy"), nonsequentialusers=True,
+                         use_json=True, eval_mode="fixed_split", reverse_user_item_data=True)
+        gold = np.load(os.path.join(GOLD, "batches.npz"))
+    return rd, gold
+
+
+def _gold_batch(gold, name, tag, bi, aux_type):
+    """(X, M_out, T) of a golden batch: in0 is X; M_out is in1 without aux inputs, else in2"""
+    p = "%s/%s/%d/" % (name, tag, bi)
+    return gold[p + "in0"], gold[p + ("in1" if aux_type is None else "in2")], gold[p + "targets"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("orient", ["I", "U"])
+@pytest.mark.parametrize("ci", range(5))
+def test_epoch_scatter_entries_vs_golden(gpu, ci, orient):
+    """xval / live-target flags of every entry of every train batch (the epoch build, both train
+    generators of the golden sequence) -> dense X, M_out, T == the reference's arrays, exactly; and at
+    most one live input / one live target per (batch row, column)"""
+    from omnidirectional_collaborative_filtering_amd.engine import ru
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    B = cfg["B"]
+    np.random.seed(cfg["seed_base"] + ci)
+    rd, gold = _toy_reader(orient)
+    N = rd.num_items
+    tr = rd.data.train
+    assert tr.dup is not None, "the golden toy data holds a duplicate (row, col) pair"
+    seq = [("train1", "train"), ("valid", "valid"), ("test", "test"), ("train2", "train")]
+    checked = 0
+    for tag, split in seq:
+        gen = rd.data_gen(B, sp, split, True, aux_type, auxv, pass_through_input_training=pt,
+                          return_target_count=split != "train")
+        if split != "train":
+            while next(gen) is not None:          # consume the generator like the golden sequence did
+                pass
+            continue
+        gen.prepare_row_lists(ru(N, 128))
+        rl = gen._rl
+        for bi in range(gen.num_batches):
+            s = rl["slot"][bi]
+            e0, e1 = int(rl["ebase_host"][s]), int(rl["ebase_host"][s + 1])
+            xval = rl["xval"][e0:e1].cpu().numpy()
+            tflag = rl["tflag"][e0:e1].cpu().numpy()
+            rows = gen.rows_host[bi]
+            lens = tr.row_lengths()[rows]
+            assert e1 - e0 == int(lens.sum())
+            brow = np.repeat(np.arange(B), lens)
+            idx = np.concatenate([np.arange(tr.row_ptr[r], tr.row_ptr[r + 1]) for r in rows])
+            col, val = tr.col[idx], tr.val[idx]
+            X = np.zeros((B, N), np.float32)
+            T = np.zeros((B, N), np.float32)
+            M = np.zeros((B, N), np.float32)
+            nx = np.zeros((B, N), np.int32)
+            nt = np.zeros((B, N), np.int32)
+            for e in range(len(idx)):
+                if xval[e] != 0:
+                    X[brow[e], col[e]] = xval[e]
+                    nx[brow[e], col[e]] += 1
+                if tflag[e]:
+                    T[brow[e], col[e]] = val[e]
+                    M[brow[e], col[e]] = auxv
+                    nt[brow[e], col[e]] += 1
+            assert nx.max() <= 1 and nt.max() <= 1, "duplicates must leave one live input / target"
+            gx, gm, gt = _gold_batch(gold, name, tag, bi, aux_type)
+            np.testing.assert_array_equal(X, gx.astype(np.float32), err_msg="%s %s %d X" % (name, tag, bi))
+            np.testing.assert_array_equal(M, gm.astype(np.float32), err_msg="%s %s %d M_out" % (name, tag, bi))
+            np.testing.assert_array_equal(T, gt.astype(np.float32), err_msg="%s %s %d T" % (name, tag, bi))
+            checked += 1
+    assert checked == 2 * (rd.train_set_size // B)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+@pytest.mark.parametrize("ci", range(5))
+def test_train_parity_golden_toy(gpu, ci, cd):
+    """every golden configuration's data semantics (s in [1,1], [0.3,0.7] with and without
+    pass-through, [0.5,0.5] without, [0,0.2] with; aux value -1 and +1) trained on the default path;
+    the oracle consumes the reference-generated batches"""
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    B = cfg["B"]
+    rd, gold = _toy_reader("I")
+    # the golden train1 batches were drawn right after np.random.seed(seed_base + ci)
+    res = run_semantics_parity(rd, B, 16, 99, sp, pt, float(auxv), cd, 0.2, cfg["seed_base"] + ci,
+                               lambda bi, rows: _gold_batch(gold, name, "train1", bi, aux_type),
+                               envelope=cd != "float32")
+    assert len(res.step_losses_g) == rd.train_set_size // B
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 2e-3)
+
+
+_DUP_DATA = {}
+
+
+def _dup_data():
+    if "ml1m" not in _DUP_DATA:
+        _DUP_DATA["ml1m"] = with_duplicates(3706, 6040, 1_000_209 // 4, seed=21)
+    return _DUP_DATA["ml1m"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+@pytest.mark.parametrize("sp,pt", [([0.3, 0.7], True), ([0.5, 0.5], False), ([0.0, 0.2], False), ([1.0, 1.0], True)])
+def test_train_parity_duplicates(gpu, sp, pt, cd):
+    """ML-1M I-AutoRec shape (3,706 item rows x 6,040 users, B = 256, H = 500 as train.py's model), a
+    quarter of ML-1M's ratings plus 3 % duplicate pairs, 0.0 ratings and shuffled lists"""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    data = _dup_data()
+    N = data.num_cols
+    B, seed = 256, 40
+    rd = data_reader(N, data.train.n_rows, dataset=data, eval_mode="fixed_split")
+    tr = data.train
+    np.random.seed(seed)
+    rows_o, keeps = replay_train_draws(tr.row_lengths()[np.arange(tr.n_rows)], rd.train_set_size, B, sp)
+
+    def oracle_batch(bi, rows):
+        assert np.array_equal(rows, rows_o[bi])
+        _, mo, x, t, _ = scatter_rows_numpy(tr.row_ptr, tr.col, tr.val, rows_o[bi], N, keep=keeps[bi], aux=-1.0,
+                                            pass_through=pt)
+        return x, mo, t
+
+    res = run_semantics_parity(rd, B, 500, 3, sp, pt, -1.0, cd, 0.2, seed, oracle_batch, eval_batches=2,
+                               envelope=cd != "float32")
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 2e-3)
