@@ -383,6 +383,36 @@ typedef struct OcfEpochRowListArgs {
 } OcfEpochRowListArgs;
 int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream);
 
+/* ocf_recip_keep -- the reference's reciprocal input/target split draws for a whole training epoch,
+ * bit-identical to NumPy's legacy global RandomState (MT19937): per batch bi, the B row sparsities
+ * s = np.random.uniform(s0, s1, B) (data_reader.py:120), then per row np.random.choice([0, 1], len,
+ * p=[1-s, s]) (:130), i.e. nb * B + n_entries doubles in that order; keep[e] = 1 where the choice is 1
+ * (the entry is an input).  key / pos: NumPy's state (np.random.get_state()[1], [2]) on entry, the state
+ * after the draws on return (hand it back with np.random.set_state).  The stream is generated on the
+ * device in parallel segments, each started by MT19937 jump-ahead (characteristic polynomial of the
+ * recurrence, x^J mod phi); the call synchronises `stream` to read the end state back.
+ *   boff  [nb][B + 1] (device) cumulative entry counts of each batch's rows (full rows: the draws'
+ *         lengths); ebase [nb + 1] (device) first entry of each batch (cumulative over batches);
+ *   keep  (device, nullable: only advance the state, e.g. data_sparsity [1, 1]) [n_entries] u8;
+ *   doubles (host, nullable) receives the raw uniforms (tests);
+ *   workspace: device scratch of ocf_recip_keep_workspace(nb, B, n_entries, pos) bytes. */
+typedef struct OcfRecipKeepArgs {
+  uint32_t key[624]; int32_t pos;
+  int32_t nb; int32_t B; int64_t n_entries;
+  const int64_t* boff; const int64_t* ebase;
+  double s0; double s1;
+  uint8_t* keep;
+  double* doubles;
+  void* workspace; int64_t workspace_bytes;
+} OcfRecipKeepArgs;
+int64_t ocf_recip_keep_workspace(int nb, int B, int64_t n_entries, int pos);
+int ocf_recip_keep(OcfRecipKeepArgs* args, void* stream);
+/* host twins of the same algorithm (segments, jump-ahead tree), for CPU tests: n doubles of
+ * np.random.random_sample from the state (key, pos), advancing it; and a jump by n_blocks * 624 words
+ * of a block-aligned state (pos = 624). */
+int ocf_mt_host_random_sample(uint32_t* key, int32_t* pos, int64_t n, double* out);
+int ocf_mt_host_jump(const uint32_t* key_in, int64_t n_blocks, uint32_t* key_out);
+
 /* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on
  *               [K][M] x [K][N] operands with 16-bit compute run on the persistent role-split kernel

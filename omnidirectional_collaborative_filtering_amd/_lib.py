@@ -128,6 +128,14 @@ class OcfTileBucketArgs(ctypes.Structure):
     ]
 
 
+class OcfRecipKeepArgs(ctypes.Structure):
+    _fields_ = [
+        ("key", ctypes.c_uint32 * 624), ("pos", ctypes.c_int32), ("nb", ctypes.c_int32), ("B", ctypes.c_int32),
+        ("n_entries", I64), ("boff", P), ("ebase", P), ("s0", ctypes.c_double), ("s1", ctypes.c_double),
+        ("keep", P), ("doubles", P), ("workspace", P), ("workspace_bytes", I64),
+    ]
+
+
 # every symbol include/ocf.h declares, with its ctypes signature
 SIGNATURES = {
     "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
@@ -148,6 +156,10 @@ SIGNATURES = {
     "ocf_row_lists": (I32, [ctypes.POINTER(OcfRowListArgs), P]),
     "ocf_epoch_row_lists": (I32, [ctypes.POINTER(OcfEpochRowListArgs), P]),
     "ocf_epoch_scatter": (I32, [ctypes.POINTER(OcfScatterArgs), ctypes.POINTER(OcfEpochScatterArgs), P]),
+    "ocf_recip_keep_workspace": (I64, [I32, I32, I64, I32]),
+    "ocf_recip_keep": (I32, [ctypes.POINTER(OcfRecipKeepArgs), P]),
+    "ocf_mt_host_random_sample": (I32, [P, P, I64, P]),
+    "ocf_mt_host_jump": (I32, [P, I64, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),

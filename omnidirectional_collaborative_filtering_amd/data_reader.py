@@ -8,7 +8,9 @@ deliberate:
   arrays that Keras immediately casts to float32);
 * the dataset is uploaded to HBM once as row-CSR (dataset.py); a batch never leaves the GPU;
 * the NumPy global RNG is consumed exactly as the reference consumes it (same permutation,
-  same ``uniform`` / ``choice`` draws -> bit-identical reciprocal masks).  The draws of a whole
+  same ``uniform`` / ``choice`` draws -> bit-identical reciprocal masks): the permutation by NumPy,
+  the epoch's uniform / choice draws by ocf_recip_keep on the GPU from NumPy's own MT19937 state
+  (jump-ahead segments, bit-identical; the state is handed back).  The draws of a whole
   training epoch are taken when the generator is first pulled: Keras 2.0.4's GeneratorEnqueuer
   drains the generator ahead of ``fit_generator`` (queue of 10 > the one batch train.py leaves
   unused), so every train draw precedes the validation permutation in the reference as well.
@@ -18,6 +20,7 @@ deliberate:
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -29,6 +32,17 @@ from .engine import TILE, cur_stream, ptr, ru
 
 AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
 GATHER_CHUNK = int(os.environ.get("OCF_GATHER_CHUNK", 256))   # entries per row-gather work unit (ocf_gather_*)
+
+
+_RNG_STREAMS = {}
+
+
+def _rng_stream(dev):
+    """one stream per device for ocf_recip_keep (created on first use)"""
+    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+    if key not in _RNG_STREAMS:
+        _RNG_STREAMS[key] = torch.cuda.Stream(device=key)
+    return _RNG_STREAMS[key]
 
 
 class _DeviceCSR:
@@ -143,9 +157,8 @@ class BatchGenerator(object):
 
     # ------------------------------------------------------------ epoch plan
     def plan(self, row_lengths1, row_lengths2=None):
-        """Host half of the epoch plan (no GPU): permutation, batch rows, batch-local entry offsets
-        and -- for train batches with rng='numpy' -- the reciprocal keep flags, drawing from the
-        NumPy global RNG exactly as data_reader.py:120,130,326-327 do."""
+        """Host half of the epoch plan (no GPU): the NumPy permutation of the row set
+        (data_reader.py:326-327), batch rows, batch-local entry offsets, target counts."""
         order = np.random.permutation(self.n) if self.shuffle else np.arange(self.n)   # :326-327
         nb, B = self.num_batches, self.B
         rows = order[: nb * B].reshape(nb, B).astype(np.int64)
@@ -153,18 +166,42 @@ class BatchGenerator(object):
         boff = np.zeros((nb, B + 1), dtype=np.int64)
         np.cumsum(lens1, axis=1, out=boff[:, 1:])
         tcount = row_lengths2[rows].sum(axis=1) if row_lengths2 is not None else None
+        return rows, boff, tcount
+
+    def _draw_keep(self, boff):
+        """The epoch's reciprocal-split draws (data_reader.py:120 uniform per batch, :130 choice per row)
+        on the device from NumPy's own global MT19937 state, bit-identical, the state handed back to
+        NumPy afterwards (ocf_recip_keep).  Returns the keep flags (None when data_sparsity is [1, 1]: every
+        rating is an input, but the stream still advances exactly as the reference's draws advance it)."""
+        nb, B = self.num_batches, self.B
+        E = int(boff[:, -1].sum()) if nb else 0
+        s0, s1 = float(self.sparsity[0]), float(self.sparsity[1])
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise ValueError("the reference's draws need NumPy's legacy MT19937 global state")
+        dev = self.r.device
+        a = _lib.OcfRecipKeepArgs()
+        key = np.ascontiguousarray(st[1], dtype=np.uint32)
+        ctypes.memmove(a.key, key.ctypes.data, 624 * 4)
+        a.pos, a.nb, a.B, a.n_entries = int(st[2]), nb, B, E
+        a.s0, a.s1 = s0, s1
         keep = None
-        if self.split == "train" and self.r.rng == "numpy":
-            s0, s1 = float(self.sparsity[0]), float(self.sparsity[1])
-            keeps = []
-            for bi in range(nb):
-                s_rows = np.random.uniform(low=s0, high=s1, size=B)                    # :120
-                u = np.random.random_sample(int(boff[bi, -1]))                          # :130, one call/batch
-                cut = (1.0 - s_rows) / ((1.0 - s_rows) + s_rows)
-                keeps.append(u >= np.repeat(cut, lens1[bi]))
-            if not (s0 >= 1.0 and s1 >= 1.0):
-                keep = np.concatenate(keeps) if keeps else np.zeros(0, bool)
-        return rows, boff, tcount, keep
+        ebase = None
+        if not (s0 >= 1.0 and s1 >= 1.0) and E:
+            keep = torch.empty(E, dtype=torch.uint8, device=dev)
+            ebase = torch.as_tensor(np.concatenate([[0], np.cumsum(boff[:, -1])]).astype(np.int64), device=dev)
+            a.keep, a.boff, a.ebase = ptr(keep), ptr(self.boff_dev), ptr(ebase)
+        nbytes = _lib.load().ocf_recip_keep_workspace(nb, B, E, a.pos)
+        if nbytes < 0:
+            raise _lib.OcfError("ocf_recip_keep_workspace: " + _lib.load().ocf_last_error().decode())
+        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        a.workspace, a.workspace_bytes = ptr(ws), int(nbytes)
+        # its own stream (the call synchronises it to hand the state back): the main stream's queued steps
+        # are not waited for
+        with torch.cuda.stream(_rng_stream(dev)):
+            _lib.call("ocf_recip_keep", a, cur_stream())
+        np.random.set_state((st[0], np.frombuffer(a.key, dtype=np.uint32).copy(), int(a.pos), st[3], st[4]))
+        return keep
 
     def _start(self):
         self.started = True
@@ -176,14 +213,14 @@ class BatchGenerator(object):
             self.src1, self.src2 = dev["valid_in"], dev["valid_tgt"]
         else:
             self.src1, self.src2 = dev["test_in"], dev["test_tgt"]
-        rows, boff, self.tcount, keep = self.plan(self.src1.rng_lens,
-                                                  None if self.src2 is None else self.src2.rng_lens)
+        rows, boff, self.tcount = self.plan(self.src1.rng_lens, None if self.src2 is None else self.src2.rng_lens)
         nb = self.num_batches
         self.rows_host = rows
         self.nnz_full = boff[:, -1].copy()
         self.nnz1 = self.src1.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)   # entries held here
         self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
         self.boff_dev = torch.as_tensor(boff, device=r.device)
+        keep = self._draw_keep(boff) if (self.split == "train" and r.rng == "numpy") else None
         # batch-local offsets of the entries held by this CSR (one scatter thread per entry)
         self.lboff1_dev = torch.as_tensor(self._local_offsets(self.src1.lens, rows), device=r.device)
         if self.src2 is not None:
@@ -195,7 +232,7 @@ class BatchGenerator(object):
         self.keep_dev = None
         self.keep_off = None
         if keep is not None:
-            self.keep_dev = torch.as_tensor(keep.astype(np.uint8), device=r.device)
+            self.keep_dev = keep
             self.keep_off = np.concatenate([[0], np.cumsum(self.nnz_full)])
         self.max_targets = int(max(self.nnz1.max() if nb else 0,
                                    self.tlocal.max() if (self.src2 is not None and nb) else 0))

@@ -18,7 +18,7 @@ HDR = os.path.join(ROOT, "include", "ocf.h")
 def declared_functions():
     src = open(HDR).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ocf_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(ocf_\w+)\s*\(", src, flags=re.M)))
 
 
 def test_header_declares_expected_entry_points():
@@ -64,6 +64,8 @@ STRUCTS = {
                                                        "ebase", "cnt", "row_ptr", "row_ent", "live"]),
     "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
                                                        "xval", "tflag"]),
+    "OcfRecipKeepArgs": (_lib.OcfRecipKeepArgs, ["key", "pos", "nb", "B", "n_entries", "boff", "ebase", "s0", "s1",
+                                                 "keep", "doubles", "workspace", "workspace_bytes"]),
 }
 
 

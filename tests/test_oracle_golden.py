@@ -82,7 +82,12 @@ def test_uniform_and_stream_concatenation():
 @pytest.mark.parametrize("orient", ["I", "U"])
 @pytest.mark.parametrize("ci", range(5))
 def test_product_epoch_plan_matches_reference(gold, gold_u, ci, orient):
-    """BatchGenerator.plan (host) + the vectorised scatter reproduce the reference train batches."""
+    """BatchGenerator.plan (host permutation) + the reciprocal draws of ocf_recip_keep's algorithm (its host
+    twin ocf_mt_host_random_sample: the same MT19937 jump-ahead segments, from NumPy's state) + the
+    vectorised scatter reproduce the reference train batches."""
+    import ctypes
+
+    from omnidirectional_collaborative_filtering_amd import _lib
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     cfg = _cfg()
     name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
@@ -98,12 +103,19 @@ def test_product_epoch_plan_matches_reference(gold, gold_u, ci, orient):
                          reverse_user_item_data=True)
     gen = rd.data_gen(B, sp, "train", True, aux_type, auxv, pass_through_input_training=pt)
     tr = rd.data.train
-    rows, boff, _, keep = gen.plan(tr.row_lengths())
+    rows, boff, _ = gen.plan(tr.row_lengths())
+    st = np.random.get_state()
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = ctypes.c_int32(int(st[2]))
+    n = len(rows) * B + int(boff[:, -1].sum())
+    u = np.empty(n, np.float64)
+    _lib.call("ocf_mt_host_random_sample", key.ctypes.data, ctypes.addressof(pos), n, u.ctypes.data)
+    d = 0
     for bi in range(len(rows)):
-        kb = None
-        if keep is not None:
-            start = int(sum(boff[j, -1] for j in range(bi)))
-            kb = keep[start: start + int(boff[bi, -1])]
+        s = sp[0] + (sp[1] - sp[0]) * u[d:d + B]                             # data_reader.py:120
+        ue = u[d + B: d + B + int(boff[bi, -1])]                              # :130, row after row
+        d += B + int(boff[bi, -1])
+        kb = ue >= np.repeat((1.0 - s) / ((1.0 - s) + s), np.diff(boff[bi]))
         m_in, m_out, x, t, m_miss = scatter_rows_numpy(tr.row_ptr, tr.col, tr.val, rows[bi], rd.num_items, keep=kb,
                                                        aux=auxv, pass_through=pt)
         np.testing.assert_array_equal(x, gold["%s/train1/%d/in0" % (name, bi)])
