@@ -56,6 +56,9 @@ def parse():
                     help="N=1, 16-bit runs: also time this many steps of the exact-fp32 parity mode "
                          "(compute_dtype float32; reported as fp32_parity_mode, not the headline)")
     ap.add_argument("--phase-timers", type=int, default=1)
+    ap.add_argument("--epoch", type=int, default=1,
+                    help="N=1: also time one whole training epoch through fit_generator (train.py:157: floor(n/B)-1 "
+                         "steps, the epoch plan and the reference RNG's draws included; reported as full_epoch)")
     ap.add_argument("--rmse", type=int, default=1)
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="diagnostic: run rank 0 of a G-way feature-parallel job alone (collectives skipped, "
@@ -69,6 +72,9 @@ def parse():
                     help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
     ap.add_argument("--ws-max-k", type=int, default=0,
                     help="largest batch K routed to the role-split dW kernel (0: library default)")
+    ap.add_argument("--rows-long", type=int, default=-1,
+                    help="row-stream dW kernel's LONG variant (entries as vectors): -1 library's choice (>= 4 "
+                         "entries per weight row), 0 never, 1 always")
     ap.add_argument("--fold-jobs", type=int, default=1,
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
@@ -192,6 +198,38 @@ def fp32_mode(args, data, rd, n_rows, dev, steps):
     return {"ms_per_step": round(ms, 4), "steps": steps, "compute": "float32 throughout (fp32 weight rows in the gathers, fp32 row-stream dW)"}
 
 
+def full_epoch(args, m, rd, B):
+    """one train.py epoch, wall clock: fresh generator (permutation, batch tables, the NumPy-stream draws
+    of data_reader.py:120,130 on the device, row lists, scatter outputs) + fit_generator over
+    floor(n/B) - 1 steps (train.py:157) + the epoch-end stats read-back.  Also the epoch plan alone with
+    a reciprocal split (data_sparsity [0.3, 0.7]: the keep flags of every rating drawn)."""
+    out = {}
+    for name, sp in (("train_py", [1.0, 1.0]), ("recip_0.3_0.7", [0.3, 0.7])):
+        np.random.seed(4321)
+        gen = rd.data_gen(B, sp, "train", True, None, -1, pass_through_input_training=sp[0] >= 1.0)
+        steps = gen.num_batches - 1
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if name == "train_py":
+            m.fit_generator(gen, steps, epochs=1, verbose=0)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            nnz = int(gen.nnz1[:steps].sum())
+            out[name] = {"batches": steps, "ms_per_batch": round(dt / steps * 1e3, 4),
+                         "ratings_per_s": round(nnz / dt, 1), "wall_s": round(dt, 4)}
+        else:
+            gen._start()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            gen.prepare_row_lists(m.engine.Np)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            out[name] = {"plan_ms": round((t1 - t0) * 1e3, 3), "row_lists_and_scatter_ms": round((t2 - t1) * 1e3, 3),
+                         "batches": gen.num_batches, "entries": int(gen.nnz_full.sum())}
+    out["rng"] = "numpy (NumPy's global MT19937 stream; the epoch's draws by ocf_recip_keep on the device)"
+    return out
+
+
 def main():
     args = parse()
     from omnidirectional_collaborative_filtering_amd.parallel import (DataParallel, feature_shard_range,
@@ -225,7 +263,8 @@ def main():
     else:
         data, Bg, shard, comm = data_full, B, None, None
     np.random.seed(1234)
-    rd = data_reader(data.num_cols, n_rows, dataset=data, eval_mode="fixed_split", rng="device", device=dev)
+    # rng="numpy": the reference's own RNG stream (NumPy's MT19937 state, epoch draws on the device)
+    rd = data_reader(data.num_cols, n_rows, dataset=data, eval_mode="fixed_split", rng="numpy", device=dev)
     om = omni_model(1, H, data.num_cols, Bg, dense_activation="sigmoid", use_causal_info=False,
                     dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev,
                     shard=shard, comm=comm)
@@ -247,9 +286,11 @@ def main():
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
         eng.shadow_blocked = bool(args.shadow_blocked)
         eng._refresh_shadows()
+    from omnidirectional_collaborative_filtering_amd import _lib
     if args.ws_max_k:
-        from omnidirectional_collaborative_filtering_amd import _lib
         _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)
+    if args.rows_long >= 0:
+        _lib.call("ocf_set_tuning", b"rows_long", int(args.rows_long), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)
@@ -371,7 +412,9 @@ def main():
                 "alg_bytes_per_launch": int(alg[dom]), "live_row_frac": round(live, 4)}
         # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
         pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
-        if pmcs and world == 1:
+        # (measured on the default headline workload only: ML-20M, B = 256, f16, one GPU)
+        if pmcs and world == 1 and args.config == "ml20m" and args.batch == 256 and args.dtype == "float16" \
+                and not args.emulate_shards:
             with open(pmcs[-1]) as f:
                 tr = json.load(f).get(dom)
             if tr:
@@ -416,6 +459,8 @@ def main():
     }
     if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
         line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)
+    if world == 1 and args.epoch and not args.emulate_shards:
+        line["full_epoch"] = full_epoch(args, m, rd, Bg)
     if world == 1 and args.cpu_baseline:
         rows_b = [gen.rows_host[bi] for bi in batches[: args.cpu_steps]]
         try:

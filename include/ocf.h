@@ -276,6 +276,10 @@ typedef struct OcfGemmArgs {
    * decoder's delta reduction rides in a weight-gradient launch that does not read its outputs (dW_out)
    * and the launches that do (dW_in, its bias / stats jobs) follow.  The struct is copied at the call. */
   const OcfRowsReduceArgs* jr;
+  /* row lists: the number of entries (0 = unknown).  With many entries per weight row (>= 4 per row on
+   * average: feature-parallel global batches, dense datasets like ML-1M) the row-stream kernel loads each
+   * row's entries as one vector (a lane per entry) and the B rows of a group of entries in one go. */
+  int64_t sp_nent;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

@@ -114,7 +114,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("jb_part", P), ("jb_parts", I32), ("jb_n", I32), ("jb_ld", I64), ("jb_p", P), ("jb_s1", P), ("jb_s2", P),
         ("jb_op", OcfOptParams),
         ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
-        ("row_live", P), ("sp_rowptr", P), ("sp_rowent", P), ("jr", P),
+        ("row_live", P), ("sp_rowptr", P), ("sp_rowent", P), ("jr", P), ("sp_nent", I64),
     ]
 
 

@@ -52,6 +52,7 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
 // (dW 132 / 111 us vs 175 / 137 us).
 int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (ocf_set_tuning "optim_rows")
 int g_optim_ws = -1;
+int g_rows_long = -1;   // row-stream LONG variant: -1 by entries per row, 0 never, 1 always ("rows_long")
 int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
 bool optim_ws_on() {
   if (g_optim_ws < 0) {
@@ -128,10 +129,18 @@ bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s
     constexpr int PARTS = 12;
     const int grid = std::max(g.M / 128 * PARTS, (jb.count() + 3) / 4);
     // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
+    // many entries per weight row (>= 4 on average): the LONG variant (entries as a vector, B rows of a
+    // group of entries in flight together)
+    const bool lng = g_rows_long < 0 ? g.sp_nent >= 4LL * g.M : g_rows_long != 0;
     auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
       constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
       constexpr int NCH = decltype(nch_tag)::value;
-      hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
+      if (lng)
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, true>), dim3(grid), dim3(RS_THREADS), 0, s,
+                           ra, jb);
+      else
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, false>), dim3(grid), dim3(RS_THREADS), 0, s,
+                           ra, jb);
     };
     using std::integral_constant;
     auto by_n = [&](auto k) {
@@ -335,6 +344,9 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   if (k == "optim_rows") {
     if (previous) *previous = g_optim_rows;
     g_optim_rows = value ? 1 : 0;
+  } else if (k == "rows_long") {
+    if (previous) *previous = g_rows_long;
+    g_rows_long = value < 0 ? -1 : (value ? 1 : 0);
   } else if (k == "optim_ws") {
     if (previous) *previous = optim_ws_on() ? 1 : 0;
     g_optim_ws = value ? 1 : 0;

@@ -29,6 +29,7 @@ namespace ocf {
 constexpr int RS_THREADS = 256;
 constexpr int RS_E0 = 2;   // entries per row loaded with the row's first loads (E0 = 1 / 3: equal / 3 % slower)
 constexpr int RS_ET = 4;   // entries loaded together beyond those (rows of long batches)
+constexpr int RS_ETL = 8;  // LONG variant: B rows of this many entries in flight per group
 
 struct RowsDwArgs {
   float* p; float* s1; float* s2;
@@ -90,26 +91,32 @@ template <> struct RsVec<2> {
 // iteration covers loads a whole iteration old.  Against the p / slot loads one stage earlier (B):
 // 75 vs 113 VGPRs (6 vs 4 waves per SIMD), dW_in 144.5 vs 157.5 us.
 // PARTS = 12 (about 7 rows per wave at ML-20M; ocf_gemm.hip launch_rows has the sweep).
-template <typename CT, int CW, int NCH, int E0, bool ADAM> struct RpRow {
+template <typename CT, int CW, int NCH, int E0, bool ADAM, bool LONG> struct RpRow {
   using F = typename RsVec<CW>::F;
   using H = RsH<CT, CW>;
   int m, lo, n;
   bool lv;
-  int2 e[E0];
-  float v[E0];
+  int2 e[LONG ? 1 : E0];
+  float v[LONG ? 1 : E0];
+  int2 ev;                // LONG: the row's first 64 entries, lane i = entry i
+  float vv;               // LONG: their values
   H h[E0][NCH];
   F p[NCH], a[NCH], b[ADAM ? NCH : 1];
   WsJobs::BiasPre bias;   // output-layer bias and its slots (colsum rows with a folded bias update)
 };
 
-template <typename CT, int KIND, int CW, int NCH, int PARTS>
+// LONG (rows with many entries: feature-parallel global batches, dense datasets): stage C loads the row's
+// entries as one vector (lane i = entry i, up to 64 at a time), stage D their values as one gather, and
+// stage E walks them in groups of RS_ETL whose B rows are all in flight at once -- the entry indices come
+// from the vector by readlane, so a group waits for its B rows only, not for an entry -> value -> B chain.
+template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
   using V = RsVec<CW>;
   using F = typename V::F;
   using H = RsH<CT, CW>;
   constexpr bool ADAM = KIND == OCF_OPT_ADAM;
   constexpr int E0 = RS_E0;
-  using Row = RpRow<CT, CW, NCH, E0, ADAM>;
+  using Row = RpRow<CT, CW, NCH, E0, ADAM, LONG>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   {  // folded small jobs (hidden-bias update from the decoder's partials, the step's stats): one per wave
     const int nj = jobs.count();
@@ -159,22 +166,38 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
     r.lo = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m]);
     r.n = __builtin_amdgcn_readfirstlane(ra.rowptr[r.m + 1]) - r.lo;
   };
+  auto rdl = [&](int x, int i) { return __builtin_amdgcn_readlane(x, i); };
   auto stC = [&](Row& r) {
     if (!r.lv) return;
+    if constexpr (LONG) {
+      r.ev = lane < r.n ? ra.rowent[r.lo + lane] : make_int2(0, 0);
+    } else {
 #pragma unroll
-    for (int e = 0; e < E0; ++e) r.e[e] = e < r.n ? ra.rowent[r.lo + e] : make_int2(0, 0);
+      for (int e = 0; e < E0; ++e) r.e[e] = e < r.n ? ra.rowent[r.lo + e] : make_int2(0, 0);
+    }
     if (ra.colsum && jobs.cb_p) r.bias = jobs.colsum_pre(r.m);
   };
   auto stD = [&](Row& r) {
     if (!r.lv) return;
     ld_pa(r);
+    if constexpr (LONG) {
+      r.vv = lane < r.n ? ra.vals[r.ev.x] : 0.f;
 #pragma unroll
-    for (int e = 0; e < E0; ++e) {
-      r.v[e] = 0.f;
-      if (e < r.n) {
-        r.v[e] = ra.vals[r.e[e].x];
+      for (int e = 0; e < E0; ++e)
+        if (e < r.n) {
+          const int k = rdl(r.ev.y, e);
 #pragma unroll
-        for (int j = 0; j < NCH; ++j) r.h[e][j] = bpiece(r.e[e].y, j);
+          for (int j = 0; j < NCH; ++j) r.h[e][j] = bpiece(k, j);
+        }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E0; ++e) {
+        r.v[e] = 0.f;
+        if (e < r.n) {
+          r.v[e] = ra.vals[r.e[e].x];
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) r.h[e][j] = bpiece(r.e[e].y, j);
+        }
       }
     }
   };
@@ -192,6 +215,48 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
 #pragma unroll
     for (int j = 0; j < NCH; ++j) g[j] = V::zero();
     float cs = 0.f;
+    if constexpr (LONG) {
+#pragma unroll
+      for (int e = 0; e < E0; ++e)
+        if (e < r.n) {
+          const float v = __int_as_float(rdl(__float_as_int(r.vv), e));
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) acc(g[j], v, r.h[e][j]);
+          cs += v;
+        }
+      // the rest in groups of RS_ETL, 64 entries per vector (the first 64 from stage C / D)
+      int2 ev = r.ev;
+      float vv = r.vv;
+      for (int e0 = E0; e0 < r.n; e0 += RS_ETL) {
+        if ((e0 & 63) < RS_ETL && e0 >= 64) {     // crossed into the next 64: reload (rows over 64 entries)
+          const int c0 = e0 & ~63;
+          ev = c0 + lane < r.n ? ra.rowent[r.lo + c0 + lane] : make_int2(0, 0);
+          vv = c0 + lane < r.n ? ra.vals[ev.x] : 0.f;
+        }
+        H hx[RS_ETL][NCH];
+#pragma unroll
+        for (int e = 0; e < RS_ETL; ++e) {
+          const int i = e0 + e;
+          if (i < r.n && (i & ~63) == (e0 & ~63)) {
+            const int k = rdl(ev.y, i & 63);
+#pragma unroll
+            for (int j = 0; j < NCH; ++j) hx[e][j] = bpiece(k, j);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < RS_ETL; ++e) {
+          const int i = e0 + e;
+          if (i < r.n && (i & ~63) == (e0 & ~63)) {
+            const float v = __int_as_float(rdl(__float_as_int(vv), i & 63));
+#pragma unroll
+            for (int j = 0; j < NCH; ++j) acc(g[j], v, hx[e][j]);
+            cs += v;
+          }
+        }
+        // a group straddling a 64-entry boundary: continue from the boundary
+        if (((e0 + RS_ETL) & ~63) != (e0 & ~63) && ((e0 + RS_ETL) & 63) != 0) e0 = ((e0 + RS_ETL) & ~63) - RS_ETL;
+      }
+    } else {
 #pragma unroll
     for (int e = 0; e < E0; ++e)
       if (e < r.n) {
@@ -221,6 +286,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
           for (int j = 0; j < NCH; ++j) acc(g[j], v[e], hx[e][j]);
           cs += v[e];
         }
+    }
     }
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {

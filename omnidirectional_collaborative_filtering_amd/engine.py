@@ -476,7 +476,7 @@ class Engine:
                     # the epoch's row lists and live records, built once per epoch by the generator
                     # (ocf_epoch_row_lists): no per-step counting, keys or tags
                     t = rl(self.Np)
-                    epoch_lists = dict(sp_rowptr=t["row_ptr"], sp_rowent=t["row_ent"])
+                    epoch_lists = dict(sp_rowptr=t["row_ptr"], sp_rowent=t["row_ent"], sp_nent=int(a.E1))
                     self._live_ptrs = (t["live"], t["live"]) if self.row_skip else None
                     # ... and the batch's scatter outputs (ocf_epoch_scatter): no per-step scatter
                     if self.epoch_scatter:
@@ -528,7 +528,7 @@ class Engine:
             a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
             a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
         call("ocf_row_lists", a, cur_stream())
-        return dict(sp_rowptr=rptr, sp_rowent=rent)
+        return dict(sp_rowptr=rptr, sp_rowent=rent, sp_nent=E)
 
     def _tile_buckets(self):
         """the batch's entries bucketed by (user tile, K-step) for the persistent weight-gradient

@@ -2,6 +2,8 @@
 built by ocf_sparse_tiles against a NumPy restatement, the fused update against a plain PyTorch fp32
 reference (g = A^T B from the same entries, Keras' optimizer formulas), rows without entries skipped
 only where that is the identity (Adagrad, l2 = 0), the output-bias column sums and their update."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -420,3 +422,46 @@ def test_epoch_scatter_matches_per_batch(gpu, rng, sparsity, pt):
         assert torch.equal(rl["tflag"][e0:e0 + E], tf)
         if sparsity[0] < 1:
             assert 0 < int((xv == 0).sum()) < E            # the split dropped some inputs and kept others
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["adagrad", "rmsprop", "adam"])
+@pytest.mark.parametrize("cd,shape", [
+    ("float16", (900, 4000, 40000, 128, 0.5)),        # ~1.4 entries per weight row
+    ("bfloat16", (3706, 6040, 1000209, 256, 0.0)),    # ML-1M I-AutoRec: ~11 per row
+    ("float32", (3706, 6040, 1000209, 256, 0.0)),
+    ("float16", (5000, 1024, 1500000, 2048, 1.0)),    # rows over 64 and over 1,024 entries
+])
+def test_rows_long_variant_bit_identical(gpu, cd, shape, opt):
+    """The row-stream kernel's LONG variant (a row's entries loaded as one vector, the B rows of 8 entries in
+    flight together; chosen by the library at >= 4 entries per weight row, ocf_set_tuning "rows_long")
+    against the scalar-chain variant: identical losses, weights, slots and shadows (same per-element
+    summation order), for every optimizer and compute dtype, short and long lists"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B, skew = shape
+    mk = {"adagrad": lambda: O.Adagrad(lr=0.01, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=0.001),
+          "adam": lambda: O.Adam(lr=0.001)}[opt]
+    out = []
+    prev = ctypes.c_int(0)
+    try:
+        for long_on in (0, 1):
+            _lib.call("ocf_set_tuning", b"rows_long", long_on, ctypes.byref(prev))
+            rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=13)
+            om = om_ = omni_model(1, 500 if cd != "float32" else 200, cols, B, dense_activation="sigmoid",
+                                  use_causal_info=False, dropout_probability=0.2, compute_dtype=cd, seed=4)
+            eng = om.engine
+            m = om.model
+            m.compile(mk(), "mean_squared_error", metrics=["mae"])
+            h = m.fit_generator(gen, min(4, gen.num_batches), epochs=1, verbose=0).history
+            assert eng.tb is not None and "sp_rowptr" in eng.tb
+            torch.cuda.synchronize()
+            out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                        [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                        [t.clone() for t in eng.Wsh if t is not None]))
+            del om_
+    finally:
+        _lib.call("ocf_set_tuning", b"rows_long", -1, None)
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)

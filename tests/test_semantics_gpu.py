@@ -147,20 +147,22 @@ def test_train_parity_golden_toy(gpu, ci, cd):
 _DUP_DATA = {}
 
 
-def _dup_data():
-    if "ml1m" not in _DUP_DATA:
-        _DUP_DATA["ml1m"] = with_duplicates(3706, 6040, 1_000_209 // 4, seed=21)
-    return _DUP_DATA["ml1m"]
+def _dup_data(frac):
+    if frac not in _DUP_DATA:
+        _DUP_DATA[frac] = with_duplicates(3706, 6040, int(1_000_209 * frac), seed=21)
+    return _DUP_DATA[frac]
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cd", ["float32", "float16"])
-@pytest.mark.parametrize("sp,pt", [([0.3, 0.7], True), ([0.5, 0.5], False), ([0.0, 0.2], False), ([1.0, 1.0], True)])
-def test_train_parity_duplicates(gpu, sp, pt, cd):
+@pytest.mark.parametrize("sp,pt,frac", [([0.3, 0.7], True, 0.25), ([0.5, 0.5], False, 0.25), ([0.0, 0.2], False, 0.25),
+                                        ([1.0, 1.0], True, 0.25), ([1.0, 1.0], True, 1.0), ([0.5, 0.5], False, 1.0)])
+def test_train_parity_duplicates(gpu, sp, pt, frac, cd):
     """ML-1M I-AutoRec shape (3,706 item rows x 6,040 users, B = 256, H = 500 as train.py's model), a
-    quarter of ML-1M's ratings plus 3 % duplicate pairs, 0.0 ratings and shuffled lists"""
+    quarter of ML-1M's ratings (~3 entries per weight row) or all of them (~11 per row: the row-stream
+    kernel's LONG variant) plus 3 % duplicate pairs, 0.0 ratings and shuffled lists"""
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
-    data = _dup_data()
+    data = _dup_data(frac)
     N = data.num_cols
     B, seed = 256, 40
     rd = data_reader(N, data.train.n_rows, dataset=data, eval_mode="fixed_split")
