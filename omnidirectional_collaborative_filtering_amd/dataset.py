@@ -201,7 +201,7 @@ class FixedSplit:
                           col_ids=list(self.col_ids[c0:c1]))
 
     def save(self, path):
-        arrs = {"num_cols": np.array(self.num_cols)}
+        arrs = {"num_cols": np.array(self.num_cols), "col_ids": np.asarray([str(c) for c in self.col_ids])}
         for name in ("train", "valid_in", "valid_tgt", "test_in", "test_tgt"):
             c = getattr(self, name)
             arrs[name + "/row_ptr"] = c.row_ptr
@@ -218,7 +218,8 @@ class FixedSplit:
             c = RatingsCSR(z[name + "/row_ptr"], z[name + "/col"], z[name + "/val"], list(z[name + "/keys"]))
             c.dup = dup_chain(c.row_ptr, c.col)
             parts[name] = c
-        return cls(int(z["num_cols"]), **parts)
+        col_ids = list(z["col_ids"]) if "col_ids" in z.files else list(range(int(z["num_cols"])))
+        return cls(int(z["num_cols"]), col_ids=col_ids, **parts)
 
 
 def load_reference_json(filepath, reverse_user_item_data=True, use_json=True):
@@ -250,11 +251,17 @@ def load_reference_json(filepath, reverse_user_item_data=True, use_json=True):
     )
 
 
-def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=None, dup_free=False):
-    """Rating-level permutation split of TrainValidTestSplit.py:74-103.
+def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=None, dup_free=False, row_keys=None,
+                  col_ids=None):
+    """Rating-level permutation split of TrainValidTestSplit.py:74-103, with the reference's orders.
 
-    valid inputs = the row's train ratings (:101, map_inputs_to_targets :183-195),
-    test inputs = the row's train+valid ratings (:83, :103); rows keyed by their index.
+    perm = rng.permutation(n_ratings) (:74; rng = NumPy's global RNG by default, as the reference);
+    train / valid / test = perm[:80 %], the next 10 %, the rest (:76-82); test inputs = train + valid
+    ratings = perm[:90 %] (:83).  Each split's rows are keyed in the order the reference's
+    build_user_item_dict inserts them into its dict -- order of first appearance in that split's
+    ratings (:121-149) -- and each row's list keeps the split's rating order; valid / test inputs are
+    the target rows' input lists or empty (map_inputs_to_targets, :183-195).  row_keys[r] labels row
+    id r (default: the integer itself); col_ids labels the columns (default 0 .. n_cols-1).
     dup_free: the (row, col) pairs are unique (synthetic_ratings), so no split has duplicates.
     """
     rng = np.random if rng is None else rng
@@ -265,32 +272,29 @@ def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=N
     rows = np.asarray(rows, np.int64)
     cols = np.asarray(cols, np.int32)
     vals = np.asarray(vals, np.float32)
+    label = (lambda r: int(r)) if row_keys is None else (lambda r: row_keys[r])
 
-    def csr_of(idx):
-        return RatingsCSR.from_coo(rows[idx], cols[idx], vals[idx], n_rows, dup_free=dup_free)
+    def by_first_appearance(idx):
+        """(CSR of ratings idx keyed by first appearance, row ids in key order, row id -> position or -1)"""
+        r = rows[idx]
+        uniq, first = np.unique(r, return_index=True)
+        order = uniq[np.argsort(first, kind="stable")]
+        pos = np.full(n_rows, -1, np.int64)
+        pos[order] = np.arange(len(order))
+        csr = RatingsCSR.from_coo(pos[r], cols[idx], vals[idx], len(order), keys=[label(x) for x in order],
+                                  dup_free=dup_free)
+        return csr, order, pos
 
-    full_tr = csr_of(tr)
-    full_va = csr_of(va)
-    full_te = csr_of(te)
-    full_te_in = csr_of(np.concatenate([tr, va]))
-    tr_rows = np.nonzero(full_tr.row_lengths())[0]
-    va_rows = np.nonzero(full_va.row_lengths())[0]
-    te_rows = np.nonzero(full_te.row_lengths())[0]
-    train = full_tr.subset_rows(tr_rows)
-    train.keys = [int(r) for r in tr_rows]
-    has_tr = full_tr.row_lengths() > 0
-    has_te_in = full_te_in.row_lengths() > 0
-
-    def pair(target_full, rows_sel, input_full, has_input):
-        tgt = target_full.subset_rows(rows_sel)
-        tgt.keys = [int(r) for r in rows_sel]
-        inp = input_full.subset_rows(np.where(has_input[rows_sel], rows_sel, -1))
-        inp.keys = list(tgt.keys)
-        return inp, tgt
-
-    va_in, va_t = pair(full_va, va_rows, full_tr, has_tr)
-    te_in, te_t = pair(full_te, te_rows, full_te_in, has_te_in)
-    return FixedSplit(n_cols, train, va_in, va_t, te_in, te_t, list(range(n_cols)))
+    train, _, pos_tr = by_first_appearance(tr)
+    va_t, order_va, _ = by_first_appearance(va)
+    te_t, order_te, _ = by_first_appearance(te)
+    te_full, _, pos_te_in = by_first_appearance(perm[:ntr + nva])
+    va_in = train.subset_rows(pos_tr[order_va])
+    va_in.keys = list(va_t.keys)
+    te_in = te_full.subset_rows(pos_te_in[order_te])
+    te_in.keys = list(te_t.keys)
+    return FixedSplit(n_cols, train, va_in, va_t, te_in, te_t,
+                      list(range(n_cols)) if col_ids is None else list(col_ids))
 
 
 # density / shape table for synthetic inputs (SURVEY.md 8(d); rows x N in I-AutoRec orientation)
