@@ -247,7 +247,7 @@ static void jump_host(const uint32_t* in, const Poly& p, uint32_t* out) {
 }
 
 // ---------------------------------------------------------------- device kernels
-constexpr int JUMP_THREADS = 640;
+constexpr int JUMP_THREADS = 640;   // mt_init_kernel
 constexpr int GEN_THREADS = 256;
 
 // buf[624 .. 1248) = the block after the window buf[0 .. 624) (three dependency phases)
@@ -269,40 +269,53 @@ __global__ void __launch_bounds__(JUMP_THREADS) mt_init_kernel(KeyArg key, uint3
   for (int i = threadIdx.x; i < NW; i += JUMP_THREADS) win[i] = key.w[i];
 }
 
-// dst[i] = Q (src[i]) for the n windows of 624 words (job i = workgroup i)
-__global__ void __launch_bounds__(JUMP_THREADS) mt_jump_kernel(const uint32_t* srcs, uint32_t* dsts, const uint64_t* poly) {
-  __shared__ uint32_t buf[2 * NW];
-  __shared__ uint64_t pc[PW];
-  const int t = threadIdx.x;
+// dst[i] = Q (src[i]) for the n windows of 624 words: workgroup (i, g) regenerates the window sequence of
+// job i and accumulates its share [JP_W g, JP_W (g + 1)) of the 624 words.  Q comes as the positions of
+// its set coefficients, per block of 624 steps, each block's list padded to a multiple of 8 with a sentinel
+// (JP_ZERO: it reads a zero region).  Lane l of the share XORs window word buf[k + w0 + l] of every listed
+// k: eight positions per two broadcast LDS reads, their reads in flight together, consecutive lanes on
+// consecutive banks.  (Measured per jump: a scalar walk of the coefficient bits by every wave 536 us; one
+// workgroup per jump, two words per lane 255 us -- LDS-bandwidth bound, 780 KB of window reads per block.)
+constexpr int JP_THREADS = 256;
+constexpr int JP_SPLIT = 8;                // workgroups per jump
+constexpr int JP_W = NW / JP_SPLIT;        // 78 words each
+constexpr int JP_ZERO = 2 * NW;            // sentinel position: buf[JP_ZERO ..] holds zeros
+static_assert(NW % JP_SPLIT == 0, "share");
+__global__ void __launch_bounds__(JP_THREADS) mt_jump_kernel(const uint32_t* srcs, uint32_t* dsts, const int* pos,
+                                                              const int* bptr, int npos) {
+  __shared__ uint32_t buf[2 * NW + 2 * NW];
+  __shared__ uint32_t fixw[2];
+  extern __shared__ int sp[];
+  const int t = threadIdx.x, g = blockIdx.y;
   const uint32_t* src = srcs + (size_t)blockIdx.x * NW;
   uint32_t* dst = dsts + (size_t)blockIdx.x * NW;
-  if (t < NW) buf[t] = src[t];
-  for (int k = t; k < PW; k += JUMP_THREADS) pc[k] = poly[k];
+  for (int i = t; i < NW; i += JP_THREADS) buf[i] = src[i];
+  for (int i = t; i < 2 * NW; i += JP_THREADS) buf[JP_ZERO + i] = 0u;
+  for (int i = t; i < npos; i += JP_THREADS) sp[i] = pos[i];
   __syncthreads();
-  uint32_t acc = 0;
+  uint32_t a = 0;
+  // this lane's window word: the share's JP_W words; share 0 also follows words 396 and 623 (lanes JP_W,
+  // JP_W + 1), which word 0's low bits are recomputed from
+  const int w = t < JP_W ? g * JP_W + t : (g == 0 && t == JP_W ? 396 : (g == 0 && t == JP_W + 1 ? 623 : 0));
   for (int blk = 0; blk * NW < DEG; ++blk) {
-    next_block_lds<JUMP_THREADS>(buf, t);
-    const int k0 = blk * NW, k1 = min(k0 + NW, DEG);
-    if (t < NW) {
-      for (int w = k0 >> 6; w <= (k1 - 1) >> 6; ++w) {
-        uint64_t m = pc[w];
-        const int b0 = w * 64;
-        if (b0 < k0) m &= ~0ull << (k0 - b0);
-        if (b0 + 64 > k1) m &= (k1 - b0 >= 64) ? ~0ull : ((1ull << (k1 - b0)) - 1);
-        while (m) {
-          const int b = __builtin_ctzll(m);
-          m &= m - 1;
-          acc ^= buf[b0 + b - k0 + t];
-        }
+    next_block_lds<JP_THREADS>(buf, t);
+    const int q0 = bptr[blk], q1 = bptr[blk + 1];
+    if (t < 128) {
+      for (int q = q0; q < q1; q += 8) {
+        const int4 k0 = *reinterpret_cast<const int4*>(sp + q);
+        const int4 k1 = *reinterpret_cast<const int4*>(sp + q + 4);
+        const uint32_t x0 = buf[k0.x + w], x1 = buf[k0.y + w], x2 = buf[k0.z + w], x3 = buf[k0.w + w];
+        const uint32_t x4 = buf[k1.x + w], x5 = buf[k1.y + w], x6 = buf[k1.z + w], x7 = buf[k1.w + w];
+        a ^= ((x0 ^ x1) ^ (x2 ^ x3)) ^ ((x4 ^ x5) ^ (x6 ^ x7));
       }
     }
     __syncthreads();
-    if (t < NW) buf[t] = buf[NW + t];
+    for (int i = t; i < NW; i += JP_THREADS) buf[i] = buf[NW + i];
     __syncthreads();
   }
-  if (t < NW) buf[t] = acc;
+  if (g == 0 && (t == JP_W || t == JP_W + 1)) fixw[t - JP_W] = a;
   __syncthreads();
-  if (t < NW) dst[t] = t == 0 ? fix_first(acc, buf[396], buf[623]) : acc;
+  if (t < JP_W) dst[w] = (g == 0 && t == 0) ? fix_first(a, fixw[0], fixw[1]) : a;
 }
 
 // segment s = seg0 + workgroup (window win[workgroup]): blocks [s * SEG_BLOCKS, ...) of the device part of the
@@ -342,22 +355,27 @@ __device__ __forceinline__ int64_t last_le(const int64_t* a, int64_t n, int64_t 
   return lo;
 }
 
-// one thread per entry of the epoch: batch bi's doubles are [bi*B + ebase[bi], ...): B row sparsities, then
-// the entries' uniforms in batch order (data_reader.py:120 then :130 row by row)
-__global__ void __launch_bounds__(256) recip_keep_kernel(const uint32_t* words, const int64_t* boff,
-                                                          const int64_t* ebase, int nb, int B, double s0, double s1,
-                                                          uint8_t* keep, int64_t E) {
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= E) return;
-  const int64_t bi = last_le(ebase, nb, g);
-  const int64_t e = g - ebase[bi];
-  const int64_t* off = boff + bi * (B + 1);
-  const int64_t b = last_le(off, B, e);
-  const int64_t d0 = bi * (int64_t)B + ebase[bi];
-  const int64_t dr = d0 + b, de = d0 + B + e;
-  const double s = s0 + (s1 - s0) * to_double(words[2 * dr], words[2 * dr + 1]);
-  const double cut = (1.0 - s) / ((1.0 - s) + s);
-  keep[g] = to_double(words[2 * de], words[2 * de + 1]) >= cut ? 1 : 0;
+// workgroups (x, bi): batch bi's entries, grid-stride over x; the batch's row offsets staged in LDS.  Batch
+// bi's doubles are [bi*B + ebase[bi], ...): B row sparsities, then the entries' uniforms in batch order
+// (data_reader.py:120 then :130 row by row)
+constexpr int RK_THREADS = 256;
+constexpr int RK_BLOCKS = 64;    // workgroups per batch
+__global__ void __launch_bounds__(RK_THREADS) recip_keep_kernel(const uint32_t* words, const int64_t* boff,
+                                                                 const int64_t* ebase, int B, double s0, double s1,
+                                                                 uint8_t* keep) {
+  extern __shared__ int64_t off[];
+  const int64_t bi = blockIdx.y;
+  for (int i = threadIdx.x; i <= B; i += RK_THREADS) off[i] = boff[bi * (B + 1) + i];
+  __syncthreads();
+  const int64_t eb = ebase[bi], E = off[B];
+  const int64_t d0 = bi * (int64_t)B + eb;
+  for (int64_t e = (int64_t)blockIdx.x * RK_THREADS + threadIdx.x; e < E; e += (int64_t)RK_BLOCKS * RK_THREADS) {
+    const int64_t b = last_le(off, B, e);
+    const int64_t dr = d0 + b, de = d0 + B + e;
+    const double s = s0 + (s1 - s0) * to_double(words[2 * dr], words[2 * dr + 1]);
+    const double cut = (1.0 - s) / ((1.0 - s) + s);
+    keep[eb + e] = to_double(words[2 * de], words[2 * de + 1]) >= cut ? 1 : 0;
+  }
 }
 
 // ---------------------------------------------------------------- plan shared by host and device paths
@@ -400,12 +418,37 @@ static void end_state(const Plan& p, const uint32_t* key_in, int pos_in, const u
   }
 }
 
-struct DevTables {
-  uint64_t* q = nullptr;   // [QMAX][PW] on this device
-  int have = 0;            // q[SEG_LOG .. SEG_LOG + have) uploaded
+// a jump polynomial as the device kernel reads it: set-coefficient positions, block by block (position
+// k of block b stored as k - 624 b), each block padded to a multiple of 8 with JP_ZERO
+struct JumpList {
+  std::vector<int> pos;
+  int bptr[34];
 };
 
-static uint64_t* device_jump_polys(int rounds) {
+static JumpList jump_list(const Poly& q) {
+  JumpList L;
+  const int nblk = (DEG + NW - 1) / NW;
+  for (int b = 0; b < nblk; ++b) {
+    L.bptr[b] = (int)L.pos.size();
+    for (int k = b * NW; k < std::min((b + 1) * NW, DEG); ++k)
+      if (bit(q.w, k)) L.pos.push_back(k - b * NW);
+    while (L.pos.size() % 8) L.pos.push_back(JP_ZERO);
+  }
+  for (int b = nblk; b < 34; ++b) L.bptr[b] = (int)L.pos.size();
+  return L;
+}
+
+struct DevJump {
+  const int* pos;
+  const int* bptr;
+  int npos;
+};
+
+struct DevTables {
+  std::vector<DevJump> r;   // r[i]: Q_{SEG_LOG + i}
+};
+
+static std::vector<DevJump> device_jump_lists(int rounds) {
   static std::mutex mx;
   static std::vector<DevTables> per_dev;
   int dev = 0;
@@ -413,14 +456,18 @@ static uint64_t* device_jump_polys(int rounds) {
   std::lock_guard<std::mutex> g(mx);
   if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1);
   DevTables& d = per_dev[dev];
-  if (!d.q) OCF_HIP(hipMalloc(&d.q, (size_t)QMAX * PW * 8));
-  if (d.have < rounds) {
+  if ((int)d.r.size() < rounds) {
     const Tables& t = jump_tables(SEG_LOG + rounds - 1);
-    for (int r = d.have; r < rounds; ++r)
-      OCF_HIP(hipMemcpy(d.q + (size_t)r * PW, t.q[SEG_LOG + r].w, PW * 8, hipMemcpyHostToDevice));
-    d.have = rounds;
+    for (int i = (int)d.r.size(); i < rounds; ++i) {
+      const JumpList L = jump_list(t.q[SEG_LOG + i]);
+      int* buf = nullptr;   // one allocation per polynomial, kept for the process (a few tens of KB)
+      OCF_HIP(hipMalloc(&buf, (L.pos.size() + 34) * sizeof(int)));
+      OCF_HIP(hipMemcpy(buf, L.pos.data(), L.pos.size() * sizeof(int), hipMemcpyHostToDevice));
+      OCF_HIP(hipMemcpy(buf + L.pos.size(), L.bptr, 34 * sizeof(int), hipMemcpyHostToDevice));
+      d.r.push_back(DevJump{buf, buf + L.pos.size(), (int)L.pos.size()});
+    }
   }
-  return d.q;
+  return std::vector<DevJump>(d.r.begin(), d.r.begin() + rounds);
 }
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -479,12 +526,12 @@ extern "C" int ocf_recip_keep(OcfRecipKeepArgs* a, void* stream) {
   if (stream_out) {
     // every segment: windows [2^r, 2^(r+1)) from windows [0, 2^r) by x^(2^r segments), r < rounds
     if (p.nblocks > 0) {
-      const uint64_t* q = device_jump_polys(p.rounds);
+      const std::vector<DevJump> q = device_jump_lists(p.rounds);
       for (int r = 0; r < p.rounds; ++r) {
         const int half = 1 << r;
         const int jobs = std::min(half, p.S - half);
-        hipLaunchKernelGGL(mt_jump_kernel, dim3(jobs), dim3(JUMP_THREADS), 0, s, win, win + (size_t)half * NW,
-                           q + (size_t)r * PW);
+        hipLaunchKernelGGL(mt_jump_kernel, dim3(jobs, JP_SPLIT), dim3(JP_THREADS), q[r].npos * sizeof(int), s, win,
+                           win + (size_t)half * NW, q[r].pos, q[r].bptr, q[r].npos);
         OCF_HIP(hipGetLastError());
       }
     }
@@ -496,12 +543,12 @@ extern "C" int ocf_recip_keep(OcfRecipKeepArgs* a, void* stream) {
     const int64_t sq = p.bq / SEG_BLOCKS;
     int top = 0;
     while ((sq >> top) > 1) ++top;
-    const uint64_t* q = device_jump_polys(sq ? top + 1 : 0);
+    const std::vector<DevJump> q = device_jump_lists(sq ? top + 1 : 0);
     int cur = 0;
     for (int k = 0; sq && k <= top; ++k)
       if ((sq >> k) & 1) {
-        hipLaunchKernelGGL(mt_jump_kernel, dim3(1), dim3(JUMP_THREADS), 0, s, win + (size_t)cur * NW,
-                           win + (size_t)(cur ^ 1) * NW, q + (size_t)k * PW);
+        hipLaunchKernelGGL(mt_jump_kernel, dim3(1, JP_SPLIT), dim3(JP_THREADS), q[k].npos * sizeof(int), s,
+                           win + (size_t)cur * NW, win + (size_t)(cur ^ 1) * NW, q[k].pos, q[k].bptr, q[k].npos);
         OCF_HIP(hipGetLastError());
         cur ^= 1;
       }
@@ -510,9 +557,9 @@ extern "C" int ocf_recip_keep(OcfRecipKeepArgs* a, void* stream) {
     OCF_HIP(hipGetLastError());
   }
   if (a->keep && a->n_entries > 0) {
-    const unsigned grid = (unsigned)((a->n_entries + 255) / 256);
-    hipLaunchKernelGGL(recip_keep_kernel, dim3(grid), dim3(256), 0, s, words, a->boff, a->ebase, a->nb, a->B, a->s0,
-                       a->s1, a->keep, a->n_entries);
+    OCF_CHECK(a->B <= 16384, "ocf_recip_keep: B <= 16384 (the batch's row offsets are staged in LDS)");
+    hipLaunchKernelGGL(recip_keep_kernel, dim3(RK_BLOCKS, a->nb), dim3(RK_THREADS), (size_t)(a->B + 1) * 8, s, words,
+                       a->boff, a->ebase, a->B, a->s0, a->s1, a->keep);
     OCF_HIP(hipGetLastError());
   }
   if (a->doubles) {   // the raw uniform stream (tests): words -> doubles on the host side of the copy
