@@ -298,6 +298,16 @@ int ocf_splitk_grad_act(const float* slabs, int splits, int64_t split_stride, in
 /* ocf_opt_step -- elementwise Adagrad / RMSprop / Adam / SGD update (Keras 2.0.4 get_updates);
  * g is multiplied by opt.gscale.  Used for biases and after the data-parallel all-reduce. */
 int ocf_opt_step(float* p, const float* g, float* s1, float* s2, int64_t n, const OcfOptParams* opt, void* stream);
+/* ocf_opt_step_ex -- ocf_opt_step on a gradient in fp32 or bf16 (g_dtype OCF_F32 / OCF_BF16: a
+ * data-parallel reduce-scatter shard as it arrives), optionally writing the updated parameter rounded
+ * to the compute dtype into shadow (OCF_F16 / OCF_BF16, RNE; the 16-bit weight copy the row gathers
+ * read), so the data-parallel step all-gathers only the 16-bit shard (extension; no reference
+ * counterpart -- the reference runs on one device). */
+typedef struct OcfOptStepArgs {
+  float* p; const void* g; int g_dtype; float* s1; float* s2; int64_t n; OcfOptParams opt;
+  void* shadow; int shadow_dtype;
+} OcfOptStepArgs;
+int ocf_opt_step_ex(const OcfOptStepArgs* args, void* stream);
 
 /* bias update from per-row-tile column partials db_part[parts][ld] (fixed summation order). */
 int ocf_bias_opt_from_partials(float* b, const float* db_part, int parts, int64_t ld, int n, float* s1, float* s2,

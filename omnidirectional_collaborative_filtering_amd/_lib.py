@@ -128,6 +128,11 @@ class OcfTileBucketArgs(ctypes.Structure):
     ]
 
 
+class OcfOptStepArgs(ctypes.Structure):
+    _fields_ = [("p", P), ("g", P), ("g_dtype", I32), ("s1", P), ("s2", P), ("n", I64), ("opt", OcfOptParams),
+                ("shadow", P), ("shadow_dtype", I32)]
+
+
 class OcfRecipKeepArgs(ctypes.Structure):
     _fields_ = [
         ("key", ctypes.c_uint32 * 624), ("pos", ctypes.c_int32), ("nb", ctypes.c_int32), ("B", ctypes.c_int32),
@@ -145,6 +150,7 @@ SIGNATURES = {
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),
+    "ocf_opt_step_ex": (I32, [ctypes.POINTER(OcfOptStepArgs), P]),
     "ocf_bias_opt_from_partials": (I32, [P, P, I32, I64, I32, P, P, P, ctypes.POINTER(OcfOptParams), P]),
     "ocf_stats_finalize": (I32, [P, I32, P, I32, I32, P, P]),
     "ocf_sumsq": (I32, [P, I64, F32, P, P, P]),

@@ -1,6 +1,7 @@
 // Split-K reductions fused with the layer epilogues, elementwise optimizers, stats reduction,
 // and the library's error state.
 #include <string>
+#include <type_traits>
 
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
@@ -62,6 +63,27 @@ __global__ void opt_kernel(float* p, const float* g, float* s1, float* s2, int64
     p[i] = w;
     if (s1) s1[i] = a;
     if (s2) s2[i] = b;
+  }
+}
+
+// ocf_opt_step_ex: gradient in fp32 or bf16 (the data-parallel reduce-scatter's shard, no widening copy),
+// and the updated parameter rounded once more into the compute-dtype shadow (the same RNE rounding the
+// fused EPI_OPTIM epilogue and a torch .to() apply), so a sharded update leaves the shadow shard ready
+// for the all-gather
+template <typename GT, typename ST>
+__global__ void __launch_bounds__(256) opt_ex_kernel(float* p, const GT* g, float* s1, float* s2, ST* sh, int64_t n,
+                                                     OcfOptParams o) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (; i < n; i += stride) {
+    float w = p[i];
+    float a = s1 ? s1[i] : 0.f;
+    float b = s2 ? s2[i] : 0.f;
+    opt_update(o, (float)g[i] * o.gscale, w, a, b);
+    p[i] = w;
+    if (s1) s1[i] = a;
+    if (s2) s2[i] = b;
+    if constexpr (!std::is_same<ST, float>::value) sh[i] = (ST)w;
   }
 }
 
@@ -209,6 +231,30 @@ extern "C" int ocf_opt_step(float* p, const float* g, float* s1, float* s2, int6
   int64_t blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(opt_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, g, s1, s2, n, *opt);
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+extern "C" int ocf_opt_step_ex(const OcfOptStepArgs* a, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(a && a->p && a->g, "ocf_opt_step_ex: null pointer");
+  OCF_CHECK(a->g_dtype == OCF_F32 || a->g_dtype == OCF_BF16, "ocf_opt_step_ex: gradients fp32 or bf16");
+  OCF_CHECK(!a->shadow || a->shadow_dtype == OCF_F16 || a->shadow_dtype == OCF_BF16,
+            "ocf_opt_step_ex: shadow f16 or bf16");
+  if (a->n == 0) return 0;
+  int64_t blocks = (a->n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipStream_t s = (hipStream_t)stream;
+  auto go = [&](auto gt, auto st) {
+    using GT = decltype(gt);
+    using ST = decltype(st);
+    hipLaunchKernelGGL((opt_ex_kernel<GT, ST>), dim3((unsigned)blocks), dim3(256), 0, s, a->p,
+                       reinterpret_cast<const GT*>(a->g), a->s1, a->s2, reinterpret_cast<ST*>(a->shadow), a->n, a->opt);
+  };
+  const bool gb = a->g_dtype == OCF_BF16;
+  if (!a->shadow) gb ? go(__bf16{}, 0.f) : go(0.f, 0.f);
+  else if (a->shadow_dtype == OCF_F16) gb ? go(__bf16{}, _Float16{}) : go(0.f, _Float16{});
+  else gb ? go(__bf16{}, __bf16{}) : go(0.f, __bf16{});
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

@@ -29,9 +29,12 @@ import torch
 from . import _lib
 from .dataset import FixedSplit, load_reference_json
 from .engine import TILE, cur_stream, ptr, ru
+from .parallel import shard_batches
 
 AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
 GATHER_CHUNK = int(os.environ.get("OCF_GATHER_CHUNK", 256))   # entries per row-gather work unit (ocf_gather_*)
+ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the library takes up to 65,535)
+ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
 
 
 _RNG_STREAMS = {}
@@ -153,6 +156,7 @@ class BatchGenerator(object):
         self.num_batches = self.n // B                                   # data_reader.py:329
         self.i = 0
         self.started = False
+        self.dp_shard = None          # (rank, world) under data parallelism (Model._train_one)
         self.seed = int(np.random.randint(0, 2 ** 31 - 1)) if reader.rng == "device" else 0
 
     # ------------------------------------------------------------ epoch plan
@@ -288,9 +292,19 @@ class BatchGenerator(object):
         if self.split != "train":
             raise ValueError("row lists are built for train batches (inputs = targets)")
         nb = self.num_batches
-        sel = np.arange(nb, dtype=np.int64) if batches is None else np.unique(np.asarray(batches, dtype=np.int64))
+        if batches is None:
+            # under data parallelism a rank only trains on its own batches (parallel.shard_batches)
+            batches = shard_batches(nb, *self.dp_shard) if self.dp_shard else np.arange(nb)
+        sel = np.unique(np.asarray(batches, dtype=np.int64))
         if len(sel) and (sel[0] < 0 or sel[-1] >= nb):
             raise ValueError("batch index out of range")
+        # one build holds at most ROWLIST_MAX_BATCHES batches and ~1 GiB of row pointers (the library's
+        # limit is 65,535); row_lists() builds the next window when it reaches a batch outside this one
+        cap = int(min(ROWLIST_MAX_BATCHES, max(1, (1 << 28) // (n_cols + 1))))
+        if len(sel) > cap:
+            sel = sel[:cap]
+        if self.src1.dup is not None and len(sel):
+            self._check_list_lengths(sel)
         dev = self.rows_dev.device
         ebase = np.zeros(len(sel) + 1, dtype=np.int64)
         np.cumsum(self.nnz1[sel], out=ebase[1:])
@@ -331,12 +345,25 @@ class BatchGenerator(object):
         keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
         self._rl = keep
 
+    def _check_list_lengths(self, sel):
+        """duplicate (row, col) ratings: a column can hold more entries than batch rows; the row-list build
+        sorts a list of up to 4,096 entries (ocf_epoch_row_lists) -- refuse longer ones loudly"""
+        csr = self.src1.host
+        for bi in sel:
+            idx = np.concatenate([np.arange(csr.row_ptr[r], csr.row_ptr[r + 1]) for r in self.rows_host[bi]])
+            if len(idx) and np.bincount(csr.col[idx]).max() > ROWLIST_MAX_ENTRIES:
+                raise ValueError("batch %d: a column holds more than %d entries (duplicate ratings); the row-list "
+                                 "build takes at most %d per column -- use a smaller batch_size"
+                                 % (bi, ROWLIST_MAX_ENTRIES, ROWLIST_MAX_ENTRIES))
+
     def row_lists(self, bi, n_cols):
         """device pointers of batch bi's row lists (sp_rowptr / sp_rowent of the row-stream weight-gradient
-        kernel) and live records; the whole epoch's are built on first use"""
+        kernel) and live records; the epoch's (or this rank's) are built on first use, in windows of at most
+        ROWLIST_MAX_BATCHES batches"""
         rl = getattr(self, "_rl", None)
         if rl is None or rl["n_cols"] != n_cols or bi not in rl["slot"]:
-            self.prepare_row_lists(n_cols)
+            want = shard_batches(self.num_batches, *self.dp_shard) if self.dp_shard else range(self.num_batches)
+            self.prepare_row_lists(n_cols, [b for b in want if b >= bi] or [bi])
             rl = self._rl
         s = rl["slot"][bi]
         e0 = int(rl["ebase_host"][s])

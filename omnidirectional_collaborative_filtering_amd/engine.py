@@ -101,6 +101,9 @@ class Engine:
         # layer i's raw gradients are written (grads_out steps), so its exchange can start right away
         self.dp_rank, self.dp_world = 0, 1
         self.grad_hook = None
+        # data parallelism with ZeRO-1 masters (parallel.DataParallel): gathers the fp32 weights before
+        # anything reads them outside the step (get_weights, predict, the l2 penalty)
+        self.master_sync = None
         self.opt = None
         self.slots = []
         self._alloc_params()
@@ -130,13 +133,17 @@ class Engine:
                 self.Wsh[i] = torch.zeros(self.W[i].shape, device=self.dev, dtype=self.tdt)
 
     def _refresh_shadows(self):
-        for w, sh in zip(self.W, self.Wsh):
-            if sh is not None:
-                if self.shadow_blocked:     # 64x64 blocks, 8 KB contiguous each (ocf.h b_blocked)
-                    R, C = w.shape
-                    sh.view(R // 64, C // 64, 64, 64).copy_(w.view(R // 64, 64, C // 64, 64).permute(0, 2, 1, 3))
-                else:
-                    sh.copy_(w)
+        for i in range(len(self.W)):
+            self._refresh_shadow(i)
+
+    def _refresh_shadow(self, i):
+        w, sh = self.W[i], self.Wsh[i]
+        if sh is not None:
+            if self.shadow_blocked:     # 64x64 blocks, 8 KB contiguous each (ocf.h b_blocked)
+                R, C = w.shape
+                sh.view(R // 64, C // 64, 64, 64).copy_(w.view(R // 64, 64, C // 64, 64).permute(0, 2, 1, 3))
+            else:
+                sh.copy_(w)
 
     def _wblk(self, i):
         return int(self.Wsh[i] is not None and self.shadow_blocked)
@@ -175,6 +182,8 @@ class Engine:
 
     def get_weights(self):
         """Keras-layout numpy list [W0, b0, W1, b1, ...] (padding stripped)."""
+        if self.master_sync is not None:
+            self.master_sync()
         out = []
         for i, b in enumerate(self.b):
             rows = torch.as_tensor(self._row_map(i), device=self.dev)
@@ -779,6 +788,8 @@ class Engine:
 
     def predict_dense(self, out_mask, out):
         """PREDICT epilogue: out[B][N] = out_mask * (h W + b)."""
+        if self.master_sync is not None:
+            self.master_sync()
         L = len(self.H)
         self._gemm(self.h[L - 1], 0, self.Hp[L - 1], self.W[L], _lib.DT_F32, 0, self.Hp[L - 1], self.Bp, self.Np,
                    self.Hp[L - 1], _lib.EPI_PREDICT, bias=self.b[L], pmask=out_mask,

@@ -75,6 +75,7 @@ class Model(object):
     def _train_one(self, gen):
         """One optimizer step; under data parallelism rank r takes the r-th of the next `world` batches."""
         if self.world > 1 and isinstance(gen, BatchGenerator):
+            gen.dp_shard = (self.rank, self.world)
             idx = [gen.next_batch_index() for _ in range(self.world)]
             if idx[-1] is None:
                 raise StopIteration("generator exhausted")
@@ -310,6 +311,8 @@ class Model(object):
         e = self.engine
         if self.dp is not None:
             self.dp.gather_slots()
+            if e.master_sync is not None:       # ZeRO-1 masters: a collective, so on every rank
+                e.master_sync()
             if self.rank != 0:
                 return
         path = self.shard_path(path)

@@ -77,23 +77,25 @@ class ShardedSync:
       start(j)         : reduce-scatter of grads[j] (sum; fp32 or bf16) into this rank's shard buffer,
                          asynchronous -- issued as soon as the engine has written that gradient, so the
                          output layer's exchange overlaps the input layer's weight-gradient kernel;
-      finish(update)   : for every started tensor in order: wait, update(j, lo, hi, g_shard_fp32) (the
-                         optimizer on this rank's 1/G of the parameters and slots), then an asynchronous
-                         all-gather of the updated parameter shard into the full tensor; waits for all.
-    Traffic per step: (G-1)/G of the gradient bytes (bf16: half) + (G-1)/G of the fp32 parameters,
-    the same as one all-reduce, with the HBM-bound optimizer pass cut to 1/G per rank."""
+      finish(update)   : for every started tensor in order: wait, update(j, lo, hi, g_shard) (the
+                         optimizer on this rank's 1/G of the parameters and slots; g_shard in the
+                         gradient's dtype), then an asynchronous in-place all-gather of gather[j]'s
+                         updated shard into the full gather[j] (default: the fp32 parameter; the 16-bit
+                         weight shadow under ZeRO-1, DataParallel); waits for all.
+    Traffic per step: (G-1)/G of the gradient bytes (bf16: half) + (G-1)/G of the gathered bytes (fp32
+    parameters, or 16-bit shadows: half), with the HBM-bound optimizer pass cut to 1/G per rank."""
 
-    def __init__(self, params, grads, rank, world, group=None):
+    def __init__(self, params, grads, rank, world, group=None, gather=None):
         self.params, self.grads = params, grads
+        self.gather = list(gather) if gather is not None else list(params)
         self.rank, self.world, self.group = rank, world, group
         self.backend = dist.get_backend(group) if dist.is_initialized() else "gloo"
-        for p, g in zip(params, grads):
-            if p.numel() % world or (p.numel() // world) % 4:
+        for p, g, t in zip(params, grads, self.gather):
+            if not shardable(p.numel(), world):
                 raise ValueError("tensor of %d elements does not split into %d 16-B aligned shards" % (p.numel(), world))
-            if g.numel() != p.numel():
-                raise ValueError("gradient / parameter size mismatch")
+            if g.numel() != p.numel() or t.numel() != p.numel():
+                raise ValueError("gradient / gathered / parameter size mismatch")
         self.shard = [torch.empty(g.numel() // world, dtype=g.dtype, device=g.device) for g in grads]
-        self.shard32 = [s if s.dtype == torch.float32 else torch.empty(s.numel(), device=s.device) for s in self.shard]
         self._started = []
 
     def bounds(self, j):
@@ -117,12 +119,9 @@ class ShardedSync:
         for j, work in self._started:
             if work is not None:
                 work.wait()
-            g32 = self.shard32[j]
-            if g32 is not self.shard[j]:
-                g32.copy_(self.shard[j])
             lo, hi = self.bounds(j)
-            update(j, lo, hi, g32)
-            flat = self.params[j].view(-1)
+            update(j, lo, hi, self.shard[j])
+            flat = self.gather[j].view(-1)
             mine = flat[lo:hi]
             if _staged(self.backend, flat):
                 fh = torch.empty(flat.numel(), dtype=flat.dtype)
@@ -135,8 +134,8 @@ class ShardedSync:
         self._started = []
 
     def gather_tensors(self, tensors):
-        """all-gather every rank's shard of same-shaped companions of the parameters (optimizer slots,
-        before a checkpoint)"""
+        """all-gather every rank's shard of same-shaped companions of the parameters (optimizer slots
+        before a checkpoint; the fp32 masters under ZeRO-1)"""
         for j, t in enumerate(tensors):
             if t is None:
                 continue
@@ -150,6 +149,11 @@ class ShardedSync:
                 dist.all_gather_into_tensor(flat, flat[lo:hi].clone(), group=self.group)
 
 
+def shardable(n, world):
+    """n elements split into `world` equal shards of a multiple of 4 elements (16-B aligned)"""
+    return n % world == 0 and (n // world) % 4 == 0
+
+
 class DataParallel:
     """Row (user/item-batch) data parallelism of one Engine replica per rank -- the north_star's
     "user-batch data parallelism with RCCL gradient all-reduce", with SURVEY 8(e)'s mitigations.
@@ -157,12 +161,19 @@ class DataParallel:
     mode 'sharded' (default): the engine writes raw per-layer gradients (EPI_GRAD; bf16 with
       grad_dtype='bfloat16'); each layer's reduce-scatter starts as soon as that layer's gradient is
       written (the output layer's overlaps the input layer's weight-gradient kernel); every rank updates
-      its 1/G of every parameter tensor and its slots (ocf_opt_step) and all-gathers the parameters.
+      its 1/G of every parameter tensor and its slots (ocf_opt_step_ex, reading the shard in its own
+      dtype).  ZeRO-1 for the weights the kernels read through a 16-bit row-major shadow (first and last
+      layer in f16 / bf16 compute, l2 = 0): the update also writes the shadow shard and only the shadow is
+      all-gathered -- half the bytes, no per-step shadow refresh; the fp32 masters stay sharded (each rank
+      current on its 1/G) until get_weights / save / predict gathers them (gather_masters).  Every other
+      tensor: the fp32 parameter shard is all-gathered.
     mode 'allreduce': one flat fp32 bucket, one all-reduce, the full optimizer on every rank.
-    Both start from rank 0's weights (broadcast here), and the engine mixes the rank into the Philox
-    stream of its dropout masks so the G local batches draw independent masks like one global batch."""
+    A tensor that does not split into G 16-B aligned shards (e.g. G = 3, 5, 6) makes 'sharded' fall back
+    to 'allreduce' (with a warning).  Both start from rank 0's weights (broadcast here), and the engine
+    mixes the rank into the Philox stream of its dropout masks so the G local batches draw independent
+    masks like one global batch."""
 
-    def __init__(self, engine, rank, world, mode="sharded", grad_dtype="float32", group=None):
+    def __init__(self, engine, rank, world, mode="sharded", grad_dtype="float32", group=None, zero=True):
         if mode not in ("sharded", "allreduce"):
             raise ValueError("mode must be 'sharded' or 'allreduce'")
         if grad_dtype not in ("float32", "bfloat16"):
@@ -170,10 +181,20 @@ class DataParallel:
         if grad_dtype == "bfloat16" and mode != "sharded":
             raise ValueError("bf16 gradients need mode='sharded'")
         self.engine, self.rank, self.world, self.group = engine, int(rank), int(world), group
+        params = [t for w, b in zip(engine.W, engine.b) for t in (w, b)]
+        if mode == "sharded" and not all(shardable(p.numel(), self.world) for p in params):
+            import warnings
+            warnings.warn("DataParallel: parameters do not split into %d aligned shards; using mode='allreduce'"
+                          % self.world)
+            mode, grad_dtype = "allreduce", "float32"
         self.mode, self.grad_dtype = mode, grad_dtype
         engine.dp_rank, engine.dp_world = self.rank, self.world
         self.broadcast_params()
-        params = [t for w, b in zip(engine.W, engine.b) for t in (w, b)]
+        # ZeRO-1 layers: weights read only through a row-major 16-bit shadow
+        self.zero_layers = set()
+        if mode == "sharded" and zero and not engine.l2 and not engine.shadow_blocked:
+            self.zero_layers = {i for i, sh in enumerate(engine.Wsh) if sh is not None}
+        self._masters_stale = False
         if mode == "allreduce":
             self.bucket = GradBucket(engine)
             self.views = self.bucket.views
@@ -184,7 +205,10 @@ class DataParallel:
             for w, b in zip(engine.W, engine.b):
                 self.views += [torch.zeros(w.shape, device=engine.dev, dtype=gdt),
                                torch.zeros(b.shape, device=engine.dev, dtype=torch.float32)]
-            self.sync = ShardedSync(params, self.views, self.rank, self.world, group)
+            gather = [engine.Wsh[j // 2] if (j % 2 == 0 and j // 2 in self.zero_layers) else p
+                      for j, p in enumerate(params)]
+            self.sync = ShardedSync(params, self.views, self.rank, self.world, group, gather=gather)
+        engine.master_sync = self.gather_masters if self.zero_layers else None
 
     def broadcast_params(self):
         e = self.engine
@@ -198,6 +222,15 @@ class DataParallel:
                     dist.broadcast(t, 0, group=self.group)
         e._refresh_shadows()
 
+    def gather_masters(self):
+        """ZeRO-1: every rank's fp32 master shards -> full fp32 weights (before reading them)"""
+        if not self._masters_stale:
+            return
+        e = self.engine
+        self.sync.gather_tensors([e.W[j // 2] if (j % 2 == 0 and j // 2 in self.zero_layers) else None
+                                  for j in range(2 * len(e.W))])
+        self._masters_stale = False
+
     def step(self):
         e = self.engine
         if self.mode == "allreduce":
@@ -205,6 +238,7 @@ class DataParallel:
             grad_sync(self.bucket, self.world)
             e.apply_grads(self.views, scale=1.0 / self.world)
             return
+        from . import _lib
         sync = self.sync
         e.grad_hook = lambda i: (sync.start(2 * i), sync.start(2 * i + 1))
         try:
@@ -214,6 +248,7 @@ class DataParallel:
         scale = 1.0 / self.world
         opw = e.opt.step_params(scale, e.l2)     # l2 regularises kernels only
         opb = e.opt.step_params(scale, 0.0)
+        stream = torch.cuda.current_stream().cuda_stream
 
         def update(j, lo, hi, g):
             i = j // 2
@@ -223,11 +258,22 @@ class DataParallel:
             sw, sb = e.slots[i]
             s = sw if j % 2 == 0 else sb
             f = lambda t: None if t is None else t.view(-1)[lo:hi].data_ptr()
-            from . import _lib
-            _lib.call("ocf_opt_step", f(p), g.data_ptr(), f(s[0]), f(s[1]), hi - lo, opw if j % 2 == 0 else opb,
-                      torch.cuda.current_stream().cuda_stream)
+            a = _lib.OcfOptStepArgs()
+            a.p, a.g, a.s1, a.s2, a.n = f(p), g.data_ptr(), f(s[0]), f(s[1]), hi - lo
+            a.g_dtype = _lib.DT_BF16 if g.dtype == torch.bfloat16 else _lib.DT_F32
+            a.opt = opw if j % 2 == 0 else opb
+            if j % 2 == 0 and i in self.zero_layers:
+                a.shadow, a.shadow_dtype = f(e.Wsh[i]), e.cdt
+            _lib.call("ocf_opt_step_ex", a, stream)
         sync.finish(update)
-        e._refresh_shadows()
+        if self.zero_layers:
+            self._masters_stale = True
+            # shadows of the other layers (none in the ZeRO-1 layouts; kept for completeness)
+            for i, sh in enumerate(e.Wsh):
+                if sh is not None and i not in self.zero_layers:
+                    e._refresh_shadow(i)
+        else:
+            e._refresh_shadows()
         e.opt.iterations += 1
 
     def gather_slots(self):

@@ -64,6 +64,7 @@ STRUCTS = {
                                                        "ebase", "cnt", "row_ptr", "row_ent", "live"]),
     "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
                                                        "xval", "tflag"]),
+    "OcfOptStepArgs": (_lib.OcfOptStepArgs, ["p", "g", "g_dtype", "s1", "s2", "n", "opt", "shadow", "shadow_dtype"]),
     "OcfRecipKeepArgs": (_lib.OcfRecipKeepArgs, ["key", "pos", "nb", "B", "n_entries", "boff", "ebase", "s0", "s1",
                                                  "keep", "doubles", "workspace", "workspace_bytes"]),
 }

@@ -95,7 +95,7 @@ def _sharded_worker(rank, world, port, q, gdt):
         sync.start(j)
 
     def update(j, lo, hi, g):            # Keras Adagrad, lr 0.005, on the shard, gradient / world
-        g = g / world
+        g = g.float() / world
         a = acc[j].view(-1)[lo:hi]
         a += g * g
         params[j].view(-1)[lo:hi] -= 0.005 * g / (a.sqrt() + 1e-8)
@@ -136,3 +136,128 @@ def test_sharded_update_equals_one_global_step(gdt):
                 np.testing.assert_allclose(ga, wa, rtol=1e-5, atol=1e-12)
     for a, b in zip(res[0][1], res[1][1]):               # replicas identical
         np.testing.assert_array_equal(a, b)
+
+
+def test_sharded_rccl_branch_ordering(monkeypatch):
+    """The data-parallel step's RCCL branch (async reduce-scatter / in-place all-gather), which the gloo
+    tests never take (they stage collectives through host copies), driven in one process with a stubbed
+    torch.distributed that records the call order: every layer's reduce-scatter starts only after that
+    layer's gradients are written (Engine.grad_hook), each shard's update runs only after its reduce-scatter
+    was waited on, the all-gather sends this rank's slice of the gathered tensor into that tensor
+    (in place), ZeRO-1 gathers the 16-bit shadows of the first / last layer (the update writes the shadow
+    shard) and the fp32 tensors otherwise, and every gather is waited on before the step returns."""
+    from omnidirectional_collaborative_filtering_amd import _lib
+    from omnidirectional_collaborative_filtering_amd import parallel as P
+    world, rank = 2, 1
+    log = []
+
+    class Work:
+        def __init__(self, tag):
+            self.tag = tag
+
+        def wait(self):
+            log.append(("wait",) + self.tag)
+
+    def name_of(t):
+        for k, v in tensors.items():
+            if t.data_ptr() == v.data_ptr() and t.numel() == v.numel():
+                return k
+        return None
+
+    def reduce_scatter_tensor(out, inp, op=None, group=None, async_op=False):
+        assert async_op, "the RCCL branch must be asynchronous"
+        n = out.numel()
+        out.copy_((inp[rank * n:(rank + 1) * n].float() * world).to(out.dtype))
+        log.append(("rs", name_of(inp)))
+        return Work(("rs", name_of(inp)))
+
+    def all_gather_into_tensor(out, inp, group=None, async_op=False):
+        assert async_op
+        assert inp.data_ptr() == out.data_ptr() + rank * inp.numel() * inp.element_size(), "in place: flat[lo:hi]"
+        assert inp.numel() * world == out.numel()
+        log.append(("ag", name_of(out)))
+        return Work(("ag", name_of(out)))
+
+    monkeypatch.setattr(P.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(P.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(P.dist, "broadcast", lambda t, src, group=None: None)
+    monkeypatch.setattr(P.dist, "reduce_scatter_tensor", reduce_scatter_tensor)
+    monkeypatch.setattr(P.dist, "all_gather_into_tensor", all_gather_into_tensor)
+    monkeypatch.setattr(P.torch.cuda, "current_stream", lambda: types.SimpleNamespace(cuda_stream=0))
+
+    def fake_call(name, *args):
+        assert name == "ocf_opt_step_ex", name
+        a = args[0]
+        log.append(("update", a.p, a.g, a.shadow, a.n))
+        return 0
+    monkeypatch.setattr(_lib, "call", fake_call)
+
+    dims = [(256, 128), (128, 256)]          # W0 [in][out], W1 stored transposed [N][H]
+
+    class Opt:
+        iterations = 0
+
+        def step_params(self, scale, l2):
+            return _lib.OcfOptParams(1, 0.005, 1e-8, 0, 0, l2, scale)
+
+    class FakeEngine:
+        def __init__(self):
+            self.W = [torch.zeros(*d) for d in dims]
+            self.b = [torch.zeros(128), torch.zeros(256)]
+            self.Wsh = [torch.zeros(*d, dtype=torch.float16) for d in dims]
+            self.l2, self.shadow_blocked, self.dev, self.cdt = 0.0, False, torch.device("cpu"), _lib.DT_F16
+            self.slots = [([torch.zeros_like(w), None], [torch.zeros_like(b), None]) for w, b in zip(self.W, self.b)]
+            self.opt, self.trainable, self.grad_hook, self.master_sync = Opt(), [True, True], None, None
+
+        def _refresh_shadows(self):
+            log.append(("refresh_all",))
+
+        def _refresh_shadow(self, i):
+            log.append(("refresh", i))
+
+        def train_step(self, grads_out):
+            for i in (1, 0):                  # output layer first, as Engine._backward_gather
+                grads_out[2 * i].fill_(1.0)
+                grads_out[2 * i + 1].fill_(1.0)
+                log.append(("grad", i))
+                if self.grad_hook:
+                    self.grad_hook(i)
+
+    e = FakeEngine()
+    dp = P.DataParallel(e, rank, world, mode="sharded", grad_dtype="bfloat16")
+    assert dp.zero_layers == {0, 1} and e.master_sync is not None
+    tensors = {"W0": e.W[0], "b0": e.b[0], "W1": e.W[1], "b1": e.b[1], "sh0": e.Wsh[0], "sh1": e.Wsh[1],
+               "gW0": dp.views[0], "gb0": dp.views[1], "gW1": dp.views[2], "gb1": dp.views[3]}
+    log.clear()
+    dp.step()
+    ev = [x[:2] for x in log]
+    for i in (0, 1):
+        assert ev.index(("grad", i)) < ev.index(("rs", "gW%d" % i)) and ev.index(("grad", i)) < ev.index(("rs", "gb%d" % i))
+    ups = [k for k, x in enumerate(log) if x[0] == "update"]
+    rs_waits = [k for k, x in enumerate(log) if x[:2] == ("wait", "rs")]
+    assert len(ups) == 4 and len(rs_waits) == 4
+    for u, w in zip(ups, rs_waits):
+        assert w < u, "update before its reduce-scatter completed"
+    # ZeRO-1: the weights' updates carry their shadow shard; the biases' do not
+    lo = rank * e.W[0].numel() // world
+    w_up = [x for x in log if x[0] == "update" and x[3]]
+    assert sorted(x[3] for x in w_up) == sorted(e.Wsh[i].view(-1)[lo:].data_ptr() for i in (0, 1))
+    gathered = [x[1] for x in log if x[0] == "ag"]
+    assert sorted(gathered) == ["b0", "b1", "sh0", "sh1"], gathered
+    for g in gathered:                                    # each gather after its update, waited before the end
+        assert ev.index(("wait", "ag")) > ev.index(("ag", g))
+    assert sum(1 for x in log if x[:2] == ("wait", "ag")) == 4
+    assert ("refresh_all",) not in log, "ZeRO-1: no full shadow refresh"
+    assert dp._masters_stale
+
+
+def test_sharded_falls_back_when_shards_do_not_divide(monkeypatch):
+    from omnidirectional_collaborative_filtering_amd import parallel as P
+    monkeypatch.setattr(P.dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(P.dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(P.dist, "broadcast", lambda t, src, group=None: None)
+    e = types.SimpleNamespace(W=[torch.zeros(256, 128)], b=[torch.zeros(128)], Wsh=[None], l2=0.0,
+                              shadow_blocked=False, dev=torch.device("cpu"), _refresh_shadows=lambda: None)
+    with pytest.warns(UserWarning, match="allreduce"):
+        dp = P.DataParallel(e, 0, 3, mode="sharded")
+    assert dp.mode == "allreduce" and dp.sync is None

@@ -26,9 +26,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, mode, gdt, causal):
+def _worker(rank, world, port, q, mode, gdt, causal, cd):
     try:
-        _work(rank, world, port, q, mode, gdt, causal)
+        _work(rank, world, port, q, mode, gdt, causal, cd)
     except BaseException:                  # surface the failure in the parent instead of a hang
         import traceback
         q.put(("error", rank, traceback.format_exc()))
@@ -45,7 +45,7 @@ def _log(rank, msg):
             f.write(msg + "\n")
 
 
-def _work(rank, world, port, q, mode, gdt, causal):
+def _work(rank, world, port, q, mode, gdt, causal, cd):
     _log(rank, "start %s %s %s" % (mode, gdt, causal))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
@@ -62,7 +62,7 @@ def _work(rank, world, port, q, mode, gdt, causal):
     rd = data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split")
     # different seeds per rank: the broadcast must make rank 0's weights everyone's
     om = omni_model(1, H, data.num_cols, B, dense_activation="sigmoid", use_causal_info=causal,
-                    dropout_probability=0.2, compute_dtype="float32", seed=11 + rank)
+                    dropout_probability=0.2, compute_dtype=cd, seed=11 + rank)
     m = om.model
     m.compile(Adagrad(lr=0.005, epsilon=1e-8), "mean_squared_error")
     _log(rank, "model built")
@@ -77,16 +77,20 @@ def _work(rank, world, port, q, mode, gdt, causal):
         h = m.fit_generator(gen, world, epochs=1, verbose=0)
         losses.append(h.history["loss"][0])
         masks.append(om.engine.mask[0][:B, :H].cpu().numpy().astype(np.float64))
-    q.put((rank, w0, m.get_weights(), masks, losses, gen.rows_host[: STEPS * world]))
+    w = m.get_weights()                    # (ZeRO-1: gathers the fp32 masters first, on every rank)
+    e = om.engine
+    sh = [(t.cpu().numpy(), e.W[i].to(t.dtype).cpu().numpy()) for i, t in enumerate(e.Wsh) if t is not None]
+    zero = sorted(m.dp.zero_layers) if m.dp is not None else []
+    q.put((rank, w0, w, masks, losses, gen.rows_host[: STEPS * world], sh, zero))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(mode, gdt, causal):
+def _run(mode, gdt, causal, cd="float32"):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, mode, gdt, causal)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q, mode, gdt, causal, cd)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = []
@@ -104,7 +108,7 @@ def _run(mode, gdt, causal):
     return res
 
 
-def _oracle(res, causal, u=None):
+def _oracle(res, causal, u=None, all_params=False):
     from oracle.model_oracle import AdagradOracle, OmniOracle
     data = dataset()
     N = data.num_cols
@@ -131,7 +135,7 @@ def _oracle(res, causal, u=None):
                 env = [np.zeros_like(g) for g in grads]
                 rmax = [np.zeros_like(g) for g in grads]
             for j, (g, G) in enumerate(zip(grads, [z for pair in zip(GW, Gb) for z in pair])):
-                if j % 2 == 0:              # weight gradients travel in bf16; biases stay fp32
+                if j % 2 == 0 or all_params:   # bf16 gradients: weights only (biases stay fp32)
                     rmax[j] = np.maximum(rmax[j], CHAIN_ROUNDINGS * u * G / np.maximum(np.abs(g), 1e-30))
                 env[j] += opt.lr * np.minimum(2.0, 3.0 * rmax[j])
         losses.append(loss)
@@ -163,6 +167,29 @@ def test_dp_bf16_gradients(gpu):
     losses, want, env = _oracle(res, False, u=2.0 ** -8)
     for lg, lo in zip(res[0][4], losses):
         assert abs(lg - lo) <= 1e-3 * lo, (lg, lo)
+    for j, (g, o, e) in enumerate(zip(res[0][2], want, env)):
+        err = np.abs(g - o)
+        assert (err <= FP32_ABS + e).all(), (j, float(err.max()), int((err > FP32_ABS + e).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gdt", ["float32", "bfloat16"])
+def test_dp_f16_zero1_shadows(gpu, gdt):
+    """f16 compute, sharded mode with ZeRO-1 (the first / last layers' fp32 masters and slots stay sharded;
+    ocf_opt_step_ex writes the f16 shadow shard and only the shadows are all-gathered): the replicas' shadows
+    are bit-identical, every shadow element is the RNE f16 rounding of its gathered fp32 master (what the
+    per-step refresh produced), and the weights stay inside the oracle's f16 envelope"""
+    res = _run("sharded", gdt, False, cd="float16")
+    assert res[0][7] == [0, 1] and res[1][7] == [0, 1], "ZeRO-1 layers"
+    for (sa, ma), (sb, mb) in zip(res[0][6], res[1][6]):
+        np.testing.assert_array_equal(sa, sb)             # replicas' shadows identical
+        np.testing.assert_array_equal(sa, ma)             # shadow == rounded master (rank 0)
+        np.testing.assert_array_equal(sb, mb)
+    for a, b in zip(res[0][2], res[1][2]):
+        np.testing.assert_array_equal(a, b)
+    losses, want, env = _oracle(res, False, u=2.0 ** -8 if gdt == "bfloat16" else 2.0 ** -11, all_params=True)
+    for lg, lo in zip(res[0][4], losses):
+        assert abs(lg - lo) <= 2e-3 * lo, (lg, lo)
     for j, (g, o, e) in enumerate(zip(res[0][2], want, env)):
         err = np.abs(g - o)
         assert (err <= FP32_ABS + e).all(), (j, float(err.max()), int((err > FP32_ABS + e).sum()))
