@@ -43,6 +43,20 @@ DEFAULTS = dict(
 )
 
 
+def shard_donor_weights(weights, c0, c1, n_total, k=1):
+    """Keras-order weights [W0, b0, ..., W_L, b_L] of a full model -> the feature-parallel shard owning
+    columns [c0, c1): W0's rows of those columns in each of the k input blocks, W_L's and b_L's columns;
+    the hidden layers whole"""
+    w = list(weights)
+    rows = np.concatenate([np.arange(b * n_total + c0, b * n_total + c1) for b in range(k)])
+    if w[0].shape[0] != k * n_total or w[-2].shape[1] != n_total:
+        raise ValueError("donor shapes %s / %s do not match a %d-column model" % (w[0].shape, w[-2].shape, n_total))
+    w[0] = w[0][rows]
+    w[-2] = w[-2][:, c0:c1]
+    w[-1] = w[-1][c0:c1]
+    return w
+
+
 class EarlyStopper(object):
     """The reference's early-stopping bookkeeping (train.py:147-177), separated from the training loop:
     the first epoch only sets the baseline and never saves (:164-165); an improvement saves and
@@ -155,7 +169,15 @@ def run(cfg):
         from .model import load_donor
         if rank == 0:
             print("Loading weights from ", cfg["load_weights_from"])
-        donor = load_donor(m.shard_path(os.path.join(cfg["model_save_path"], cfg["load_weights_from"])))
+        full = os.path.join(cfg["model_save_path"], cfg["load_weights_from"])
+        if fp and not os.path.exists(m.shard_path(full)):
+            # a donor saved by an ordinary single-device run (the reference's case): this rank's columns of
+            # the first and last layers
+            donor = load_donor(full)
+            donor.weights = shard_donor_weights(donor.weights, shard[0], shard[1], shard[2],
+                                                1 + int(cfg["use_causal_info"]) + int(cfg["auxilliary_mask_type"] == "both"))
+        else:
+            donor = load_donor(m.shard_path(full))
         if cfg["perform_finetuning"]:
             if rank == 0:
                 print("Fine tuning")

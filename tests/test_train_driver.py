@@ -57,3 +57,20 @@ def test_seed_agreement_single_process():
     assert _agree_on_seed(17, 1) == 17
     s = _agree_on_seed(None, 1)
     assert isinstance(s, int) and 0 <= s < 2 ** 31
+
+
+def test_shard_donor_weights_slices_like_the_engine():
+    """a single-device donor (the reference's load_weights_from case) sliced for feature-parallel rank
+    columns [c0, c1): the same rows / columns Engine.init_weights gives a column shard"""
+    import numpy as np
+    from omnidirectional_collaborative_filtering_amd.train import shard_donor_weights
+    rng = np.random.RandomState(0)
+    NT, H, k, c0, c1 = 300, 7, 2, 128, 256
+    w = [rng.rand(k * NT, H), rng.rand(H), rng.rand(H, H), rng.rand(H), rng.rand(H, NT), rng.rand(NT)]
+    s = shard_donor_weights(w, c0, c1, NT, k)
+    rows = np.concatenate([np.arange(b * NT + c0, b * NT + c1) for b in range(k)])
+    np.testing.assert_array_equal(s[0], w[0][rows])
+    np.testing.assert_array_equal(s[1], w[1])
+    np.testing.assert_array_equal(s[2], w[2])
+    np.testing.assert_array_equal(s[4], w[4][:, c0:c1])
+    np.testing.assert_array_equal(s[5], w[5][c0:c1])
