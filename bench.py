@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--rows-long", type=int, default=-1,
                     help="row-stream dW kernel's LONG variant (entries as vectors): -1 library's choice (>= 4 "
                          "entries per weight row), 0 never, 1 always")
+    ap.add_argument("--rows-small-waves", type=int, default=-1,
+                    help="row-stream dW kernel: 32 workgroups per 128-row tile when 12 would give fewer waves than "
+                         "this (-1: library default)")
     ap.add_argument("--fold-jobs", type=int, default=1,
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
@@ -291,6 +294,8 @@ def main():
         _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)
     if args.rows_long >= 0:
         _lib.call("ocf_set_tuning", b"rows_long", int(args.rows_long), None)
+    if args.rows_small_waves >= 0:
+        _lib.call("ocf_set_tuning", b"rows_small_waves", int(args.rows_small_waves), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)

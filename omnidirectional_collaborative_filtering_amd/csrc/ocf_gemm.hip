@@ -53,6 +53,7 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
 int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (ocf_set_tuning "optim_rows")
 int g_optim_ws = -1;
 int g_rows_long = -1;   // row-stream LONG variant: -1 by entries per row, 0 never, 1 always ("rows_long")
+int g_rows_small_waves = 8192;   // row-stream kernel: 32 parts per tile below this many waves at 12 ("rows_small_waves")
 int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
 bool optim_ws_on() {
   if (g_optim_ws < 0) {
@@ -126,8 +127,13 @@ bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s
     // workgroups per 128-row tile (each a twelfth of the tile's live rows): with the 75-VGPR pipeline
     // (6 waves per SIMD) 12 parts measured best, ML-20M step 0.4243-0.4269 ms against 6 / 8 / 16 / 24 / 32
     // parts 0.439-0.441 / 0.4332-0.4364 / 0.437 / 0.430 / 0.446
-    constexpr int PARTS = 12;
-    const int grid = std::max(g.M / 128 * PARTS, (jb.count() + 3) / 4);
+    // A weight of few rows (ML-1M: 48 tiles; ML-100K: 8; an 8-way feature rank's 136) leaves the chip
+    // mostly idle at 12 parts, each wave walking ~3 rows through the 5-stage pipeline's fill: there a wave
+    // takes ~one row (32 parts).  Measured (ms/step, 12 -> 32 parts): ML-1M bf16 0.1225 -> 0.1064, ML-100K
+    // fp32 0.0875 -> 0.0794, 8-way emulated rank step 0.2308 -> 0.2178 (ML-20M, 1,082 tiles: 12 parts)
+    const bool small = g.M / 128 * 12 * 4 < g_rows_small_waves;
+    const int parts = small ? 32 : 12;
+    const int grid = std::max(g.M / 128 * parts, (jb.count() + 3) / 4);
     // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
     // many entries per weight row (>= 4 on average): the LONG variant (entries as a vector, B rows of a
     // group of entries in flight together)
@@ -135,12 +141,14 @@ bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s
     auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
       constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
       constexpr int NCH = decltype(nch_tag)::value;
-      if (lng)
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, true>), dim3(grid), dim3(RS_THREADS), 0, s,
-                           ra, jb);
+      if (lng && small)
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 32, true>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
+      else if (lng)
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 12, true>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
+      else if (small)
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 32, false>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
       else
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, false>), dim3(grid), dim3(RS_THREADS), 0, s,
-                           ra, jb);
+        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 12, false>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
     };
     using std::integral_constant;
     auto by_n = [&](auto k) {
@@ -347,6 +355,9 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   } else if (k == "rows_long") {
     if (previous) *previous = g_rows_long;
     g_rows_long = value < 0 ? -1 : (value ? 1 : 0);
+  } else if (k == "rows_small_waves") {
+    if (previous) *previous = g_rows_small_waves;
+    g_rows_small_waves = value;
   } else if (k == "optim_ws") {
     if (previous) *previous = optim_ws_on() ? 1 : 0;
     g_optim_ws = value ? 1 : 0;

@@ -32,7 +32,12 @@ from .engine import TILE, cur_stream, ptr, ru
 from .parallel import shard_batches
 
 AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
-GATHER_CHUNK = int(os.environ.get("OCF_GATHER_CHUNK", 256))   # entries per row-gather work unit (ocf_gather_*)
+# entries per row-gather work unit (ocf_gather_*): a group of 32 lanes walks its chunk's entries 4 at a time,
+# so a chunk's latency grows with its length; batches of fewer entries than GATHER_BIG use short chunks
+# (more workgroups, each a few dependent steps), large batches the long ones (fewer partial sums)
+GATHER_CHUNK = 256
+GATHER_CHUNK_SMALL = 64
+GATHER_BIG = 100_000
 ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the library takes up to 65,535)
 ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
 
@@ -242,11 +247,15 @@ class BatchGenerator(object):
                                    self.tlocal.max() if (self.src2 is not None and nb) else 0))
 
     @staticmethod
-    def _chunk_tables(lens, rows, dev, chunk=GATHER_CHUNK):
-        """Every batch's rows cut into chunks of <= `chunk` entries: (batch row, first, end local entry)
-        per chunk, [nb][B+1] first chunk of each row (relative to the batch), per-batch chunk base."""
+    def _chunk_tables(lens, rows, dev, chunk=None):
+        """Every batch's rows cut into chunks of <= `chunk` entries (of equal length within a row): (batch
+        row, first, end local entry) per chunk, [nb][B+1] first chunk of each row (relative to the batch),
+        per-batch chunk base.  chunk: GATHER_CHUNK, or GATHER_CHUNK_SMALL for batches of few entries."""
         nb, B = rows.shape
         L = lens[rows].astype(np.int64).reshape(-1)                  # [nb*B]
+        if chunk is None:
+            per_batch = L.sum() / max(nb, 1)
+            chunk = GATHER_CHUNK if per_batch >= GATHER_BIG else GATHER_CHUNK_SMALL
         nc = (L + chunk - 1) // chunk
         row_cptr = np.zeros((nb, B + 1), dtype=np.int32)
         np.cumsum(nc.reshape(nb, B), axis=1, out=row_cptr[:, 1:])
@@ -256,8 +265,10 @@ class BatchGenerator(object):
         rep = np.repeat(np.arange(nb * B, dtype=np.int64), nc)
         first = np.repeat(np.cumsum(nc) - nc, nc)
         k = np.arange(tot, dtype=np.int64) - first
-        j0 = k * chunk
-        j1 = np.minimum(j0 + chunk, L[rep])
+        ncr = nc[rep]
+        Lr = L[rep]
+        j0 = k * Lr // ncr                 # equal-length chunks within a row
+        j1 = (k + 1) * Lr // ncr
         t = lambda x: torch.as_tensor(np.ascontiguousarray(x, dtype=np.int32), device=dev)
         max_chunks = nc.reshape(nb, B).max(axis=1) if nb else np.zeros(0, np.int64)
         return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase,

@@ -1,11 +1,14 @@
-# PARTS 12 (in-tree) against 8 on the other workloads: Netflix width, B = 4,096, an 8-way feature-parallel rank
+#!/bin/bash
+# row-stream dW kernel: 12 vs 32 workgroups per tile on the small weights (ML-1M, ML-100K) and the emulated
+# 8-way rank step -> gpurun_out/parts/
 set -e -o pipefail
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_rows_dw_gpu.py > gpurun_out/parts_tests.log 2>&1 && tail -1 gpurun_out/parts_tests.log
-for a in "nf:--config netflix --steps 15" "b4k:--batch 4096 --steps 10" "fp8:--emulate-shards 8 --steps 30"; do
-  n=${a%%:*}; x=${a#*:}
-  for lib in base p8; do
-    if [ "$lib" = base ]; then unset OCF_LIB_PATH; else export OCF_LIB_PATH=$PWD/omnidirectional_collaborative_filtering_amd/libocf_$lib.so; fi
-    timeout -k 10 300 python bench.py $x --cpu-baseline 0 --rmse 0 --fp32-steps 0 > gpurun_out/parts_${n}_$lib.log 2>&1
-    grep '^{' gpurun_out/parts_${n}_$lib.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$n $lib', d['ms_per_step'])"
-  done
+O=gpurun_out/parts; mkdir -p $O
+B="--cpu-baseline 0 --fp32-steps 0 --epoch 0 --rmse 0"
+for W in 0 100000; do
+  timeout -k 10 200 python bench.py $B --rows-small-waves $W --config ml1m --dtype bfloat16 > $O/ml1m_W$W.json 2>> $O/err.log
+  timeout -k 10 200 python bench.py $B --rows-small-waves $W --config ml100k --dtype float32 > $O/ml100k_W$W.json 2>> $O/err.log
+  timeout -k 10 200 python bench.py $B --rows-small-waves $W --emulate-shards 8 > $O/fp8_W$W.json 2>> $O/err.log
+  echo W=$W done
 done
+timeout -k 10 200 python bench.py $B > $O/ml20m.json 2>> $O/err.log
+for f in $O/*.json; do python -c "import json; d=json.loads(open('$f').read().strip().splitlines()[-1]); print('$f', d['ms_per_step'], d['phases_ms'])"; done
