@@ -233,8 +233,144 @@ def full_epoch(args, m, rd, B):
     return out
 
 
+def jester_arrays(n=73_421, N=100, seed=1):
+    """train_jester.py:34-75 on synthetic data of the Jester shape (the CSV is not in the image): ratings
+    uniform in [-10, 10] (2 decimals) with 99 = missing at Jester's ~56 % density, the observed mask, and
+    the reciprocal 0.5 input / output split drawn once with np.random.choice (:69-74)"""
+    rng = np.random.RandomState(seed)
+    data = np.where(rng.rand(n, N) < 0.56, np.round(rng.uniform(-10, 10, (n, N)), 2), 99.0)
+    observed = (data != 99).astype(np.float64)
+    np.random.seed(seed)
+    drop = np.random.choice([0, 1], size=data.shape, p=[0.5, 0.5])
+    in_m, out_m = drop * observed, (1 - drop) * observed
+    return (data * in_m).astype(np.float32), observed.astype(np.float32), out_m.astype(np.float32), \
+        (data * out_m).astype(np.float32)
+
+
+def jester_main(args):
+    """BASELINE configs[4]: the Jester omnidirectional denoising AE with train_jester.py's parameters --
+    100 jokes, causal concat of the observed mask (input 200), 2 x 256 tanh hidden layers, linear output,
+    RMSprop (Keras defaults), batch 128, Model.fit on dense arrays with validation_split 0.1 (:44-79).  A step
+    is one Model.fit batch (the dense MFMA path: split-K encoder, hidden-layer GEMM, masked-MSE decoder,
+    backward GEMMs with fused RMSprop); ratings/s counts the observed ratings of the batches."""
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rank, world, local = 0, 1, 0
+    if args.gpus != 1:
+        raise SystemExit("--config jester: one GPU per process (replicas only; see DESIGN.md)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    t0 = time.time()
+    inputs, observed, out_m, targets = jester_arrays()
+    n, N = inputs.shape
+    B, H = 128, 256
+    om = omni_model(2, H, N, B, dense_activation="tanh", use_causal_info=True, compute_dtype=args.dtype, seed=3,
+                    rating_range=20, device=dev)
+    m = om.model
+    m.compile("rmsprop", "mean_squared_error", metrics=["mae", "accurate_MAE", "nMAE"])
+    w0 = m.get_weights()
+    e = om.engine
+    split_at = int(n * 0.9)
+    np.random.seed(42)
+    idx = np.arange(split_at)
+    np.random.shuffle(idx)                     # Model.fit's shuffle of the training part
+    x = [inputs, observed, out_m]
+    n_batches = split_at // B
+    obs_per = [int(observed[idx[s * B:(s + 1) * B]].sum()) for s in range(n_batches)]
+    setup_s = time.time() - t0
+
+    # Model.fit's data path: the arrays resident on the device, each batch gathered by row index
+    xd = [torch.as_tensor(a).to(dev) for a in x]
+    yd = torch.as_tensor(targets).to(dev)
+    idx_d = torch.as_tensor(idx, dtype=torch.int64).to(dev)
+
+    def step(i):
+        s = i % n_batches
+        m._load_rows(xd, yd, idx_d[s * B:(s + 1) * B])
+        e.train_step()
+        return obs_per[s]
+
+    e.enable_timers(bool(args.phase_timers))
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    phases = e.phase_times_ms(skip=1 if args.warmup > 1 else 0)
+    e.enable_timers(False)
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    nnz = 0
+    for i in range(args.steps):
+        nnz += step(args.warmup + i)
+    t_issued = time.perf_counter()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    e.take_stats()
+    ms = elapsed / args.steps * 1e3
+    # algorithmic work per step (SURVEY 8(d)): dims 200 -> 256 -> 256 -> 100, no input gradient
+    dims = [2 * N, H, H, N]
+    P = sum(a * b + b for a, b in zip(dims[:-1], dims[1:]))
+    flops = sum(6.0 * B * a * b for a, b in zip(dims[:-1], dims[1:])) - 2.0 * B * dims[0] * dims[1]
+    w_b = 4 if args.dtype == "float32" else 2
+    step_bytes = P * (16 + 4) + w_b * (sum(a * b for a, b in zip(dims[:-1], dims[1:])) * 2) + 5 * B * N * 4
+    cand = {k: v for k, v in phases.items() if k in ("dW_in", "dW_out", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
+    dom = max(cand, key=lambda k: cand[k]["mean_ms"]) if cand else None
+    line = {
+        "metric": METRIC, "value": round(nnz / elapsed, 1), "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": {"float16": "f16", "bfloat16": "bf16", "float32": "f32"}[args.dtype],
+        "data": "synthetic Jester-shaped dense matrix (73,421 users x 100 jokes, ~56 % observed, ratings in "
+                "[-10, 10], 99 = missing, reciprocal 0.5 split drawn once); random-init weights",
+        "config": {"workload": "Jester omnidirectional denoising AE train step, Model.fit (BASELINE configs[4], "
+                               "train_jester.py:44-79)", "rows": n, "N": N, "hidden": [H, H], "input": 2 * N,
+                   "batch_per_gpu": B, "global_batch": B, "optimizer": "rmsprop", "activation": "tanh",
+                   "compute": args.dtype + " MFMA, fp32 accumulate", "parallelism": "dp1"},
+        "roofline": None,
+        "step_roofline": {"alg_bytes": int(step_bytes), "alg_flops": int(flops),
+                          "hbm_bound_ms": round(step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 5),
+                          "mfma_bound_ms": round(flops / (MFMA_F16_PEAK_TFS * 1e12) * 1e3, 5),
+                          "frac_of_binding_roof": round(max(step_bytes / (HBM_PEAK_GBS * 1e9),
+                                                            flops / (MFMA_F16_PEAK_TFS * 1e12)) / (ms * 1e-3), 4)},
+        "phases_ms": {k: round(v["mean_ms"], 4) for k, v in phases.items()},
+        "phases_from": "warm-up steps 2..%d, every phase bracketed by HIP events" % args.warmup,
+        "host_issue_ms_per_step": round((t_issued - t_start) / args.steps * 1e3, 4),
+        "setup_s": round(setup_s, 1),
+    }
+    if dom is not None:
+        # the dominant launch against its own algorithmic bytes (tiny model: latency-bound, reported as is)
+        Pd = {"dW_in": dims[0] * dims[1], "dW_out": dims[2] * dims[3], "enc_gemm": dims[0] * dims[1],
+              "dec_gemm_mse": dims[2] * dims[3], "dec_bwd_gemm": dims[2] * dims[3]}[dom]
+        alg = Pd * (16 if dom.startswith("dW") else w_b) + 2 * B * max(dims) * w_b
+        kms = cand[dom]["mean_ms"]
+        line["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "traffic": None,
+                            "kernel": dom, "kernel_mean_us": round(kms * 1e3, 2), "alg_bytes_per_launch": int(alg),
+                            "note": "a 0.14 M-parameter model: every launch is latency-bound; the fraction is "
+                                    "reported, not a target"}
+    if args.cpu_baseline:
+        from threadpoolctl import threadpool_info
+        from oracle.model_oracle import OmniOracle, RMSpropOracle
+        ora = OmniOracle(dims, activation="tanh", dtype=np.float32).set_params(w0[0::2], w0[1::2])
+        opt = RMSpropOracle(lr=0.001)
+        ks = max(args.cpu_steps, 20)
+        t1 = time.perf_counter()
+        nn = 0
+        for s in range(ks):
+            sel = idx[s * B:(s + 1) * B]
+            xin = np.concatenate([inputs[sel], observed[sel]], 1)
+            _, _, gW, gb = ora.loss_and_grads(xin, out_m[sel], targets[sel])
+            ora.set_flat(opt.step(ora.params(), [g for pair in zip(gW, gb) for g in pair]))
+            nn += obs_per[s]
+        dt = time.perf_counter() - t1
+        threads = max([d.get("num_threads", 1) for d in threadpool_info()] + [1])
+        line["cpu_baseline"] = {"value": round(nn / dt, 1), "unit": "ratings/s", "cores": int(threads), "kind": "port",
+                                "sample": "%d Model.fit steps of the same workload: NumPy fp32 dense model step "
+                                          "(RMSprop) on %d BLAS threads, %.2f ms/step" % (ks, threads, dt / ks * 1e3)}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "jester":
+        return jester_main(args)
     from omnidirectional_collaborative_filtering_amd.parallel import (DataParallel, feature_shard_range,
                                                                       init_from_env, make_comm, shard_batches)
     rank, world, local = init_from_env()

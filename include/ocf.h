@@ -182,14 +182,17 @@ int ocf_rows_reduce(const OcfRowsReduceArgs* args, void* stream);
 /* out[n] = gscale * sum_{b < B} d[b][n] for a dense [*][ld] array in dtype (output-bias gradient) */
 int ocf_colsum(const void* d, int dtype, int64_t ld, int B, int N, float gscale, float* out, void* stream);
 
-/* Target buckets from dense target / output-mask arrays (Model.train_on_batch on user arrays). */
+/* Target buckets from dense target / output-mask arrays (Model.train_on_batch / fit on user arrays):
+ * an entry wherever T != 0 or M != 0, bucketed per 128-column tile in (row, column) order
+ * (deterministic).  rows (nullable): batch row b is row rows[b] of T / M (a device-resident dataset). */
 int ocf_dense_targets(const float* T, const float* M, int64_t ld, int B, int N, int n_tiles, int* tile_cnt,
-                      int* bk_ptr, int* bk_cur, int32_t* bk_rc, float* bk_t, float* bk_m, void* stream);
+                      int* bk_ptr, int* bk_cur, int32_t* bk_rc, float* bk_t, float* bk_m, const int64_t* rows,
+                      void* stream);
 
-/* Pack up to three dense fp32 [B][ld_src] inputs into the compute-dtype concatenated layer-0
- * input (model.py:47-56 concatenate). */
+/* Pack up to three dense fp32 [*][ld_src] inputs into the compute-dtype concatenated layer-0
+ * input (model.py:47-56 concatenate); rows (nullable) as for ocf_dense_targets. */
 int ocf_pack_input(const float* s0, const float* s1, const float* s2, int64_t ld_src, int B, int N, void* xin,
-                   int dtype, int64_t xin_ld, int64_t xin_block, int B_pad, void* stream);
+                   int dtype, int64_t xin_ld, int64_t xin_block, int B_pad, const int64_t* rows, void* stream);
 
 /*
  * ocf_gemm -- one MFMA GEMM  C[M,N] = A[M,K] * B[K,N]  with a fused epilogue.  Replaces the TF
@@ -280,6 +283,10 @@ typedef struct OcfGemmArgs {
    * average: feature-parallel global batches, dense datasets like ML-1M) the row-stream kernel loads each
    * row's entries as one vector (a lane per entry) and the B rows of a group of entries in one go. */
   int64_t sp_nent;
+  /* MASKED_MSE dense target mode (nullable dn_t): targets / output masks as dense fp32 arrays, batch row b
+   * at row dn_rows[b] (nullable: b) of [*][ld_dn], columns < n_real; an entry wherever t != 0 or m != 0.
+   * Replaces the bucket pass of ocf_dense_targets for dense batches (Model.fit / train_on_batch). */
+  const float* dn_t; const float* dn_m; int64_t ld_dn; const int64_t* dn_rows;
 } OcfGemmArgs;
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);

@@ -115,6 +115,7 @@ class OcfGemmArgs(ctypes.Structure):
         ("jb_op", OcfOptParams),
         ("js_sp", P), ("js_rs", P), ("js_out", P), ("js_nparts", I32), ("js_ntiles", I32), ("js_M", I32),
         ("row_live", P), ("sp_rowptr", P), ("sp_rowent", P), ("jr", P), ("sp_nent", I64),
+        ("dn_t", P), ("dn_m", P), ("ld_dn", I64), ("dn_rows", P),
     ]
 
 
@@ -144,8 +145,8 @@ class OcfRecipKeepArgs(ctypes.Structure):
 # every symbol include/ocf.h declares, with its ctypes signature
 SIGNATURES = {
     "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
-    "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P]),
-    "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P]),
+    "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P, P]),
+    "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),

@@ -382,6 +382,13 @@ struct EpiMaskedMSE {
     const int64_t* t_lboff;
     int t_ntiles;
     float t_aux;
+    // dense target mode (dn_t != nullptr): targets / output masks as dense fp32 arrays, batch row b at row
+    // dn_rows[b] (or b) of [*][ld_dn]; an entry wherever t != 0 or m != 0 (Model.fit / train_on_batch)
+    const float* dn_t;
+    const float* dn_m;
+    int64_t ld_dn;
+    const int64_t* dn_rows;
+    int n_real;
     void* d_out;              // dense delta [M][ld_d] compute dtype (nullable: eval)
     int d_dtype;
     int64_t ld_d;
@@ -408,6 +415,7 @@ struct EpiMaskedMSE {
     q.s_lo = q.s_hi = q.lb = 0;
 #pragma unroll
     for (int k = 0; k < NPRE; ++k) { q.rc[k] = -1; q.t[k] = 0.f; q.m[k] = 0.f; }
+    if (p.dn_t) return q;
     if (p.bk_ptr) {
       q.b0 = p.bk_ptr[tile_n];
       q.b1 = p.bk_ptr[tile_n + 1];
@@ -476,7 +484,46 @@ struct EpiMaskedMSE {
     __syncthreads();
     // 2. this tile's target entries
     float sse = 0.f, sae = 0.f, cnt = 0.f;
-    if (p.bk_ptr) {
+    if (p.dn_t) {
+      // dense targets: thread tid owns row tid % 128 of the tile and its half (tid / 128) of the columns, so
+      // its row-SSE share, the row's mask bits and every sum are its own (no atomics but the final
+      // two-addend row SSE, order-independent); 16 T / M loads in flight at a time
+      const int ml = c.tid & (GT_BM - 1), c0 = (c.tid >> 7) * (GT_BN / 2);
+      const int b = c.m0 + ml;
+      float rs = 0.f;
+      uint32_t w0 = 0u, w1 = 0u;
+      if (b < p.m_real) {
+        const int64_t ro = (p.dn_rows ? p.dn_rows[b] : (int64_t)b) * p.ld_dn + c.n0 + c0;
+        const int nmax = p.n_real - (c.n0 + c0);
+        constexpr int U = 16;
+        for (int j0 = 0; j0 < GT_BN / 2; j0 += U) {
+          float t[U], m[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const bool ok = j0 + u < nmax;
+            t[u] = ok ? p.dn_t[ro + j0 + u] : 0.f;
+            m[u] = ok ? p.dn_m[ro + j0 + u] : 0.f;
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (t[u] == 0.f && m[u] == 0.f) continue;
+            const int nl = c0 + j0 + u;
+            const float yhat = m[u] * Y[ml * YS + nl];
+            const float err = yhat - t[u];
+            Y[ml * YS + nl] = err * m[u];
+            if (j0 + u < 32) w0 |= 1u << (j0 + u);
+            else w1 |= 1u << (j0 + u - 32);
+            rs += err * err;
+            sae += fabsf(err);
+            cnt += (t[u] + yhat != 0.f) ? 1.f : 0.f;
+          }
+        }
+      }
+      bits[ml * 4 + (c0 >> 5)] = w0;
+      bits[ml * 4 + (c0 >> 5) + 1] = w1;
+      sse = rs;
+      atomicAdd(&rsse[ml], rs);   // exactly two addends onto 0: order-independent
+    } else if (p.bk_ptr) {
 #pragma unroll
       for (int k = 0; k < NPRE; ++k) entry(Y, bits, rsse, c.m0, q.rc[k], q.t[k], q.m[k], sse, sae, cnt);
       for (int e = q.b0 + c.tid + NPRE * GT_THREADS; e < q.b1; e += GT_THREADS)

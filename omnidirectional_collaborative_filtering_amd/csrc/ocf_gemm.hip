@@ -246,10 +246,13 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
         p.t_rows = g.t_rows; p.t_rp = g.t_rp; p.t_tptr = g.t_tptr; p.t_col = g.t_col; p.t_val = g.t_val;
         p.t_lidx = g.t_lidx; p.t_flag = g.t_flag; p.t_lboff = g.t_lboff; p.t_ntiles = g.t_ntiles; p.t_aux = g.t_aux;
         p.m_real = g.m_real;
+        p.dn_t = g.dn_t; p.dn_m = g.dn_m; p.ld_dn = g.ld_dn; p.dn_rows = g.dn_rows; p.n_real = g.n_real;
+        OCF_CHECK(!g.dn_t || (g.dn_m && g.ld_dn >= g.n_real && g.n_real <= g.N),
+                  "ocf_gemm MASKED_MSE: dense targets need dn_m, ld_dn >= n_real, n_real <= N");
         OCF_CHECK(g.stats_part, "ocf_gemm MASKED_MSE: stats_part required");
         OCF_CHECK(!g.db_part || g.h_out, "ocf_gemm MASKED_MSE: db_part needs the delta output (h_out)");
         OCF_CHECK((int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31), "ocf_gemm MASKED_MSE: delta block over 2 GiB");
-        OCF_CHECK(g.bk_ptr || (g.t_rows && g.t_rp && g.t_tptr && g.t_col && g.t_val && g.t_lidx && g.t_flag &&
+        OCF_CHECK(g.dn_t || g.bk_ptr || (g.t_rows && g.t_rp && g.t_tptr && g.t_col && g.t_val && g.t_lidx && g.t_flag &&
                                g.t_lboff && g.t_ntiles * GT_BN >= g.N),
                   "ocf_gemm MASKED_MSE: bucket or row-segment targets required");
         launch<CT, ACOL, BCOL, WGT, EpiMaskedMSE>(g, p, s);

@@ -233,7 +233,15 @@ class Engine:
         self.db_h = [torch.zeros(Bp // 4, h, device=d, dtype=torch.float32) for h in self.Hp]
         self.splits0 = self._pick_splits(self.pad_dims[0], self.Hp[0])
         self.splitsL = self._pick_splits(self.Np, self.Hp[-1])
-        smax = max(self.splits0 * self.Hp[0], self.splitsL * self.Hp[-1])
+        # hidden -> hidden layers (forward: h[i-1] W[i]; backward: dh[i] W[i]^T): a batch of 128 rows and
+        # 256 hidden units is 2 output tiles, i.e. 2 workgroups for the whole GEMM (Jester: 74 / 47 us
+        # in fp32).  With few tiles the K-loop is split into one K-step per workgroup (EPI_SLAB) and the
+        # layer epilogue runs in the split-K reduction (ocf_splitk_bias_act / ocf_splitk_grad_act)
+        self.splits_fwd = [1] + [self._pick_splits_hidden(self.Hp[i - 1], self.Hp[i]) for i in range(1, len(self.H))]
+        self.splits_bwd = [1] + [self._pick_splits_hidden(self.Hp[i], self.Hp[i - 1]) for i in range(1, len(self.H))]
+        smax = max([self.splits0 * self.Hp[0], self.splitsL * self.Hp[-1]] +
+                   [self.splits_fwd[i] * self.Hp[i] for i in range(1, len(self.H))] +
+                   [self.splits_bwd[i] * self.Hp[i - 1] for i in range(1, len(self.H))])
         self.slabs = torch.zeros(smax * Bp, device=d, dtype=torch.float32)
         self.tile_cnt = torch.zeros(self.n_tiles, device=d, dtype=torch.int32)
         self.bk_ptr = torch.zeros(self.n_tiles + 1, device=d, dtype=torch.int32)
@@ -377,10 +385,26 @@ class Engine:
             out[k] = {"mean_ms": float(np.mean(ts)), "total_ms": float(np.sum(ts)), "n": len(ts)}
         return out
 
+    def _pick_splits_hidden(self, K, N):
+        """split-K factor of a hidden -> hidden GEMM [Bp][K] x [K][N]: 1 (fused epilogue) when it has 16+
+        output tiles, else one K-step per workgroup (up to 64 workgroups)"""
+        bk = 32 if self.cdt == _lib.DT_F32 else 64
+        tiles = (self.Bp // TILE) * (N // TILE)
+        if tiles >= 16:
+            return 1
+        ks = K // bk
+        s = max(1, min(ks, 64 // tiles))
+        while ks % s:
+            s -= 1
+        return s
+
     def _pick_splits(self, K, Hp):
         bk = 32 if self.cdt == _lib.DT_F32 else 64
         ksteps = K // bk
         tiles = (self.Bp // TILE) * (Hp // TILE)
+        if ksteps < 64 and tiles < 16:
+            # a short K-loop over few tiles (Jester's 200-wide input): one or two K-steps per workgroup
+            return self._pick_splits_hidden(K, Hp)
         s = max(1, min(ksteps // 8, max(1, 512 // tiles)))
         return s
 
@@ -562,34 +586,52 @@ class Engine:
         call("ocf_sparse_tiles", a, cur_stream())
         return out
 
-    def load_dense(self, inputs, out_mask, targets):
-        """API path: dense arrays (torch/numpy) in the model.py input order."""
+    def load_dense(self, inputs, out_mask, targets, rows=None):
+        """API path: dense arrays in the model.py input order.  rows (device int64 [B]): the batch is rows
+        `rows` of device-resident fp32 [n][ld] arrays (Model.fit uploads its arrays once), gathered by the
+        packing and target kernels -- no per-step copy and no host synchronisation; otherwise [B, N]
+        host or device arrays are staged into one device buffer first."""
         B, N = self.B, self.N
-        if self.dense_in is None:
-            self.dense_in = torch.zeros(5, self.B, self.Np, device=self.dev, dtype=torch.float32)
-        buf = self.dense_in
-        buf.zero_()
-        srcs = list(inputs) + [out_mask, targets]
-        for i, s in enumerate(srcs):
-            t = torch.as_tensor(np.asarray(s) if not torch.is_tensor(s) else s)
-            if tuple(t.shape) != (B, N):
-                raise ValueError("input %d has shape %s, expected (%d, %d)" % (i, tuple(t.shape), B, N))
-            slot = i if i < len(inputs) else (3 if s is out_mask else 4)
-            buf[slot, :, :N] = t.to(self.dev, torch.float32)
-        p0 = ptr(buf[0])
-        p1 = ptr(buf[1]) if len(inputs) > 1 else None
-        p2 = ptr(buf[2]) if len(inputs) > 2 else None
         s = cur_stream()
-        call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
-             self.Bp, s)
+        if rows is not None:
+            srcs = list(inputs) + [out_mask, targets]
+            ld = srcs[0].stride(0)
+            for t in srcs:
+                if not (torch.is_tensor(t) and t.is_cuda and t.dtype == torch.float32 and t.dim() == 2
+                        and t.shape[1] == N and t.stride(0) == ld and t.stride(1) == 1):
+                    raise ValueError("load_dense(rows=...): device fp32 [n, %d] arrays with one row stride" % N)
+            if rows.numel() != B or rows.dtype != torch.int64 or not rows.is_cuda:
+                raise ValueError("load_dense(rows=...): rows must be %d device int64 indices" % B)
+            p = [ptr(t) for t in inputs] + [None] * (3 - len(inputs))
+            call("ocf_pack_input", p[0], p[1], p[2], ld, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
+                 self.Bp, ptr(rows), s)
+            T, M, rp = targets, out_mask, ptr(rows)
+        else:
+            if self.dense_in is None:
+                self.dense_in = torch.zeros(5, self.B, self.Np, device=self.dev, dtype=torch.float32)
+            buf = self.dense_in
+            buf.zero_()
+            srcs = list(inputs) + [out_mask, targets]
+            for i, src in enumerate(srcs):
+                t = torch.as_tensor(np.asarray(src) if not torch.is_tensor(src) else src)
+                if tuple(t.shape) != (B, N):
+                    raise ValueError("input %d has shape %s, expected (%d, %d)" % (i, tuple(t.shape), B, N))
+                slot = i if i < len(inputs) else (3 if src is out_mask else 4)
+                buf[slot, :, :N] = t.to(self.dev, torch.float32)
+            p0 = ptr(buf[0])
+            p1 = ptr(buf[1]) if len(inputs) > 1 else None
+            p2 = ptr(buf[2]) if len(inputs) > 2 else None
+            call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
+                 self.Bp, None, s)
+            T, M, rp, ld = buf[4], buf[3], None, self.Np
         self._xin_clean = False      # xin written densely
-        self._grow_buckets(B * N)
         self.tb = None
-        self.tseg = None
         self.gt = None                 # dense batch: the GEMM path, never a previous batch's gather tables
         self._enc_fused = None
-        call("ocf_dense_targets", ptr(buf[4]), ptr(buf[3]), self.Np, B, N, self.n_tiles, ptr(self.tile_cnt),
-             ptr(self.bk_ptr), ptr(self.bk_cur), ptr(self.bk_rc), ptr(self.bk_t), ptr(self.bk_m), s)
+        # the masked-MSE epilogue reads the dense targets / output masks directly (no bucket pass); keep
+        # the arrays alive while the step is queued
+        self.tseg = dict(dn_t=ptr(T), dn_m=ptr(M), ld_dn=ld, dn_rows=rp, n_real=N)
+        self._dense_keep = (T, M, rows)
 
     # ---------------------------------------------------------------- GEMM helper
     def _gemm(self, A, a_col, lda, Bm, b_dtype, b_col, ldb, M, N, K, epi, **kw):
@@ -651,6 +693,15 @@ class Engine:
                  keep, self.seed, stream_id, None, ptr(self.mask[0]) if keep < 1 else None, ptr(self.a[0]),
                  ptr(self.h[0]), self.cdt, self.B, self.H[0], s)
         for i in range(1, L):
+            sp = self.splits_fwd[i]
+            if sp > 1:
+                st = Bp * self.Hp[i]
+                self._gemm(self.h[i - 1], 0, self.Hp[i - 1], self.W[i], _lib.DT_F32, 1, self.Hp[i], Bp, self.Hp[i],
+                           self.Hp[i - 1], _lib.EPI_SLAB, splits=sp, out=self.slabs, ld_out=self.Hp[i], split_stride=st)
+                call("ocf_splitk_bias_act", ptr(self.slabs), sp, st, Bp, self.Hp[i], self.Hp[i], ptr(self.b[i]), self.act,
+                     keep, self.seed, stream_id + i, None, ptr(self.mask[i]) if keep < 1 else None, ptr(self.a[i]),
+                     ptr(self.h[i]), self.cdt, self.B, self.H[i], s)
+                continue
             self._gemm(self.h[i - 1], 0, self.Hp[i - 1], self.W[i], _lib.DT_F32, 1, self.Hp[i], Bp, self.Hp[i],
                        self.Hp[i - 1], _lib.EPI_BIAS_ACT, bias=self.b[i], act=self.act, keep=keep, seed=self.seed,
                        stream=stream_id + i, mask_out=self.mask[i] if keep < 1 else None, a_out=self.a[i],
@@ -852,16 +903,12 @@ class Engine:
         parts_last = Bp // 4
         for i in range(L - 1, 0, -1):
             # delta of hidden layer i-1 through W_i (before W_i changes)
-            self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
-                       self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
-                       act=self.act, h_out=self.dh[i - 1], h_dtype=self.cdt, ld_out=self.Hp[i - 1],
-                       db_part=self.db_h[i - 1], opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
-                       m_real=self.B, n_real=self.H[i - 1])
+            parts_next = self._hidden_delta(i, gscale)
             self._bias_update(i, self.db_h[i], parts_last, self.Hp[i], self.Hp[i], grads_out, op)
             self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
                                 self.Hp[i], gscale, grads_out, op)
             self._grad_ready(i, grads_out)
-            parts_last = Bp // TILE
+            parts_last = parts_next
         self._bias_update(0, self.db_h[0], parts_last, self.Hp[0], self.Hp[0], grads_out, op)
         with self.phase("dW_in"):
             self._weight_update(0, self.xin, self.pad_dims[0], self.dh[0], self.Hp[0], self.pad_dims[0],
@@ -990,22 +1037,39 @@ class Engine:
             self._bias_update(L, self.db_out_col, 1, self.Np, self.Np, grads_out, op)
         self._grad_ready(L, grads_out)
         for i in range(L - 1, 0, -1):
-            self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
-                       self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
-                       act=self.act, h_out=self.dh[i - 1], h_dtype=self.cdt, ld_out=self.Hp[i - 1],
-                       db_part=self.db_h[i - 1], opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
-                       m_real=self.B, n_real=self.H[i - 1])
+            parts_next = self._hidden_delta(i, gscale)
             self._bias_update(i, db_last, parts_last, self.Hp[i], self.Hp[i], grads_out, op)
             self._weight_update(i, self.h[i - 1], self.Hp[i - 1], self.dh[i], self.Hp[i], self.Hp[i - 1],
                                 self.Hp[i], gscale, grads_out, op)
             self._grad_ready(i, grads_out)
-            db_last, parts_last = self.db_h[i - 1], Bp // TILE
+            db_last, parts_last = self.db_h[i - 1], parts_next
         self._bias_update(0, db_last, parts_last, self.Hp[0], self.Hp[0], grads_out, op)
         with self.phase("dW_in"):
             self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
         self._grad_ready(0, grads_out)
         if fused:
             self.opt.iterations += 1
+
+    def _hidden_delta(self, i, gscale):
+        """dh[i-1] = (dh[i] W_i^T) * act'(a[i-1]) * dropout, and the hidden bias' gradient partials db_h[i-1];
+        returns how many partial rows db_h[i-1] holds (fused GRAD_ACT epilogue: one per 128-row tile;
+        split-K reduction: one per 4 rows)"""
+        Bp = self.Bp
+        sp = self.splits_bwd[i]
+        if sp > 1:
+            st = Bp * self.Hp[i - 1]
+            self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1], self.Hp[i],
+                       _lib.EPI_SLAB, splits=sp, out=self.slabs, ld_out=self.Hp[i - 1], split_stride=st)
+            call("ocf_splitk_grad_act", ptr(self.slabs), sp, st, Bp, self.Hp[i - 1], self.Hp[i - 1], ptr(self.a[i - 1]),
+                 ptr(self.mask[i - 1]), self.keep, self.act, ptr(self.dh[i - 1]), self.cdt, ptr(self.db_h[i - 1][0]),
+                 gscale, self.B, self.H[i - 1], cur_stream())
+            return Bp // 4
+        self._gemm(self.dh[i], 0, self.Hp[i], self.W[i], _lib.DT_F32, 0, self.Hp[i], Bp, self.Hp[i - 1],
+                   self.Hp[i], _lib.EPI_GRAD_ACT, a_in=self.a[i - 1], mask_in=self.mask[i - 1], keep=self.keep,
+                   act=self.act, h_out=self.dh[i - 1], h_dtype=self.cdt, ld_out=self.Hp[i - 1],
+                   db_part=self.db_h[i - 1], opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale),
+                   m_real=self.B, n_real=self.H[i - 1])
+        return Bp // TILE
 
     def _bias_update(self, i, part, parts, ld, n, grads_out, op):
         if grads_out is None and not self.trainable[i]:

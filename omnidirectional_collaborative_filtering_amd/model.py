@@ -257,25 +257,32 @@ class Model(object):
         bs = int(batch_size or e.B)
         if bs != e.B:
             raise ValueError("batch_size must equal the model batch_size (Dropout noise_shape, model.py:73)")
-        x = [np.asarray(a) if not torch.is_tensor(a) else a for a in x]
-        n = len(x[0])
+        # the arrays go to the device once; every batch is then gathered there by row index (no per-step
+        # host copies, no synchronisation between steps)
+        dev = e.dev
+
+        def on_dev(a):
+            t = a if torch.is_tensor(a) else torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32))
+            return t.to(dev, torch.float32).contiguous()
+        xd = [on_dev(a) for a in x]
+        yd = on_dev(y)
+        n = len(xd[0])
         split_at = int(n * (1.0 - validation_split)) if validation_split else n
         hist = History()
         callbacks = callbacks or []
+        val_rows = torch.arange(split_at, n, dtype=torch.int64, device=dev)
         for epoch in range(epochs):
             idx = np.arange(split_at)
             if shuffle:
                 np.random.shuffle(idx)
+            idx_d = torch.as_tensor(idx, dtype=torch.int64).to(dev)
             for s in range(split_at // bs):
-                sel = idx[s * bs:(s + 1) * bs]
-                self._load(([a[sel] for a in x], y[sel]))
+                self._load_rows(xd, yd, idx_d[s * bs:(s + 1) * bs])
                 e.train_step()
             logs = self._logs_from_stats(e.take_stats())
             if split_at < n and (n - split_at) >= bs:
-                vals = []
                 for s in range((n - split_at) // bs):
-                    sel = np.arange(split_at + s * bs, split_at + (s + 1) * bs)
-                    self._load(([a[sel] for a in x], y[sel]))
+                    self._load_rows(xd, yd, val_rows[s * bs:(s + 1) * bs])
                     e.eval_step()
                 vl = self._logs_from_stats(e.take_stats())
                 for k, v in vl.items():
@@ -289,6 +296,11 @@ class Model(object):
             if self.stop_training:
                 break
         return hist
+
+    def _load_rows(self, xd, yd, rows):
+        """batch = rows `rows` of the device-resident arrays of Model.fit"""
+        blocks, out_mask = self._split_inputs(xd)
+        self.engine.load_dense(blocks, out_mask, yd, rows=rows)
 
     # ------------------------------------------------------------------ weights / checkpoints
     def get_weights(self):

@@ -54,7 +54,7 @@ STRUCTS = {
                                        "t_aux", "p_shadow", "b_nt", "shadow_blocked", "a_sparse",
                                        "sp_lboff", "sp_krows", "sp_colsum", "sp_bptr", "sp_ent", "cb_op", "jb_part",
                                        "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
-                                       "sp_rowent", "jr", "sp_nent"]),
+                                       "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
                                                        "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",
                                                        "row_ptr", "row_ent"]),
