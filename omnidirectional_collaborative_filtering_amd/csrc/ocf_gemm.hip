@@ -80,8 +80,10 @@ WsJobs ws_jobs(const OcfGemmArgs& g) {
   j.js_sp = g.js_sp; j.js_rs = g.js_rs; j.js_out = g.js_out; j.js_nparts = g.js_nparts; j.js_ntiles = g.js_ntiles;
   j.js_M = g.js_M;
   if (g.jr) {
-    OCF_CHECK(g.jr->mode == OCF_REDUCE_GRAD_ACT && g.jr->part && g.jr->row_cptr && g.jr->h_out && g.jr->a_in,
-              "ocf_gemm: the folded row reduction (jr) takes OCF_REDUCE_GRAD_ACT with part, row_cptr, h_out, a_in");
+    OCF_CHECK(g.jr->mode == OCF_REDUCE_GRAD_ACT && g.jr->part && g.jr->row_cptr && g.jr->h_out && g.jr->a_in &&
+                  g.jr->H <= 512,
+              "ocf_gemm: the folded row reduction (jr) takes OCF_REDUCE_GRAD_ACT with part, row_cptr, h_out, a_in, "
+              "H <= 512");
     j.jr = *g.jr;
     j.jr_on = 1;
   }
@@ -133,7 +135,7 @@ bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s
     // fp32 0.0875 -> 0.0794, 8-way emulated rank step 0.2308 -> 0.2178 (ML-20M, 1,082 tiles: 12 parts)
     const bool small = g.M / 128 * 12 * 4 < g_rows_small_waves;
     const int parts = small ? 32 : 12;
-    const int grid = std::max(g.M / 128 * parts, (jb.count() + 3) / 4);
+    const int grid = (jb.count() + 3) / 4 + g.M / 128 * parts;   // job-only workgroups, then the rows
     // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
     // many entries per weight row (>= 4 on average): the LONG variant (entries as a vector, B rows of a
     // group of entries in flight together)

@@ -279,10 +279,30 @@ struct WsJobs {
     GradActParams p;
     p.a = jr.a_in; p.mask = jr.mask_in; p.keep = jr.keep; p.act = jr.act; p.d_out = jr.h_out; p.d_dtype = jr.h_dtype;
     p.ld = jr.H; p.db_part = nullptr; p.gscale = jr.gscale; p.m_real = jr.B; p.n_real = jr.n_real;
-    for (int x = lane; x < jr.H; x += 64) {
-      float v = 0.f;
-      for (int c = c0; c < c1; ++c) v += jr.part[(int64_t)c * jr.H + x];
-      const float d = grad_act_value(p, b, x, v);
+    // H <= 512: the lane's (up to) 8 columns summed over the row's chunks in chunk order, the partial
+    // loads of 4 chunks x 8 columns in flight together (the per-column loop waited once per chunk)
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    const int nx = (jr.H - lane + 63) / 64;
+    for (int c = c0; c < c1; c += 4) {
+      float x4[4][8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          x4[k][i] = (c + k < c1 && i < nx) ? jr.part[(int64_t)(c + k) * jr.H + lane + 64 * i] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < c1)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] += x4[k][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i >= nx) break;
+      const int x = lane + 64 * i;
+      const float d = grad_act_value(p, b, x, v[i]);
       store_ct(jr.h_out, jr.h_dtype, (int64_t)b * jr.H + x, d);
       if (jr.db_part) jr.db_part[(int64_t)b * jr.H + x] = d * jr.gscale;
     }

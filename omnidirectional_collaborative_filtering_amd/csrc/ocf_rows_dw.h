@@ -118,13 +118,18 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
   constexpr int E0 = RS_E0;
   using Row = RpRow<CT, CW, NCH, E0, ADAM, LONG>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {  // folded small jobs (hidden-bias update from the decoder's partials, the step's stats): one per wave
-    const int nj = jobs.count();
-    for (int j = blockIdx.x * 4 + wave; j < nj; j += gridDim.x * 4) jobs.run<KIND>(j, lane);
+  // folded small jobs (the decoder's row reduction, hidden-bias update, the step's stats): one per wave of
+  // the FIRST workgroups, which take no rows -- the row workgroups start at once on the other CUs instead
+  // of behind a job (a job is a chain of dependent loads: 10-20 us; ML-1M's dW launches were ~25 us of
+  // which the jobs' were the floor)
+  const int njwg = (jobs.count() + 3) / 4;
+  if ((int)blockIdx.x < njwg) {
+    const int j = blockIdx.x * 4 + wave;
+    if (j < jobs.count()) jobs.run<KIND>(j, lane);
+    return;
   }
-  const int t = blockIdx.x / PARTS, part = blockIdx.x % PARTS;
-  // workgroups past the last tile exist only for the jobs (a small M with many jobs): no rows, no
-  // record (reading one past the last tile's would name rows of a neighbouring table)
+  const int wb = blockIdx.x - njwg;
+  const int t = wb / PARTS, part = wb % PARTS;
   if (t >= ra.M / 128) return;
   const int m0 = t * 128;
   const uint8_t* rec = ra.live ? ra.live + (int64_t)t * OCF_LIVE_REC : nullptr;
