@@ -82,8 +82,6 @@ def parse():
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
                     help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
-    ap.add_argument("--dw-rows", type=int, default=-1,
-                    help="weight gradients by the row-stream kernel (1) or the role-split MFMA kernel (0); -1: engine default")
     ap.add_argument("--split-dw", type=int, default=1,
                     help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
     ap.add_argument("--fuse-enc", type=int, default=1,
@@ -128,6 +126,7 @@ def optim(name, lr):
 
 # BASELINE.json configs by workload name: (index, dataset shape label)
 CONFIGS = {"ml100k": (0, "ML-100K", "1,682 x 943"), "ml1m": (1, "ML-1M", "3,706 x 6,040"),
+           "ml1m_u": (1, "ML-1M (U orientation: 256 users x 3,706 items)", "6,040 x 3,706"),
            "ml20m": (2, "ML-20M", "26,744 x 138,493"), "netflix": (3, "Netflix", "17,770 x 480,189")}
 REF_ASM_MS_PER_128 = {"ml20m": 233.9, "ml1m": 41.7}   # the reference's own assembler, 1 core
 
@@ -420,8 +419,6 @@ def main():
     eng.split_dw_streams = bool(args.split_dw)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
     eng.epoch_row_lists = bool(args.epoch_lists)
-    if args.dw_rows >= 0:
-        eng.dw_rows = bool(args.dw_rows)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
         eng.shadow_blocked = bool(args.shadow_blocked)
         eng._refresh_shadows()
@@ -464,7 +461,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     nnz = 0
-    epoch_lists = eng.epoch_row_lists and eng.dw_rows and eng.sparse_dw and eng.use_sparse
+    epoch_lists = eng.epoch_row_lists and eng.sparse_dw and eng.use_sparse
     if epoch_lists:
         # the timed batches' row lists, built inside the timed region (one launch sequence, as at the
         # start of every training epoch)
@@ -575,7 +572,8 @@ def main():
                 % (CONFIGS[args.config][1], CONFIGS[args.config][2],
                    (data_full.train.nnz + data_full.valid_tgt.nnz + data_full.test_tgt.nnz) / 1e6,
                    "popularity ~ rank^-%g" % args.skew if args.skew > 0 else "uniform popularity"),
-        "config": {"workload": "%s I-AutoRec train step (BASELINE configs[%d])" % (args.config, CONFIGS[args.config][0]),
+        "config": {"workload": "%s %s train step (BASELINE configs[%d])" % (args.config, "U-AutoRec" if args.config.endswith("_u")
+                                                                            else "I-AutoRec", CONFIGS[args.config][0]),
                    "rows": n_rows, "N": N,
                    "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
                    "activation": "sigmoid", "dropout": args.dropout, "compute": args.dtype + " MFMA, fp32 accumulate",
@@ -596,7 +594,7 @@ def main():
         "host_issue_ms_per_step": round(host_ms, 4),
         "row_lists": ("per epoch: ocf_epoch_row_lists for the %d timed batches inside the timed region"
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
-                     if epoch_lists else "per step (ocf_row_lists)" if eng.dw_rows else "n/a",
+                     if epoch_lists else "per step (ocf_row_lists)" if eng.sparse_dw else "n/a",
     }
     if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
         line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)

@@ -45,23 +45,17 @@ void launch(const OcfGemmArgs& g, const typename Epi::Params& ep, hipStream_t s)
   OCF_HIP(hipGetLastError());
 }
 
-// tuning switches (ocf_set_tuning); env OCF_OPTIM_WS=0 disables the role-split optimizer kernel.
+// tuning switches (ocf_set_tuning; no environment variables).
 // The role split pays off while the MFMA role's K-loop fits under the stream of a tile: at K = 256
 // (ML-20M, one GPU) 238-251 us vs 290-316 us for the generic kernel; at K = 2,048 (8-way feature
 // parallel global batch) the K-loop dominates and the generic kernel's two workgroups per CU win
 // (dW 132 / 111 us vs 175 / 137 us).
 int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (ocf_set_tuning "optim_rows")
-int g_optim_ws = -1;
+int g_optim_ws = 1;      // role-split kernel for dense-A EPI_OPTIM (ocf_set_tuning "optim_ws")
 int g_rows_long = -1;   // row-stream LONG variant: -1 by entries per row, 0 never, 1 always ("rows_long")
 int g_rows_small_waves = 8192;   // row-stream kernel: 32 parts per tile below this many waves at 12 ("rows_small_waves")
 int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
-bool optim_ws_on() {
-  if (g_optim_ws < 0) {
-    const char* e = std::getenv("OCF_OPTIM_WS");
-    g_optim_ws = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_optim_ws != 0;
-}
+bool optim_ws_on() { return g_optim_ws != 0; }
 
 int cu_count() {
   static int n[64] = {0};
@@ -285,14 +279,12 @@ void dispatch_epi(const OcfGemmArgs& g, hipStream_t s) {
           // row lists of a sparse batch operand: one wave per weight row, no MFMA over the zeros
           if (g.a_sparse && g.sp_rowptr && g.sp_rowent && g.sp_vals && g_optim_rows && launch_rows<CT>(g, p, s)) return;
           if constexpr (sizeof(CT) == 2) {
-            // role-split kernel: slots present (SGD stays generic), row-major B, and for a sparse A
-            // the (column tile, K-step) buckets of ocf_sparse_tiles
+            // role-split kernel for a dense A (16-bit, slots present -- SGD stays generic --, row-major B);
+            // a sparse A goes to the row-stream kernel above or, without row lists, the generic kernel
             const bool ws_kind = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
                                  (g.opt.kind == OCF_OPT_ADAM && g.s2);
-            if (optim_ws_on() && g.K <= g_optim_ws_max_k && ws_kind && g.s1 && !g.b_blocked &&
-                (!g.a_sparse || (g.sp_bptr && g.sp_ent))) {
-              if (g.a_sparse) launch_ws<CT, true>(g, p, s);
-              else launch_ws<CT, false>(g, p, s);
+            if (optim_ws_on() && g.K <= g_optim_ws_max_k && ws_kind && g.s1 && !g.b_blocked && !g.a_sparse) {
+              launch_ws<CT, false>(g, p, s);
               return;
             }
           }

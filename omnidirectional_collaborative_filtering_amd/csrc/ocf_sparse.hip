@@ -349,11 +349,8 @@ template <typename WT> bool gather_shape(int H, int& G, int& ppl) {
   const int pieces = H / EPc<WT>::v;
   // group width cap: 32 lanes x 2 pieces per entry beat 64 x 1 at H = 512 (ML-20M step: decoder
   // 72 -> 55 us, encoder 57 -> 50 us): twice the entries in flight per workgroup and one shuffle
-  // step less per dot product.  OCF_RG_GMAX overrides (diagnostics).
-  static const int gmax = [] {
-    const char* e = std::getenv("OCF_RG_GMAX");
-    return e ? std::atoi(e) : 32;
-  }();
+  // step less per dot product.
+  constexpr int gmax = 32;
   for (int g : {64, 32, 16})
     if (g <= gmax && pieces % g == 0 && pieces / g <= 4) {
       G = g;

@@ -301,6 +301,8 @@ def split_ratings(rows, cols, vals, n_rows, n_cols, split=(0.8, 0.1, 0.1), rng=N
 SYNTH_SHAPES = {
     "ml100k": dict(rows=1682, cols=943, nnz=100_000, half_stars=False),
     "ml1m": dict(rows=3706, cols=6040, nnz=1_000_209, half_stars=False),
+    # BASELINE configs[1] as worded ("256 users x ~3.7k items"): the U orientation, rows = users
+    "ml1m_u": dict(rows=6040, cols=3706, nnz=1_000_209, half_stars=False),
     "ml20m": dict(rows=26_744, cols=138_493, nnz=20_000_263, half_stars=True),
     "netflix": dict(rows=17_770, cols=480_189, nnz=100_480_507, half_stars=False),
 }

@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -36,7 +35,7 @@ TILE = 128
 # (O(chunks^2) per row): past this many chunks in a batch row, a separate ocf_rows_reduce runs instead
 # (skewed ML-20M-shaped batch, rows up to ~170 chunks: fused 128 us vs 135 us for the two gathers;
 # a Netflix-sized row of 900 chunks would re-read 1.6 GB of partials)
-FUSE_MAX_CHUNKS = int(os.environ.get("OCF_FUSE_MAX_CHUNKS", 256))
+FUSE_MAX_CHUNKS = 256
 DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
           "bfloat16": (_lib.DT_BF16, torch.bfloat16)}
 DTYPE_ALIASES = {"f32": "float32", "fp32": "float32", "f16": "float16", "fp16": "float16", "half": "float16",
@@ -265,17 +264,12 @@ class Engine:
         # of up to 512 hidden units
         rows_ok = max(self.Hp[0], self.Hp[-1]) <= 512
         self.sparse_dw = Bp <= (4096 if rows_ok else 2048 if self.cdt != _lib.DT_F32 else 512)
-        self.dw_buckets = True      # sparse dW operands bucketed per batch -> persistent dW kernel
-        # ... and as row lists (the buckets' transpose) for the row-stream kernel (ocf_rows_dw.h): one
-        # wave per live weight row streams whole parameter / slot rows and forms the row's gradient from
-        # its ~2 entries, no MFMA over the mostly-zero batch operand.  ML-20M step 0.50 -> 0.44 ms
-        # (dW 200 -> 150-165 us per launch).  16-bit and fp32 compute (fp32: the B rows of h / dh are
-        # fp32, no shadow; the exact-fp32 ML-20M step 1.27 ms on the generic MFMA kernel before).
-        self.dw_rows = rows_ok
+        # ... and as row lists (per weight row: the batch's entries in that column) for the row-stream kernel
+        # (ocf_rows_dw.h): one wave per live weight row streams whole parameter / slot rows and forms the
+        # row's gradient from its entries, no MFMA over the mostly-zero batch operand.  ML-20M step 0.50 ->
+        # 0.44 ms against the role-split MFMA kernel on per-batch tile buckets (that sparse path is gone: the
+        # row lists serve every sparse first / last layer of up to 512 hidden units, fp32 and 16-bit).
 
-        # with it, sparse operands pay off up to K = 2,048 (the 8-way feature-parallel global batch):
-        # emulated rank steps 4-way 0.353 -> 0.308 ms, 8-way 0.317 -> 0.294 ms vs the dense-operand
-        # generic kernel
         self.tb = None
         self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
         # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
@@ -294,7 +288,6 @@ class Engine:
         self.live_rec = [torch.zeros(self.Np // TILE * _lib.LIVE_REC, device=d, dtype=torch.uint8) for _ in range(2)]
         self._rtag_val = 0
         self._rtag_live = False
-        self._tb_par = 0
         self._stats_pending = None
         self._gbuf = {}
         HpL = self.Hp[-1]
@@ -320,10 +313,12 @@ class Engine:
         self._side_busy = False
         # generator batches: the row lists come from the generator's per-epoch build (BatchGenerator.
         # prepare_row_lists) instead of the per-step ocf_row_lists launches
-        self.epoch_row_lists = os.environ.get("OCF_EPOCH_LISTS", "1") != "0"
-        self.epoch_scatter = os.environ.get("OCF_EPOCH_SCATTER", "1") != "0"   # ... and their scatter outputs
+        # (False: per-step ocf_scatter_batch + ocf_row_lists, for a batch source without an epoch plan;
+        # bit-identical, tests/test_rows_dw_gpu.py, and oracle-checked, tests/test_semantics_gpu.py)
+        self.epoch_row_lists = True
+        self.epoch_scatter = True   # ... and their scatter outputs
         # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
-        self.fold_reduce = os.environ.get("OCF_FOLD_REDUCE", "1") != "0"
+        self.fold_reduce = True
         self._reduce_job = None
         self._fused_step = False
         self._live_ptrs = None
@@ -503,9 +498,9 @@ class Engine:
         if gather is not None and self.sparse_ok and self.use_sparse:
             xval = self._buf("xval", int(a.E1))
             a.xval1 = ptr(xval)
-            if self.sparse_dw and self.dw_buckets and targets["flag"] == 1:   # train split: inputs = targets
+            if self.sparse_dw and targets["flag"] == 1:   # train split: inputs = targets
                 rl = gather.get("row_lists") if self.epoch_row_lists else None
-                if self.dw_rows and rl is not None:
+                if rl is not None:
                     # the epoch's row lists and live records, built once per epoch by the generator
                     # (ocf_epoch_row_lists): no per-step counting, keys or tags
                     t = rl(self.Np)
@@ -514,17 +509,11 @@ class Engine:
                     # ... and the batch's scatter outputs (ocf_epoch_scatter): no per-step scatter
                     if self.epoch_scatter:
                         epoch_entries = dict(xval=t["xval"], flag=t["tflag"])
-                elif self.dw_rows:
+                else:
                     # per-column counts and entry keys from the scatter -> row lists (ocf_row_lists)
                     a.col_cnt = ptr(self._buf("col_cnt", self.Np, torch.int32))
                     a.ecb = ptr(self._buf("ecb", int(a.E1), torch.int32))
                     lists = True
-                else:
-                    # tile-bucket counts from the scatter (ocf_sparse_tiles then skips its count pass);
-                    # two counter sets alternate so the fill pass can zero the next batch's
-                    gm, nk = self.Np // TILE, self.Bp // 64
-                    self._tb_par ^= 1
-                    a.tb_cnt, a.tb_nk = ptr(self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)), nk
                 if self.row_skip and epoch_lists is None:
                     self._rtag_val = self._rtag_val % 255 + 1
                     a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
@@ -544,7 +533,7 @@ class Engine:
             if epoch_lists is not None:
                 self.tb = epoch_lists
             else:
-                self.tb = self._row_lists(int(a.E1)) if lists else (self._tile_buckets() if a.tb_cnt else None)
+                self.tb = self._row_lists(int(a.E1)) if lists else None
         self._xin_clean = False
 
     def _row_lists(self, E):
@@ -562,29 +551,6 @@ class Engine:
             a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
         call("ocf_row_lists", a, cur_stream())
         return dict(sp_rowptr=rptr, sp_rowent=rent, sp_nent=E)
-
-    def _tile_buckets(self):
-        """the batch's entries bucketed by (user tile, K-step) for the persistent weight-gradient
-        kernel (ocf_sparse_tiles); shared by dW_out (deltas) and dW_in (inputs): same entries"""
-        t = self.tseg
-        gm, nk = self.Np // TILE, self.Bp // 64
-        a = _lib.OcfTileBucketArgs()
-        p = lambda v: ptr(v) if torch.is_tensor(v) else v
-        a.rows, a.rp, a.tptr, a.col, a.lidx, a.lboff = (p(t[k]) for k in ("t_rows", "t_rp", "t_tptr", "t_col", "t_lidx",
-                                                                          "t_lboff"))
-        a.krows, a.ntiles, a.gm, a.nk = self.B, t["t_ntiles"], gm, nk
-        cnt = self._buf("tb_cnt%d" % self._tb_par, gm * nk, torch.int32)        # counted by the scatter
-        nxt = self._buf("tb_cnt%d" % (self._tb_par ^ 1), gm * nk, torch.int32)
-        bptr = self._buf("tb_ptr", gm * nk + 1, torch.int32)
-        ent = self._buf("tb_ent", 2 * self.gt["E"], torch.int32)
-        a.cnt, a.bptr, a.ent, a.cap = ptr(cnt), ptr(bptr), ptr(ent), self.gt["E"]
-        a.counted, a.cnt_clear = 1, ptr(nxt)
-        out = dict(sp_bptr=bptr, sp_ent=ent)
-        if self._rtag_live:
-            a.rtag_in, a.rtag_out, a.rtag = ptr(self.rtag[0]), ptr(self.rtag[1]), self._rtag_val
-            a.live_in, a.live_out = ptr(self.live_rec[0]), ptr(self.live_rec[1])
-        call("ocf_sparse_tiles", a, cur_stream())
-        return out
 
     def load_dense(self, inputs, out_mask, targets, rows=None):
         """API path: dense arrays in the model.py input order.  rows (device int64 [B]): the batch is rows

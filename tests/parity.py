@@ -217,7 +217,7 @@ def with_duplicates(rows, cols, nnz, dup_frac=0.03, half_stars=True, seed=0):
 
 
 def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_dtype, dropout, seed, oracle_batch,
-                         eval_batches=4, envelope=False, lr=0.005):
+                         eval_batches=4, envelope=False, lr=0.005, epoch_lists=True):
     """The DEFAULT training path (data_reader with rng='numpy' -> fit_generator, one hidden layer,
     aux None = k=1 row gathers, the per-epoch row lists and scatter outputs, row-stream dW with
     live-row skipping) on the reference's data semantics: reciprocal split with s<1, pass-through
@@ -232,6 +232,7 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
     om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype=compute_dtype,
                     seed=11, dropout_probability=dropout)
     m = om.model
+    om.engine.epoch_row_lists = om.engine.epoch_scatter = epoch_lists
     m.compile(Adagrad(lr=lr, epsilon=1e-8), "mean_squared_error", metrics=["accurate_MSE"])
     w0 = m.get_weights()
     np.random.seed(seed)
@@ -247,8 +248,12 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
             masks.append([om.engine.mask[0][:B, :H].cpu().numpy().astype(np.float64)])
     e = om.engine
     # the default path really ran: row gathers, the epoch's row lists + scatter outputs, live-row records
-    assert e.gt is not None and "xval" in e.gt and "flag" in e.gt, "epoch scatter outputs not used"
-    assert getattr(gen, "_rl", None) is not None and e.tb is not None and "sp_rowptr" in e.tb
+    if epoch_lists:
+        assert e.gt is not None and "xval" in e.gt and "flag" in e.gt, "epoch scatter outputs not used"
+        assert getattr(gen, "_rl", None) is not None
+    else:                                  # per-step ocf_scatter_batch + ocf_row_lists
+        assert e.gt is not None and getattr(gen, "_rl", None) is None
+    assert e.tb is not None and "sp_rowptr" in e.tb
     assert e._rtag_live, "live-row records expected (Adagrad, l2 = 0)"
     w_gpu = m.get_weights()
     ora = OmniOracle([N, H, N], activation="sigmoid", dropout=dropout, dtype=np.float64).set_params(w0[0::2],

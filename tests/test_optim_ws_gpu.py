@@ -1,6 +1,8 @@
-"""The persistent role-split optimizer kernel (ocf_optim_ws.h) is bit-identical to the generic tile
-kernel + EpiOptim epilogue: dense and sparse batch operands, every optimizer, shadows, the in-kernel
-output-bias column sums, K from one K-step to many (odd and even), fewer tiles than workgroups."""
+"""The persistent role-split optimizer kernel (ocf_optim_ws.h; the dense-operand EPI_OPTIM path: 16-bit
+dense batches, K <= 512) is bit-identical to the generic tile kernel + EpiOptim epilogue: every optimizer,
+shadows, the in-kernel output-bias column sums, K from one K-step to many (odd and even), fewer tiles than
+workgroups; its oracle parity is tests/test_train_gpu.py::test_low_precision_dropout[False-*].  Also the
+tile buckets / row lists of ocf_sparse_tiles (the row-stream kernel tests build their lists with it)."""
 import numpy as np
 import pytest
 import torch
@@ -184,32 +186,6 @@ def test_sparse_tiles_buckets(gpu, shape):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(256, 128, 64, 40), (1280, 512, 256, 256), (512, 256, 320, 300)])
-def test_ws_sparse_bit_identical_and_equals_dense(gpu, shape):
-    M, N, K, krows = shape
-    cd = _lib.DT_F16
-    sp, dense = _sparse_batch(M, K, krows, seed=K)
-    bptr, ent = _buckets(sp, M, K)
-    _, Bm, state = _operands(cd, M, N, K, seed=5)
-    Ad = torch.from_numpy(dense).half().cuda()
-    opt = OPTS["adagrad"](2e-3)
-    # generic sparse kernel (tptr walk) vs the role-split kernel on the buckets
-    prev = set_ws(0)
-    try:
-        ref = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=sp, shadow_blocked=0, colsum=True)
-        set_ws(1)
-        got = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=dict(sp, sp_bptr=bptr, sp_ent=ent), shadow_blocked=0,
-                   colsum=True)
-        # the sparse operand is the dense one: same LDS image, same result
-        dn = _run(cd, M, N, K, opt, Ad, Bm, state, shadow_blocked=0, colsum=True)
-    finally:
-        set_ws(prev)
-    for r, x, y in zip(ref, got, dn):
-        assert torch.equal(r, x)
-        assert torch.equal(r, y)
-
-
-@pytest.mark.gpu
 def test_ws_matches_torch_reference(gpu):
     """Adagrad on the f16 product against a float64 torch reference of the same op."""
     M, N, K = 768, 256, 256
@@ -304,60 +280,6 @@ def _rec_valid(rec):
     for t, n in enumerate(L):
         out.append([rec[t, 16 + (k % 8) * 16 + k // 8] for k in range(n)])
     return L, out
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(1280, 512, 256, 256), (2560, 512, 128, 100), (512, 256, 320, 300)])
-@pytest.mark.parametrize("cd", [_lib.DT_F16, _lib.DT_BF16])
-def test_ws_live_rows_bit_identical(gpu, shape, cd):
-    """Row skipping (ocf.h OcfGemmArgs row_live): with Adagrad and l2 = 0 only the listed rows of each
-    tile are streamed (densely, by rank); rows not listed (no batch entry in that column: zero
-    gradient) are neither read nor written.  The result -- parameters, slot, shadow, column sums --
-    equals the full update bit for bit; listed rows include every column with an entry plus random
-    extra rows (a superset is allowed).  The records come from ocf_sparse_tiles (checked against the
-    NumPy restatement)."""
-    M, N, K, krows = shape
-    sp, dense = _sparse_batch(M, K, krows, seed=K + 1, col_frac=0.6)
-    _, Bm, state = _operands(cd, M, N, K, seed=9)
-    Ad = torch.from_numpy(dense).to(torch.float16 if cd == _lib.DT_F16 else torch.bfloat16).cuda()
-    rng = np.random.RandomState(M)
-    TAG = 7
-    tags = rng.randint(0, 256, size=M).astype(np.uint8)
-    tags[tags == TAG] = 0
-    used = (dense != 0).any(0)
-    tags[used] = TAG
-    tags[rng.rand(M) < 0.1] = TAG
-    tags[:128][(rng.rand(128) < 0.5) & ~used[:128]] = TAG + 1     # tile 0: only the used rows live
-    if M >= 384:
-        assert not (dense[:, 128:256] != 0).any()
-        tags[128:256] = 0                           # tile 1: no live row at all
-    live = tags == TAG
-    assert (~live).sum() > M // 10                  # there is something to skip
-    # records through ocf_sparse_tiles (both record arrays; targets tagged with the inputs' tags)
-    gm, nk = M // 128, K // 64
-    rt = torch.from_numpy(tags).cuda()
-    rec_in = torch.full((gm * _lib.LIVE_REC,), 0xEE, dtype=torch.uint8, device="cuda")
-    rec_out = torch.full_like(rec_in, 0xEE)
-    bptr, ent = _buckets(sp, M, K, extra=dict(rtag_in=rt, rtag_out=rt, rtag=TAG, live_in=rec_in, live_out=rec_out))
-    want_L, want = _rec_valid(live_records(live))
-    for rec in (rec_in, rec_out):
-        got_L, got = _rec_valid(rec.cpu().numpy())
-        np.testing.assert_array_equal(got_L, want_L)
-        assert got == want
-    opt = OPTS["adagrad"](2e-3)
-    spb = dict(sp, sp_bptr=bptr, sp_ent=ent)
-    prev = set_ws(1)
-    try:
-        full = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True)
-        skip = _run(cd, M, N, K, opt, Ad, Bm, state, sparse=spb, shadow_blocked=0, colsum=True,
-                    extra=dict(row_live=rec_in))
-    finally:
-        set_ws(prev)
-    for r, x in zip(full, skip):
-        assert torch.equal(r, x)
-    dead = torch.from_numpy(~live).cuda()
-    assert torch.equal(skip[0][dead], state[0][dead])      # rows not listed untouched
-    assert not torch.equal(skip[0][~dead], state[0][~dead])
 
 
 @pytest.mark.gpu

@@ -144,6 +144,25 @@ def test_train_parity_golden_toy(gpu, ci, cd):
         assert_low_precision(res, 2e-3)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+@pytest.mark.parametrize("ci", [1, 3, 4])
+def test_train_parity_per_step_row_lists(gpu, ci, cd):
+    """the same training against the reference batches with the per-step row lists (ocf_scatter_batch with
+    per-column counts + ocf_row_lists + the scatter's row tags: Engine.epoch_row_lists = False, the path for
+    a batch source without an epoch plan)"""
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    rd, gold = _toy_reader("I")
+    res = run_semantics_parity(rd, cfg["B"], 16, 99, sp, pt, float(auxv), cd, 0.2, cfg["seed_base"] + ci,
+                               lambda bi, rows: _gold_batch(gold, name, "train1", bi, aux_type),
+                               envelope=cd != "float32", epoch_lists=False)
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 2e-3)
+
+
 _DUP_DATA = {}
 
 
