@@ -4,8 +4,8 @@
   configs[1] MovieLens-1M I-AutoRec (3,706 x 6,040), 1 x 500, B = 256, bf16 MFMA
   configs[2] MovieLens-20M I-AutoRec (26,744 x 138,493): bench.py's exact step (f16 MFMA, row gathers,
              sparse dW operands, live-row skipping, dropout 0.2, Adagrad 0.005)
-  configs[3] Netflix I-AutoRec, N = 480,189 users on one GPU (2,048 of the 17,770 item rows, full width):
-             one step vs the oracle, and row skipping on/off bit-identical
+  configs[3] Netflix I-AutoRec, N = 480,189 users on one GPU (4,096 of the 17,770 item rows, full width):
+             three steps vs the oracle, and row skipping on/off bit-identical
   configs[4] Jester (train_jester.py: 100 jokes, causal concat -> 200 inputs, 2 x 256 tanh, RMSprop,
              reciprocal 0.5 input/output split, Model.fit with validation_split 0.1), all 73,421 users
 
@@ -46,8 +46,8 @@ def test_ml20m_bench_step(gpu):
     def hook(om):
         e = om.engine
         assert e.use_sparse and e.sparse_ok and e.row_skip
-    res = run_parity("float16", "adagrad", 1, "sigmoid", steps=2, B=256, H=500, dropout=0.2, data=_synth("ml20m"),
-                     envelope=True, sparse_oracle=True, eval_batches=2, model_hook=hook)
+    res = run_parity("float16", "adagrad", 1, "sigmoid", steps=6, B=256, H=500, dropout=0.2, data=_synth("ml20m"),
+                     envelope=True, sparse_oracle=True, eval_batches=8, model_hook=hook)
     e = res.om.engine
     assert e.sparse_dw and res.live_rows_used, "the benchmarked path (sparse dW operands + live-row records) ran"
     assert_low_precision(res, 2e-3)
@@ -57,11 +57,11 @@ def test_ml20m_bench_step(gpu):
 @pytest.mark.timeout(900)
 def test_netflix_width_one_gpu(gpu):
     """N = 480,189: the full-width model (W1 / W_out 480,189 x 500, slots, shadows: ~4 GB) on one GPU;
-    one step vs the oracle; then the same step with row skipping off is bit-identical"""
-    data = _synth("netflix", scale_rows=2048)
+    three steps vs the oracle; then the same steps with row skipping off are bit-identical"""
+    data = _synth("netflix", scale_rows=4096)
     assert data.num_cols == 480_189
-    res = run_parity("float16", "adagrad", 1, "sigmoid", steps=1, B=256, H=500, dropout=0.2, data=data,
-                     envelope=True, sparse_oracle=True, eval_batches=1)
+    res = run_parity("float16", "adagrad", 1, "sigmoid", steps=3, B=256, H=500, dropout=0.2, data=data,
+                     envelope=True, sparse_oracle=True, eval_batches=2)
     assert res.live_rows_used
     assert_low_precision(res, 2e-3)
     w_skip = res.w
@@ -69,7 +69,7 @@ def test_netflix_width_one_gpu(gpu):
 
     def no_skip(om):
         om.engine.row_skip = False
-    res2 = run_parity("float16", "adagrad", 1, "sigmoid", steps=1, B=256, H=500, dropout=0.2, data=data,
+    res2 = run_parity("float16", "adagrad", 1, "sigmoid", steps=3, B=256, H=500, dropout=0.2, data=data,
                       eval_rmse=False, model_hook=no_skip)
     assert not res2.live_rows_used
     for a, b in zip(w_skip, res2.w):
