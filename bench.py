@@ -439,6 +439,8 @@ def main():
 
     def step(i):
         bi = batches[i % len(batches)]
+        if dpo is None and eng.fast_train_step(gen, bi):    # Model._train_one's one-call step
+            return int(nnz_of[bi])
         m._load(None, gen, bi)
         if dpo is not None:
             dpo.step()

@@ -291,6 +291,31 @@ typedef struct OcfGemmArgs {
 
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
 
+/*
+ * ocf_train_step_rows -- one whole single-GPU training step of a one-hidden-layer model on a sparse
+ * (generator) batch, the Keras train_on_batch that fit_generator runs per step (train.py:157 ->
+ * model.py:64-86 forward, train.py:49 masked MSE, train.py:50-51 Adagrad / RMSprop / Adam): the encoder
+ * gather, the decoder gather (with the hidden layer's epilogue), dW_out (+ the folded row reduction jr
+ * when jr_on, the output bias) and dW_in (+ the hidden bias, the step's stats), i.e.
+ *   ocf_gather_encoder(&enc); ocf_gather_decoder(&dec); ocf_gemm(&dw_out with .jr = &jr); ocf_gemm(&dw_in)
+ * in one library call: each member is exactly what the four calls take (the same checks run).  The host
+ * keeps one of these per model and rewrites only the batch's table pointers and the step's Philox stream /
+ * stats slot / optimizer constants between steps (engine.Engine.fast_train_step), so issuing a step costs
+ * one call instead of building four argument blocks (the small configs' steps are host-bound otherwise).
+ * dw_out.jr is ignored (jr_on selects the folded reduction).
+ */
+typedef struct OcfRowStepArgs {
+  OcfGatherArgs enc;
+  OcfGatherArgs dec;
+  OcfGemmArgs dw_out;
+  OcfGemmArgs dw_in;
+  OcfRowsReduceArgs jr; int jr_on;
+  /* (nullable) hipEvent_t recorded on `stream` before / after each launch: encoder, decoder, dW_out, dW_in
+   * (the per-kernel timing bench.py reports; recorded only where set) */
+  void* ev[8];
+} OcfRowStepArgs;
+int ocf_train_step_rows(const OcfRowStepArgs* args, void* stream);
+
 /* split-K reductions fused with the layer epilogue (see OCF_EPI_BIAS_ACT / OCF_EPI_GRAD_ACT).
  * ocf_splitk_grad_act writes bias-gradient partials db[M/4][ld] (one row per 4 batch rows,
  * already * gscale) for ocf_bias_opt_from_partials. */

@@ -119,6 +119,11 @@ class OcfGemmArgs(ctypes.Structure):
     ]
 
 
+class OcfRowStepArgs(ctypes.Structure):
+    _fields_ = [("enc", OcfGatherArgs), ("dec", OcfGatherArgs), ("dw_out", OcfGemmArgs), ("dw_in", OcfGemmArgs),
+                ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8)]
+
+
 class OcfTileBucketArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
@@ -148,6 +153,7 @@ SIGNATURES = {
     "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P, P]),
     "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
+    "ocf_train_step_rows": (I32, [ctypes.POINTER(OcfRowStepArgs), P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),

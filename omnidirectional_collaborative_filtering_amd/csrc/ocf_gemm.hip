@@ -400,3 +400,29 @@ extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   }
   OCF_TRY_END
 }
+
+// one training step of the row-gather path in one call (ocf.h): the four launches of
+// engine.Engine.train_step's folded single-GPU sequence, each through its own entry point (same checks)
+extern "C" int ocf_train_step_rows(const OcfRowStepArgs* a, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(a != nullptr, "ocf_train_step_rows: null arguments");
+  hipStream_t s = (hipStream_t)stream;
+  auto ev = [&](int k) {
+    if (a->ev[k]) OCF_HIP(hipEventRecord((hipEvent_t)a->ev[k], s));
+  };
+  ev(0);
+  OCF_CHECK(ocf_gather_encoder(&a->enc, stream) == 0, ocf_last_error());
+  ev(1);
+  ev(2);
+  OCF_CHECK(ocf_gather_decoder(&a->dec, stream) == 0, ocf_last_error());
+  ev(3);
+  OcfGemmArgs o = a->dw_out;
+  o.jr = a->jr_on ? &a->jr : nullptr;
+  ev(4);
+  OCF_CHECK(ocf_gemm(&o, stream) == 0, ocf_last_error());
+  ev(5);
+  ev(6);
+  OCF_CHECK(ocf_gemm(&a->dw_in, stream) == 0, ocf_last_error());
+  ev(7);
+  OCF_TRY_END
+}

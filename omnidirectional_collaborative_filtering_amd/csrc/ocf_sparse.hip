@@ -187,6 +187,23 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
   float hv[V];
+  // entry indices one iteration ahead; the bias of each entry's column loads with its weight row.  The
+  // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->
+  // LDS) and this one (flag / column / target) overlap instead of running back to back
+  bool live[RG_U];
+  int n[RG_U];
+  float t[RG_U];
+  auto idx = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < RG_U; ++u) {
+      const int ju = j + u * NG;
+      const bool ok = ju < j1;
+      live[u] = ok && a.flag[lb + ju];
+      n[u] = ok ? a.col[s + ju] : 0;
+      t[u] = ok ? a.val[s + ju] : 0.f;
+    }
+  };
+  idx(j0 + grp);
   if (a.enc_part) {
     // the hidden layer's epilogue from the encoder partials (rows_reduce_kernel BIAS_ACT arithmetic); the
     // row's first chunk stores a / h / mask for the backward pass
@@ -199,8 +216,16 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
     p.m_real = a.m_real; p.n_real = a.n_real;
     const int e0 = a.enc_cptr[b], e1 = a.enc_cptr[b + 1];
     for (int x = threadIdx.x; x < a.H; x += RG_THREADS) {
+      // the chunk partials of 4 chunks in flight together, added in chunk order (the same sums)
       float v = 0.f;
-      for (int c = e0; c < e1; ++c) v += a.enc_part[(int64_t)c * a.H + x];
+      for (int c = e0; c < e1; c += 4) {
+        float q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = c + k < e1 ? a.enc_part[(int64_t)(c + k) * a.H + x] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (c + k < e1) v += q[k];
+      }
       red[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, v));
     }
     __syncthreads();
@@ -222,21 +247,6 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
   float sse = 0.f, sae = 0.f, cnt = 0.f;
-  // entry indices one iteration ahead; the bias of each entry's column loads with its weight row
-  bool live[RG_U];
-  int n[RG_U];
-  float t[RG_U];
-  auto idx = [&](int j) {
-#pragma unroll
-    for (int u = 0; u < RG_U; ++u) {
-      const int ju = j + u * NG;
-      const bool ok = ju < j1;
-      live[u] = ok && a.flag[lb + ju];
-      n[u] = ok ? a.col[s + ju] : 0;
-      t[u] = ok ? a.val[s + ju] : 0.f;
-    }
-  };
-  idx(j0 + grp);
   for (int j = j0 + grp; j < j1; j += NG * RG_U) {
     uint4 w[RG_U][PPL];
     bool lv[RG_U];

@@ -40,6 +40,7 @@ GATHER_CHUNK_SMALL = 64
 GATHER_BIG = 100_000
 ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the library takes up to 65,535)
 ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
+ROWS_DENSE_MAX_COLS = 170 * 128  # the row-stream kernel's small regime (ocf_gemm.hip rows_small_waves: 170 tiles)
 
 
 _RNG_STREAMS = {}
@@ -291,6 +292,11 @@ class BatchGenerator(object):
                             max_chunks=int(ch["max_chunks"][bi]))
         if self.split == "train":      # train batches: inputs = targets -> the weight-gradient row lists
             out["row_lists"] = lambda n_cols, bi=bi: self.row_lists(bi, n_cols)
+            # >= 2 entries per weight row on average: (nearly) every row is live, and on a weight of few row
+            # tiles (the row-stream kernel's small regime: about one row per wave) the live-row records' two
+            # dependent loads would only lengthen every wave's index chain -> the engine passes no records
+            N = self.r.num_items
+            out["rows_dense"] = bool(self.num_batches and self.nnz1.mean() >= 2 * N and N <= ROWS_DENSE_MAX_COLS)
         return out
 
     def prepare_row_lists(self, n_cols, batches=None):
@@ -382,6 +388,35 @@ class BatchGenerator(object):
                     row_ent=rl["row_ent"].data_ptr() + 8 * e0,
                     live=rl["live"].data_ptr() + s * (n_cols // 128) * _lib.LIVE_REC,
                     xval=rl["xval"].data_ptr() + 4 * e0, tflag=rl["tflag"].data_ptr() + e0)
+
+    def step_fields(self, bi, n_cols):
+        """batch bi's table pointers and sizes for the one-call training step (Engine.fast_train_step):
+        (rows, lboff, ch_row, ch_j0, ch_j1, n_chunks, row_cptr, max_chunks, entries, row_ptr, row_ent, live,
+        xval, tflag) -- the values gather_tables / targets / row_lists give -- or None when batch bi's row
+        lists are not built (row_lists builds them on the general path).  Computed once per row-list window."""
+        rl = getattr(self, "_rl", None)
+        if self.split != "train" or rl is None or rl["n_cols"] != n_cols:
+            return None
+        s = rl["slot"].get(bi)
+        if s is None:
+            return None
+        ff = rl.get("fields")
+        if ff is None:
+            B, ch = self.B, self.chunks1
+            sel = np.fromiter(rl["slot"].keys(), dtype=np.int64, count=len(rl["slot"]))
+            slots = np.fromiter(rl["slot"].values(), dtype=np.int64, count=len(rl["slot"]))
+            order = np.argsort(slots)
+            sel, slots = sel[order], slots[order]
+            c0 = ch["cbase"][sel]
+            e0 = rl["ebase_host"][slots]
+            cols = [self.rows_dev.data_ptr() + 4 * sel * B, self.lboff1_dev.data_ptr() + 8 * sel * (B + 1),
+                    ch["ch_row"].data_ptr() + 4 * c0, ch["ch_j0"].data_ptr() + 4 * c0, ch["ch_j1"].data_ptr() + 4 * c0,
+                    ch["cbase"][sel + 1] - c0, ch["row_cptr"].data_ptr() + 4 * sel * (B + 1), ch["max_chunks"][sel],
+                    self.nnz1[sel], rl["row_ptr"].data_ptr() + 4 * slots * (n_cols + 1),
+                    rl["row_ent"].data_ptr() + 8 * e0, rl["live"].data_ptr() + slots * (n_cols // 128) * _lib.LIVE_REC,
+                    rl["xval"].data_ptr() + 4 * e0, rl["tflag"].data_ptr() + e0]
+            ff = rl["fields"] = list(zip(*[np.asarray(c, dtype=np.int64).tolist() for c in cols]))
+        return ff[s]
 
     @staticmethod
     def _local_offsets(lens, rows):

@@ -28,7 +28,17 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import OcfGemmArgs, OcfScatterArgs, call
+from ._lib import OcfGemmArgs, OcfScatterArgs
+
+# while Engine._recorded_step runs: every library call of the step as (name, args) -- the template of the
+# one-call step (Engine.fast_train_step)
+_recorder = None
+
+
+def call(name, *args):
+    if _recorder is not None:
+        _recorder.append((name, args))
+    return _lib.call(name, *args)
 
 TILE = 128
 # the decoder gather re-reduces a row's encoder chunk partials in every one of that row's chunks
@@ -95,6 +105,11 @@ class Engine:
         self.pad_dims = [self.k * self.Np] + self.Hp + [self.Np]
         self.n_tiles = self.Np // TILE
         self.step_count = 0
+        # one-call training steps (fast_train_step): template + per-batch rewrite, invalidated by any
+        # reallocation of a buffer the step reads (_bufgen)
+        self.fast_steps = True
+        self._plan = None
+        self._bufgen = 0
         # row data parallelism (parallel.DataParallel): the rank is mixed into the dropout stream so the
         # G local batches draw independent masks, like one global batch; grad_hook(i) is called once
         # layer i's raw gradients are written (grads_out steps), so its exchange can start right away
@@ -210,6 +225,7 @@ class Engine:
 
     def set_optimizer(self, opt):
         self.opt = opt
+        self._bufgen += 1
         self.slots = []
         for w, b in zip(self.W, self.b):
             sw = [torch.zeros_like(w) for _ in range(opt.n_slots)] + [None] * (2 - opt.n_slots)
@@ -282,7 +298,8 @@ class Engine:
         # live target with the step's tag (cycling 1..255, no clearing); with Adagrad and l2 = 0 the
         # role-split dW kernels skip the parameter / slot / shadow traffic of the untagged rows, whose
         # update is the identity (zero gradient).  Bit-identical to the full update.
-        self.row_skip = True
+        self.row_skip = True        # (epoch row lists: records only for batches of < 2 entries per weight row
+        #                             on average; "always": records whatever the density)
         self.rtag = [torch.zeros(self.Np, device=d, dtype=torch.uint8) for _ in range(2)]   # inputs, targets
         # per 128-row tile: the live rows (ocf.h OCF_LIVE_REC), built by ocf_sparse_tiles from the tags
         self.live_rec = [torch.zeros(self.Np // TILE * _lib.LIVE_REC, device=d, dtype=torch.uint8) for _ in range(2)]
@@ -410,6 +427,7 @@ class Engine:
         if t is None or t.numel() < n:
             t = torch.zeros(max(n + n // 4, 1 << 12), device=self.dev, dtype=dtype)
             self._gbuf[name] = t
+            self._bufgen += 1          # the one-call step's template holds the old pointers
         return t
 
     def _grow_buckets(self, n):
@@ -505,7 +523,11 @@ class Engine:
                     # (ocf_epoch_row_lists): no per-step counting, keys or tags
                     t = rl(self.Np)
                     epoch_lists = dict(sp_rowptr=t["row_ptr"], sp_rowent=t["row_ent"], sp_nent=int(a.E1))
-                    self._live_ptrs = (t["live"], t["live"]) if self.row_skip else None
+                    # live-row records only where rows go without entries: with >= 2 entries per weight row
+                    # on average (ML-1M, ML-100K, feature-parallel global batches) nearly every row is live
+                    # and the records' two dependent loads would only lengthen each wave's index chain
+                    self._live_ptrs = (t["live"], t["live"]) if (
+                        self.row_skip == "always" or (self.row_skip and not gather.get("rows_dense"))) else None
                     # ... and the batch's scatter outputs (ocf_epoch_scatter): no per-step scatter
                     if self.epoch_scatter:
                         epoch_entries = dict(xval=t["xval"], flag=t["tflag"])
@@ -752,6 +774,7 @@ class Engine:
         if (with_grad and self.comm is None and self._fused_step and self.fold_reduce and self._folds()
                 and self.trainable[0]):
             self._reduce_job = r          # rides in the dW_out launch (OcfGemmArgs jr), see _backward_gather
+            self._last_jr = r             # (kept alive: the recorded step's dW_out arguments point at it)
         else:
             call("ocf_rows_reduce", r, cur_stream())
 
@@ -1103,6 +1126,203 @@ class Engine:
         self.output_loss(with_grad=True)
         self.backward_update(grads_out)
         self._join()
+        self.step_count += 1
+
+    # ---------------------------------------------------------------- one-call training step
+    # A step of the default single-GPU path (one hidden layer, generator batch, epoch row lists, the folded
+    # jobs) is four library calls whose argument blocks differ from step to step only in the batch's table
+    # pointers / sizes, the dropout stream, the stats slot and the optimizer constants.  Building the blocks
+    # in Python costs ~0.07 ms per step -- as long as the whole GPU step of ML-100K / ML-1M.  So the blocks
+    # of one recorded step become a template (ocf.h OcfRowStepArgs) and later steps rewrite only those
+    # fields and issue ocf_train_step_rows.  The template is checked before use: a second recorded step
+    # must equal the template rewritten for that step, byte for byte (any field that varies and is not
+    # rewritten fails the check and the engine stays on the general path).
+    _STEP_CALLS = ("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm", "ocf_gemm")
+    # generator step fields (BatchGenerator.step_fields): rows, lboff, ch_row, ch_j0, ch_j1, n_chunks,
+    # row_cptr, max_chunks, entries, row_ptr, row_ent, live, xval, tflag -> template fields
+    _F_ROWS, _F_LBOFF, _F_CHR, _F_J0, _F_J1, _F_NCH, _F_CPTR, _F_MAXCH, _F_E, _F_RPTR, _F_RENT, _F_LIVE, \
+        _F_XVAL, _F_TFLAG = range(14)
+    _GATHER_FIELDS = (("rows", 0), ("lboff", 1), ("ch_row", 2), ("ch_j0", 3), ("ch_j1", 4), ("n_chunks", 5))
+    _DW_FIELDS = (("sp_rows", 0), ("sp_lboff", 1), ("sp_nent", 8), ("sp_rowptr", 9), ("sp_rowent", 10))
+
+    def _fast_key(self, gen):
+        """identity of everything the template holds besides the per-step fields, or None when the step
+        takes the general path"""
+        tok = getattr(gen, "_step_token", None)
+        if tok is None:
+            from .data_reader import BatchGenerator
+            if not (isinstance(gen, BatchGenerator) and gen.split == "train"):
+                return None
+            Engine._gen_tokens += 1
+            tok = gen._step_token = Engine._gen_tokens
+        key = (tok, self._bufgen, id(self.opt), self.opt.lr, self.opt.decay, getattr(self.opt, "epsilon", 0.0),
+               self.row_skip, self.shadow_blocked, self.keep,
+               self.seed, self.act, self.comm, self.dp_world, self.use_sparse, self.sparse_dw, self.epoch_row_lists,
+               self.epoch_scatter, self.fold_jobs, self.fold_reduce, self.fuse_enc_epilogue, self.l2,
+               tuple(self.trainable), self.grad_hook, self.master_sync)
+        pl = self._plan
+        if pl is not None and pl["key"] == key:
+            return key
+        if not (self.comm is None and self.dp_world == 1 and len(self.H) == 1 and self.sparse_ok and self.use_sparse
+                and self.sparse_dw and self.epoch_row_lists and self.epoch_scatter and self.fold_jobs and
+                self.fold_reduce and self.fuse_enc_epilogue and not self.l2 and all(self.trainable) and
+                self.grad_hook is None and self.master_sync is None):
+            return None
+        return key
+
+    _gen_tokens = 0
+
+    def fast_train_step(self, gen, bi):
+        """Model._train_one's step on generator batch bi through ocf_train_step_rows; False when this step
+        must take the general path (then nothing was done)."""
+        if not self.fast_steps or (self.timers is not None and self.timer_only is None):
+            return False
+        key = self._fast_key(gen)
+        if key is None:
+            return False
+        pl = self._plan
+        if pl is not None and pl.get("ready") and pl["key"] == key:
+            f = gen.step_fields(bi, self.Np)
+            if f is not None and self._fits(pl, f):
+                self._issue(pl, f)
+                return True
+        # the general path, recorded
+        self._grow_stats(self.n_stats + 1)
+        per = self._per_step()
+        calls = self._recorded_step(gen, bi)
+        key = self._fast_key(gen)              # (buffers may have grown during the step)
+        f = gen.step_fields(bi, self.Np)
+        if key is None or f is None or tuple(n for n, _ in calls) != self._STEP_CALLS:
+            self._plan = None
+            return True
+        if pl is not None and pl["key"] == key and not pl.get("ready") and pl.get("bad", 0) < 2:
+            # second recorded step: the template rewritten for it must reproduce it exactly
+            st = _lib.OcfRowStepArgs.from_buffer_copy(pl["st"])
+            cand = dict(pl, st=st)
+            self._bind(cand)
+            self._rewrite(cand, f, per)
+            if self._same(cand, calls):
+                cand["ready"] = True
+                self._plan = cand
+            else:                              # start over from this step (at most twice)
+                self._plan = self._template(key, calls, f)
+                self._plan["bad"] = pl.get("bad", 0) + 1
+            return True
+        if pl is not None and pl.get("bad", 0) >= 2 and pl["key"] == key:
+            return True                        # this template does not verify: stay on the general path
+        self._plan = self._template(key, calls, f)
+        return True
+
+    def _recorded_step(self, gen, bi):
+        global _recorder
+        a = gen.scatter_args(bi, engine_args=self.scatter_args())
+        self.load_batch(a, gen.targets(bi, self.N), gather=gen.gather_tables(bi))
+        _recorder = []
+        try:
+            self.train_step()
+            return list(_recorder)
+        finally:
+            _recorder = None
+
+    def _per_step(self):
+        """the fields of a step that change with the step itself: Philox stream of the dropout mask
+        (forward), stats slot, optimizer constants (Keras decay / Adam bias correction)"""
+        row = self.stats_hist.data_ptr() + self.n_stats * self.stats_hist.stride(0) * 4
+        stream = (self.step_count * self.dp_world + self.dp_rank) * 16
+        if self.opt.kind != _lib.OPT_ADAM and not self.opt.decay and self._plan is not None \
+                and self._plan.get("ready"):
+            return stream, row, None, None     # constant optimizer scalars: the template's stand
+        gscale = 2.0 / (self.B * self.N_total)
+        op = self.opt.step_params(1.0, self.l2)
+        o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
+        return stream, row, o, self.opt.step_params(1.0, 0.0)
+
+    def _template(self, key, calls, f):
+        st = _lib.OcfRowStepArgs()
+        enc, dec, g_out, g_in = [c[1][0] for c in calls]
+        ctypes.memmove(ctypes.addressof(st.enc), ctypes.addressof(enc), ctypes.sizeof(enc))
+        ctypes.memmove(ctypes.addressof(st.dec), ctypes.addressof(dec), ctypes.sizeof(dec))
+        ctypes.memmove(ctypes.addressof(st.dw_out), ctypes.addressof(g_out), ctypes.sizeof(g_out))
+        ctypes.memmove(ctypes.addressof(st.dw_in), ctypes.addressof(g_in), ctypes.sizeof(g_in))
+        if g_out.jr:
+            ctypes.memmove(ctypes.addressof(st.jr), g_out.jr, ctypes.sizeof(st.jr))
+            st.jr_on = 1
+        st.dw_out.jr = None
+        pl = dict(key=key, st=st, cap_enc=self._gbuf["part_enc"].numel() // self.Hp[0],
+                  cap_dec=min(self._gbuf["part_dec"].numel() // self.Hp[-1], self._gbuf["chunk_stats"].numel() // 4),
+                  cap_e=self._gbuf["delta_e"].numel())
+        self._bind(pl)
+        return pl
+
+    def _bind(self, pl):
+        st = pl["st"]
+        sets = []
+        for obj in (st.enc, st.dec):
+            sets += [(obj, n, i) for n, i in self._GATHER_FIELDS]
+        for obj in (st.dw_out, st.dw_in):
+            sets += [(obj, n, i) for n, i in self._DW_FIELDS]
+            sets.append((obj, "row_live", self._F_LIVE))
+        sets += [(st.enc, "xval", self._F_XVAL), (st.dec, "flag", self._F_TFLAG), (st.dec, "enc_cptr", self._F_CPTR),
+                 (st.dw_in, "sp_vals", self._F_XVAL)]
+        if st.jr_on:
+            sets.append((st.jr, "row_cptr", self._F_CPTR))
+        pl["sets"] = sets
+        pl["live"] = bool(st.dw_out.row_live)
+
+    def _fits(self, pl, f):
+        return (f[self._F_NCH] <= pl["cap_enc"] and f[self._F_NCH] <= pl["cap_dec"] and f[self._F_E] <= pl["cap_e"]
+                and f[self._F_MAXCH] <= FUSE_MAX_CHUNKS and self.n_stats < self.stats_cap)
+
+    def _rewrite(self, pl, f, per):
+        for obj, name, i in pl["sets"]:
+            setattr(obj, name, f[i])
+        st = pl["st"]
+        if not pl["live"]:
+            st.dw_out.row_live = st.dw_in.row_live = None
+        st.dec.stream, st.dw_in.js_out = per[0], per[1]
+        if per[2] is not None:
+            st.dw_out.opt = st.dw_in.opt = per[2]
+            st.dw_out.cb_op = st.dw_in.jb_op = per[3]
+
+    def _same(self, pl, calls):
+        st = pl["st"]
+        enc, dec, g_out, g_in = [c[1][0] for c in calls]
+        b = lambda x: ctypes.string_at(ctypes.addressof(x), ctypes.sizeof(x))
+        o = type(g_out).from_buffer_copy(g_out)
+        jr_ok = (not g_out.jr and not st.jr_on) or (
+            g_out.jr and st.jr_on and ctypes.string_at(g_out.jr, ctypes.sizeof(st.jr)) == b(st.jr))
+        o.jr = None
+        return jr_ok and b(enc) == b(st.enc) and b(dec) == b(st.dec) and b(o) == b(st.dw_out) and b(g_in) == b(st.dw_in)
+
+    _EV_PHASES = ("enc_gemm", "dec_gemm_mse", "dW_out", "dW_in")
+
+    def _issue(self, pl, f):
+        self._rewrite(pl, f, self._per_step())
+        st = pl["st"]
+        timed = []
+        if self.timers is not None:            # bench.py's per-kernel HIP events, recorded by the library
+            for k, name in enumerate(self._EV_PHASES):
+                if self.timer_only is None or name in self.timer_only:
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()                 # (creates the events; the library records them again)
+                    b.record()
+                    st.ev[2 * k], st.ev[2 * k + 1] = a.cuda_event, b.cuda_event
+                    timed.append((k, name, a, b))
+        call("ocf_train_step_rows", st, cur_stream())
+        for k, name, a, b in timed:
+            self.timers.setdefault(name, []).append((a, b))
+            st.ev[2 * k] = st.ev[2 * k + 1] = None
+        # the general path's bookkeeping (load_batch + train_step)
+        self._fused_step = True
+        self._xin_clean = False
+        # what the general path leaves behind for the loaded batch (callers inspect the path taken)
+        self.gt = dict(xval=f[self._F_XVAL], flag=f[self._F_TFLAG], E=f[self._F_E], one_call=True)
+        self.tb = dict(sp_rowptr=f[self._F_RPTR], sp_rowent=f[self._F_RENT], sp_nent=f[self._F_E])
+        self._rtag_live = pl["live"]
+        self.tseg = None
+        self._enc_fused = self._reduce_job = self._stats_pending = None
+        self.n_stats += 1
+        self.opt.iterations += 1
         self.step_count += 1
 
     def eval_step(self):

@@ -81,6 +81,16 @@ class Model(object):
                 raise StopIteration("generator exhausted")
             self._check_gen(gen)
             self._load(None, gen, idx[self.rank])
+        elif self.dp is None and isinstance(gen, BatchGenerator):
+            self._check_gen(gen)
+            bi = gen.next_batch_index()
+            if bi is None:
+                raise StopIteration("generator exhausted (data_reader.py:418 yields None)")
+            # the whole step in one library call when the engine's template applies (Engine.fast_train_step)
+            if not self.engine.fast_train_step(gen, bi):
+                self._load(None, gen, bi)
+                self.engine.train_step()
+            return
         else:
             self._pull(gen)
         if self.dp is not None:

@@ -254,7 +254,8 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
     else:                                  # per-step ocf_scatter_batch + ocf_row_lists
         assert e.gt is not None and getattr(gen, "_rl", None) is None
     assert e.tb is not None and "sp_rowptr" in e.tb
-    assert e._rtag_live, "live-row records expected (Adagrad, l2 = 0)"
+    assert e._rtag_live == (e.row_skip == "always" or getattr(gen, "_rl", None) is None or
+                            not gen.gather_tables(0)["rows_dense"]), "live-row records expected (Adagrad, l2 = 0)"
     w_gpu = m.get_weights()
     ora = OmniOracle([N, H, N], activation="sigmoid", dropout=dropout, dtype=np.float64).set_params(w0[0::2],
                                                                                                    w0[1::2])

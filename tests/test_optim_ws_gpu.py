@@ -313,7 +313,7 @@ def test_engine_row_skip_bit_identical(gpu, cd):
         om = om_ = omni_model(1, 200, cols, B, dense_activation="sigmoid", use_causal_info=False,
                               compute_dtype=cd, seed=4)
         eng = om.engine
-        eng.row_skip = skip
+        eng.row_skip = "always" if skip else False
         m = om.model
         m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
         gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
