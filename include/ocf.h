@@ -158,6 +158,9 @@ typedef struct OcfGatherArgs {
    * arithmetic; the first chunk of each batch row also stores a_out, mask_out and h (h is then written) */
   const float* enc_part; const int32_t* enc_cptr; const float* bias_h; int act; float keep;
   uint64_t seed, stream; float* a_out; uint8_t* mask_out; int m_real, n_real;
+  /* decoder, optional: a word the launch sets to zero (ocf_gemm_pair's sync word for the step's pair launch
+   * that follows: the engine lets the decoder clear it instead of a separate memset) */
+  uint64_t* zero_word;
 } OcfGatherArgs;
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);
@@ -292,13 +295,26 @@ typedef struct OcfGemmArgs {
 int ocf_gemm(const OcfGemmArgs* args, void* stream);
 
 /*
+ * ocf_gemm_pair -- ocf_gemm(a) then ocf_gemm(b) for the two weight updates of a one-hidden-layer step
+ * (a = the output layer, with the decoder's folded row reduction jr; b = the input layer, whose operand B
+ * and job inputs that reduction writes: train.py:50-51 for both kernels).  When both take the row-stream
+ * kernel with the same instance they run as ONE launch: b's workgroups wait, in the kernel, for a's
+ * row-reduction workgroups (agent-scope release / acquire on sync[0]), so the two row streams run back to
+ * back without a kernel boundary.  sync: device uint64[2]; sync[0] must be zero when the launch starts
+ * (the caller clears it: the engine's decoder gather does, OcfGatherArgs zero_word); NULL = two launches.
+ * Results are identical to the two ocf_gemm calls.
+ */
+int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, void* sync, void* stream);
+
+/*
  * ocf_train_step_rows -- one whole single-GPU training step of a one-hidden-layer model on a sparse
  * (generator) batch, the Keras train_on_batch that fit_generator runs per step (train.py:157 ->
  * model.py:64-86 forward, train.py:49 masked MSE, train.py:50-51 Adagrad / RMSprop / Adam): the encoder
  * gather, the decoder gather (with the hidden layer's epilogue), dW_out (+ the folded row reduction jr
  * when jr_on, the output bias) and dW_in (+ the hidden bias, the step's stats), i.e.
  *   ocf_gather_encoder(&enc); ocf_gather_decoder(&dec); ocf_gemm(&dw_out with .jr = &jr); ocf_gemm(&dw_in)
- * in one library call: each member is exactly what the four calls take (the same checks run).  The host
+ * in one library call (dw_out / dw_in through ocf_gemm_pair when pair_sync is set): each member is exactly
+ * what the four calls take (the same checks run).  The host
  * keeps one of these per model and rewrites only the batch's table pointers and the step's Philox stream /
  * stats slot / optimizer constants between steps (engine.Engine.fast_train_step), so issuing a step costs
  * one call instead of building four argument blocks (the small configs' steps are host-bound otherwise).
@@ -313,6 +329,8 @@ typedef struct OcfRowStepArgs {
   /* (nullable) hipEvent_t recorded on `stream` before / after each launch: encoder, decoder, dW_out, dW_in
    * (the per-kernel timing bench.py reports; recorded only where set) */
   void* ev[8];
+  /* (nullable) ocf_gemm_pair's sync words: dW_out and dW_in as one launch (events 4 and 7 bracket it) */
+  void* pair_sync;
 } OcfRowStepArgs;
 int ocf_train_step_rows(const OcfRowStepArgs* args, void* stream);
 

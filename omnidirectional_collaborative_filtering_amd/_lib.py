@@ -75,7 +75,7 @@ class OcfGatherArgs(ctypes.Structure):
         ("h", P), ("h_dtype", I32), ("bias", P), ("aux", F32), ("delta_e", P), ("chunk_stats", P),
         ("d_out", P), ("d_dtype", I32), ("ld_d", I64),
         ("enc_part", P), ("enc_cptr", P), ("bias_h", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64),
-        ("a_out", P), ("mask_out", P), ("m_real", I32), ("n_real", I32),
+        ("a_out", P), ("mask_out", P), ("m_real", I32), ("n_real", I32), ("zero_word", P),
     ]
 
 
@@ -121,7 +121,7 @@ class OcfGemmArgs(ctypes.Structure):
 
 class OcfRowStepArgs(ctypes.Structure):
     _fields_ = [("enc", OcfGatherArgs), ("dec", OcfGatherArgs), ("dw_out", OcfGemmArgs), ("dw_in", OcfGemmArgs),
-                ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8)]
+                ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8), ("pair_sync", P)]
 
 
 class OcfTileBucketArgs(ctypes.Structure):
@@ -153,6 +153,7 @@ SIGNATURES = {
     "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P, P]),
     "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
+    "ocf_gemm_pair": (I32, [ctypes.POINTER(OcfGemmArgs), ctypes.POINTER(OcfGemmArgs), P, P]),
     "ocf_train_step_rows": (I32, [ctypes.POINTER(OcfRowStepArgs), P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),

@@ -103,66 +103,102 @@ void jobs_after(const OcfGemmArgs& g, hipStream_t s) {
 // EPI_OPTIM over a sparse batch operand given as row lists: the row-stream kernel (ocf_rows_dw.h),
 // one wave per weight row.  Takes 16-bit or fp32 compute, Adagrad / RMSprop / Adam with their slots, N a
 // multiple of 128 up to 512 and a row-major shadow; anything else returns false (the tile kernels).
+struct RowsLaunch {
+  RowsDwArgs ra;
+  WsJobs jb;
+  int grid, parts, N;
+  bool lng, small;
+  int kind;
+};
+
+bool rows_setup(const OcfGemmArgs& g, const EpiOptim::Params& ep, RowsLaunch& L) {
+  // a lane's B elements are one 4-, 8- or 16-B load (16-bit or fp32 compute)
+  const bool kind_ok = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
+                       (g.opt.kind == OCF_OPT_ADAM && g.s2);
+  if (!(kind_ok && g.s1 && g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N && g.M % 128 == 0))
+    return false;
+  if (ep.shadow && ep.shadow_blocked) return false;
+  RowsDwArgs& ra = L.ra;
+  ra = RowsDwArgs{};
+  ra.p = g.p; ra.s1 = g.s1; ra.s2 = g.s2; ra.ld = g.ld_out; ra.M = g.M; ra.N = g.N;
+  ra.B = g.B; ra.ldb = g.ldb;
+  ra.rowptr = g.sp_rowptr; ra.rowent = reinterpret_cast<const int2*>(g.sp_rowent); ra.vals = g.sp_vals;
+  ra.live = g.row_live;
+  ra.op = g.opt;
+  ra.shadow = ep.shadow;
+  ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
+  L.jb = ws_jobs(g);
+  // workgroups per 128-row tile (each a twelfth of the tile's live rows): with the 75-VGPR pipeline
+  // (6 waves per SIMD) 12 parts measured best, ML-20M step 0.4243-0.4269 ms against 6 / 8 / 16 / 24 / 32
+  // parts 0.439-0.441 / 0.4332-0.4364 / 0.437 / 0.430 / 0.446
+  // A weight of few rows (ML-1M: 48 tiles; ML-100K: 8; an 8-way feature rank's 136) leaves the chip
+  // mostly idle at 12 parts, each wave walking ~3 rows through the 5-stage pipeline's fill: there a wave
+  // takes ~one row (32 parts).  Measured (ms/step, 12 -> 32 parts): ML-1M bf16 0.1225 -> 0.1064, ML-100K
+  // fp32 0.0875 -> 0.0794, 8-way emulated rank step 0.2308 -> 0.2178 (ML-20M, 1,082 tiles: 12 parts)
+  L.small = g.M / 128 * 12 * 4 < g_rows_small_waves;
+  L.parts = L.small ? 32 : 12;
+  L.grid = (L.jb.count() + 3) / 4 + g.M / 128 * L.parts;   // job-only workgroups, then the rows
+  // many entries per weight row (>= 4 on average): the LONG variant (entries as a vector, B rows of a
+  // group of entries in flight together)
+  L.lng = g_rows_long < 0 ? g.sp_nent >= 4LL * g.M : g_rows_long != 0;
+  L.N = g.N;
+  L.kind = g.opt.kind;
+  return true;
+}
+
+// the kernel instance for (optimizer, N, parts, LONG): f(kernel template tag) launches it
+template <typename CT, typename F>
+void rows_dispatch(const RowsLaunch& L, F&& f) {
+  auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
+    constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
+    constexpr int NCH = decltype(nch_tag)::value;
+    if (L.lng && L.small) f.template go<CT, KIND, CW, NCH, 32, true>();
+    else if (L.lng) f.template go<CT, KIND, CW, NCH, 12, true>();
+    else if (L.small) f.template go<CT, KIND, CW, NCH, 32, false>();
+    else f.template go<CT, KIND, CW, NCH, 12, false>();
+  };
+  using std::integral_constant;
+  auto by_n = [&](auto k) {
+    switch (L.N) {
+      case 128: go(k, integral_constant<int, 2>{}, integral_constant<int, 1>{}); break;
+      case 256: go(k, integral_constant<int, 4>{}, integral_constant<int, 1>{}); break;
+      case 384: go(k, integral_constant<int, 2>{}, integral_constant<int, 3>{}); break;
+      default: go(k, integral_constant<int, 4>{}, integral_constant<int, 2>{});
+    }
+  };
+  switch (L.kind) {
+    case OCF_OPT_ADAGRAD: by_n(integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
+    case OCF_OPT_RMSPROP: by_n(integral_constant<int, OCF_OPT_RMSPROP>{}); break;
+    default: by_n(integral_constant<int, OCF_OPT_ADAM>{});
+  }
+}
+
+struct RowsOne {
+  const RowsLaunch& L;
+  hipStream_t s;
+  template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
+    hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, LONG>), dim3(L.grid), dim3(RS_THREADS), 0, s,
+                       L.ra, L.jb);
+  }
+};
+struct RowsPair {
+  const RowsLaunch& A;
+  const RowsLaunch& B;
+  RsPair ps;
+  hipStream_t s;
+  template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
+    hipLaunchKernelGGL((optim_rowpipe_pair_kernel<CT, KIND, CW, NCH, PARTS, LONG>), dim3(A.grid + B.grid),
+                       dim3(RS_THREADS), 0, s, A.ra, A.jb, B.ra, B.jb, ps);
+  }
+};
+
 template <typename CT>
 bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
-  {   // a lane's B elements are one 4-, 8- or 16-B load (16-bit or fp32 compute)
-    const bool kind_ok = g.opt.kind == OCF_OPT_ADAGRAD || g.opt.kind == OCF_OPT_RMSPROP ||
-                         (g.opt.kind == OCF_OPT_ADAM && g.s2);
-    if (!(kind_ok && g.s1 && g.N % 128 == 0 && g.N <= 512 && g.ldb >= g.N && g.ld_out == g.N && g.M % 128 == 0))
-      return false;
-    if (ep.shadow && ep.shadow_blocked) return false;
-    RowsDwArgs ra{};
-    ra.p = g.p; ra.s1 = g.s1; ra.s2 = g.s2; ra.ld = g.ld_out; ra.M = g.M; ra.N = g.N;
-    ra.B = g.B; ra.ldb = g.ldb;
-    ra.rowptr = g.sp_rowptr; ra.rowent = reinterpret_cast<const int2*>(g.sp_rowent); ra.vals = g.sp_vals;
-    ra.live = g.row_live;
-    ra.op = g.opt;
-    ra.shadow = ep.shadow;
-    ra.colsum = g.sp_colsum; ra.colsum_scale = g.opt.gscale;
-    const WsJobs jb = ws_jobs(g);
-    // workgroups per 128-row tile (each a twelfth of the tile's live rows): with the 75-VGPR pipeline
-    // (6 waves per SIMD) 12 parts measured best, ML-20M step 0.4243-0.4269 ms against 6 / 8 / 16 / 24 / 32
-    // parts 0.439-0.441 / 0.4332-0.4364 / 0.437 / 0.430 / 0.446
-    // A weight of few rows (ML-1M: 48 tiles; ML-100K: 8; an 8-way feature rank's 136) leaves the chip
-    // mostly idle at 12 parts, each wave walking ~3 rows through the 5-stage pipeline's fill: there a wave
-    // takes ~one row (32 parts).  Measured (ms/step, 12 -> 32 parts): ML-1M bf16 0.1225 -> 0.1064, ML-100K
-    // fp32 0.0875 -> 0.0794, 8-way emulated rank step 0.2308 -> 0.2178 (ML-20M, 1,082 tiles: 12 parts)
-    const bool small = g.M / 128 * 12 * 4 < g_rows_small_waves;
-    const int parts = small ? 32 : 12;
-    const int grid = (jb.count() + 3) / 4 + g.M / 128 * parts;   // job-only workgroups, then the rows
-    // (CW, NCH): chunk width and chunks per lane, N = 64 CW NCH
-    // many entries per weight row (>= 4 on average): the LONG variant (entries as a vector, B rows of a
-    // group of entries in flight together)
-    const bool lng = g_rows_long < 0 ? g.sp_nent >= 4LL * g.M : g_rows_long != 0;
-    auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
-      constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
-      constexpr int NCH = decltype(nch_tag)::value;
-      if (lng && small)
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 32, true>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
-      else if (lng)
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 12, true>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
-      else if (small)
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 32, false>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
-      else
-        hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, 12, false>), dim3(grid), dim3(RS_THREADS), 0, s, ra, jb);
-    };
-    using std::integral_constant;
-    auto by_n = [&](auto k) {
-      switch (g.N) {
-        case 128: go(k, integral_constant<int, 2>{}, integral_constant<int, 1>{}); break;
-        case 256: go(k, integral_constant<int, 4>{}, integral_constant<int, 1>{}); break;
-        case 384: go(k, integral_constant<int, 2>{}, integral_constant<int, 3>{}); break;
-        default: go(k, integral_constant<int, 4>{}, integral_constant<int, 2>{});
-      }
-    };
-    switch (g.opt.kind) {
-      case OCF_OPT_ADAGRAD: by_n(integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
-      case OCF_OPT_RMSPROP: by_n(integral_constant<int, OCF_OPT_RMSPROP>{}); break;
-      default: by_n(integral_constant<int, OCF_OPT_ADAM>{});
-    }
-    OCF_HIP(hipGetLastError());
-    return true;
-  }
+  RowsLaunch L;
+  if (!rows_setup(g, ep, L)) return false;
+  rows_dispatch<CT>(L, RowsOne{L, s});
+  OCF_HIP(hipGetLastError());
+  return true;
 }
 
 // EPI_OPTIM on [K][M] x [K][N] operands (the dW GEMMs) through the persistent role-split kernel
@@ -367,9 +403,8 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   OCF_TRY_END
 }
 
-extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
-  OCF_TRY_BEGIN
-  const OcfGemmArgs& g = *args;
+namespace {
+void check_gemm(const OcfGemmArgs& g) {
   OCF_CHECK((g.A || g.a_sparse) && g.B, "ocf_gemm: null operand");
   OCF_CHECK(g.M > 0 && g.N > 0 && g.K > 0, "ocf_gemm: empty shape");
   OCF_CHECK(g.M % GT_BM == 0 && g.N % GT_BN == 0, "ocf_gemm: M and N must be multiples of 128");
@@ -391,12 +426,73 @@ extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   OCF_CHECK(!g.cb_p || g.sp_colsum, "ocf_gemm: cb_p needs sp_colsum");
   OCF_CHECK(!g.jb_part || g.jb_p, "ocf_gemm: jb_part needs jb_p");
   OCF_CHECK(!g.js_sp || g.js_out, "ocf_gemm: js_sp needs js_out");
+}
+
+// both weight updates of a step in one row-stream launch (ocf_gemm_pair), when both take the row-stream
+// kernel with the same instance
+EpiOptim::Params optim_params(const OcfGemmArgs& g) {
+  EpiOptim::Params p{g.p, g.s1, g.s2, g.ld_out, g.opt, g.p_shadow, g.compute_dtype, g.shadow_blocked != 0};
+  p.row_live = g.row_live;
+  return p;
+}
+bool rows_pair_ok(const OcfGemmArgs& g) {
+  return g.epi == OCF_EPI_OPTIM && g.a_col && g.b_col && g.a_sparse && g.sp_rowptr && g.sp_rowent && g.sp_vals &&
+         g.p && g.b_dtype == g.compute_dtype && (int64_t)g.M * g.ld_out * 4 < (int64_t(1) << 31) &&
+         (!g.p_shadow || g.compute_dtype != OCF_F32) && (!g.row_live || (g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f));
+}
+template <typename CT>
+bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, unsigned long long* sync, hipStream_t s) {
+  if (!g_optim_rows || !rows_pair_ok(a) || !rows_pair_ok(b)) return false;
+  RowsLaunch A, B;
+  if (!rows_setup(a, optim_params(a), A) || !rows_setup(b, optim_params(b), B)) return false;
+  if (A.kind != B.kind || A.N != B.N || A.parts != B.parts || A.lng != B.lng || A.small != B.small) return false;
+  // small weights (about one row per wave) keep two launches: there the in-kernel wait (the producers'
+  // L2 write-back, the consumers' polling) cost more than the boundary it replaces (ML-1M 36.9 vs 36.8 us,
+  // ML-100K 25.8 vs 21.7; ML-20M 303 vs 307: tools/step_parts_probe.py)
+  if (A.small) return false;
+  RsPair ps;
+  ps.sync = sync;
+  ps.n_a = A.grid;
+  ps.n_prod = A.jb.jr_on ? (A.jb.jr.Bp + 3) / 4 : 0;   // the job-only workgroups holding the row reduction
+  rows_dispatch<CT>(A, RowsPair{A, B, ps, s});
+  OCF_HIP(hipGetLastError());
+  return true;
+}
+}  // namespace
+
+extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
+  OCF_TRY_BEGIN
+  const OcfGemmArgs& g = *args;
+  check_gemm(g);
   hipStream_t s = (hipStream_t)stream;
   switch (g.compute_dtype) {
     case OCF_F16: dispatch<_Float16>(g, s); break;
     case OCF_BF16: dispatch<__bf16>(g, s); break;
     case OCF_F32: dispatch<float>(g, s); break;
     default: throw std::runtime_error("ocf_gemm: bad compute dtype");
+  }
+  OCF_TRY_END
+}
+
+extern "C" int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, void* sync, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(a && b, "ocf_gemm_pair: null arguments");
+  check_gemm(*a);
+  check_gemm(*b);
+  hipStream_t s = (hipStream_t)stream;
+  auto* sy = reinterpret_cast<unsigned long long*>(sync);
+  bool done = false;
+  if (sy && a->compute_dtype == b->compute_dtype) {
+    switch (a->compute_dtype) {
+      case OCF_F16: done = launch_rows_pair<_Float16>(*a, *b, sy, s); break;
+      case OCF_BF16: done = launch_rows_pair<__bf16>(*a, *b, sy, s); break;
+      case OCF_F32: done = launch_rows_pair<float>(*a, *b, sy, s); break;
+      default: break;
+    }
+  }
+  if (!done) {
+    OCF_CHECK(ocf_gemm(a, stream) == 0, ocf_last_error());
+    OCF_CHECK(ocf_gemm(b, stream) == 0, ocf_last_error());
   }
   OCF_TRY_END
 }
@@ -418,11 +514,17 @@ extern "C" int ocf_train_step_rows(const OcfRowStepArgs* a, void* stream) {
   ev(3);
   OcfGemmArgs o = a->dw_out;
   o.jr = a->jr_on ? &a->jr : nullptr;
-  ev(4);
-  OCF_CHECK(ocf_gemm(&o, stream) == 0, ocf_last_error());
-  ev(5);
-  ev(6);
-  OCF_CHECK(ocf_gemm(&a->dw_in, stream) == 0, ocf_last_error());
-  ev(7);
+  if (a->pair_sync) {          // both updates in one launch (ocf_gemm_pair): events 4 / 7 bracket it
+    ev(4);
+    OCF_CHECK(ocf_gemm_pair(&o, &a->dw_in, a->pair_sync, stream) == 0, ocf_last_error());
+    ev(7);
+  } else {
+    ev(4);
+    OCF_CHECK(ocf_gemm(&o, stream) == 0, ocf_last_error());
+    ev(5);
+    ev(6);
+    OCF_CHECK(ocf_gemm(&a->dw_in, stream) == 0, ocf_last_error());
+    ev(7);
+  }
   OCF_TRY_END
 }

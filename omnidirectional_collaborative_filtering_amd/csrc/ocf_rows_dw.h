@@ -109,8 +109,9 @@ template <typename CT, int CW, int NCH, int E0, bool ADAM, bool LONG> struct RpR
 // entries as one vector (lane i = entry i, up to 64 at a time), stage D their values as one gather, and
 // stage E walks them in groups of RS_ETL whose B rows are all in flight at once -- the entry indices come
 // from the vector by readlane, so a group waits for its B rows only, not for an entry -> value -> B chain.
+// the workgroup body of one weight matrix's launch: workgroup wbx of [job-only workgroups][row workgroups]
 template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
-__global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
+__device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs& jobs, const int wbx) {
   using V = RsVec<CW>;
   using F = typename V::F;
   using H = RsH<CT, CW>;
@@ -123,12 +124,12 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
   // of behind a job (a job is a chain of dependent loads: 10-20 us; ML-1M's dW launches were ~25 us of
   // which the jobs' were the floor)
   const int njwg = (jobs.count() + 3) / 4;
-  if ((int)blockIdx.x < njwg) {
-    const int j = blockIdx.x * 4 + wave;
+  if (wbx < njwg) {
+    const int j = wbx * 4 + wave;
     if (j < jobs.count()) jobs.run<KIND>(j, lane);
     return;
   }
-  const int wb = blockIdx.x - njwg;
+  const int wb = wbx - njwg;
   const int t = wb / PARTS, part = wb % PARTS;
   if (t >= ra.M / 128) return;
   const int m0 = t * 128;
@@ -347,5 +348,63 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
     r2s = r3s;
     r3s = r4;
   }
+}
+
+template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
+__global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
+  rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(ra, jobs, blockIdx.x);
+}
+
+// Both weight-gradient launches of a one-hidden-layer step in ONE launch (ocf_gemm_pair): workgroups
+// [0, n_a) are the output layer's (its job-only workgroups first, then its rows), the rest the input
+// layer's.  The input layer's operand B (the hidden delta) and its jobs' inputs (bias-gradient rows,
+// stats rows) are written by the output layer's folded row reduction -- the first n_prod job-only
+// workgroups.  Those publish with an agent-scope release (their XCD's L2 written back) and count in
+// sync[0]; every input-layer workgroup waits for sync[0] == n_prod before it starts (see the wait).  Deadlock-free: workgroups are dispatched in index order, so every
+// producer is resident or done before a consumer can wait, and producers wait on nothing.  The wait is
+// bounded anyway (it never ends a kernel by hanging).  The last consumer to pass resets both counters
+// (sync[1] counts the passed consumers), so the next launch finds them zero.  The two layers' rows then
+// stream back to back without a kernel boundary, and on small weights (about one row per wave, each a
+// chain of dependent loads) their latency chains overlap.
+struct RsPair {
+  unsigned long long* sync;   // [0]: completed producer workgroups (zero at the launch)
+  int n_a, n_prod;
+};
+
+template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
+__global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwArgs ra, WsJobs ja, RowsDwArgs rb,
+                                                                        WsJobs jb, RsPair ps) {
+  const int bx = blockIdx.x;
+  if (bx < ps.n_a) {
+    rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(ra, ja, bx);
+    if (bx < ps.n_prod) {
+      // every wave waits for its stores to reach the L2, then ONE release (one L2 write-back per workgroup:
+      // a release per wave made the wait cost ~15 us) publishes them with the count
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.sync, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // The wait: one plain load first (L2-cached: once a consumer of this XCD has seen the count complete,
+  // the later ones find it there), then relaxed agent-scope loads until the count is complete.  Measured
+  // and rejected: an agent-scope acquire per consumer (it invalidates the XCD's L2) and a consumer count
+  // for a self-reset (thousands of atomics on one word): the ML-20M pair launch took 1.0-1.3 ms instead of
+  // 0.31.  No invalidation is needed: the data the wait guards (the row reduction's outputs) is read in
+  // this kernel only after the wait and the kernel start invalidated every L1 / L2 line from before it, so
+  // a consumer's caches hold no stale copy -- its reads miss to memory, which the producers' release (L2
+  // write-back) has updated, or hit lines a producer on the same XCD wrote.  sync[0] is zeroed by the
+  // caller before the launch (the engine's decoder gather does it: OcfGatherArgs zero_word).
+  if (threadIdx.x == 0) {
+    const unsigned long long want = (unsigned long long)ps.n_prod;
+    if (*reinterpret_cast<volatile unsigned long long*>(ps.sync) < want)
+      for (int it = 0; it < (1 << 22); ++it) {
+        if (__hip_atomic_load(ps.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(rb, jb, bx - ps.n_a);
 }
 }  // namespace ocf

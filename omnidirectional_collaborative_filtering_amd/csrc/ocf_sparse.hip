@@ -186,6 +186,8 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   const int64_t lb = a.lboff[b];
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
+  if (a.zero_word && c == 0 && threadIdx.x == 0)
+    __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float hv[V];
   // entry indices one iteration ahead; the bias of each entry's column loads with its weight row.  The
   // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->

@@ -337,6 +337,9 @@ class Engine:
         # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
         self.fold_reduce = True
         self._reduce_job = None
+        # ... and dW_out + dW_in as one launch (ocf_gemm_pair; its two sync words stay zero between launches)
+        self.pair_dw = True
+        self.pair_sync = torch.zeros(2, device=d, dtype=torch.int64)
         self._fused_step = False
         self._live_ptrs = None
         if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
@@ -638,9 +641,12 @@ class Engine:
         g.order = kw.pop("order", 0)
         g.epi = epi
         g.keep = 1.0
+        issue = kw.pop("_issue", True)
         T = torch.Tensor
         for k, v in kw.items():
             setattr(g, k, v.data_ptr() if isinstance(v, T) else v)
+        if not issue:
+            return g
         call("ocf_gemm", g, cur_stream())
 
     # ---------------------------------------------------------------- forward
@@ -748,6 +754,8 @@ class Engine:
         g.flag = self.gt.get("flag") or ptr(self.tflag)
         g.h, g.h_dtype, g.bias, g.aux = ptr(self.h[L - 1]), self.cdt, ptr(self.b[L]), self.gt["aux"]
         g.chunk_stats = ptr(cst)
+        if with_grad and self._fused_step and self.pair_dw:
+            g.zero_word = ptr(self.pair_sync)      # cleared for this step's ocf_gemm_pair launch
         ef, self._enc_fused = self._enc_fused, None
         if ef is not None:
             g.enc_part, g.enc_cptr, g.keep, g.stream = ef["enc_part"], ef["enc_cptr"], ef["keep"], ef["stream"]
@@ -906,7 +914,7 @@ class Engine:
         if fused:
             self.opt.iterations += 1
 
-    def _weight_update_sparse(self, i, vals, Bm, ldb, N, gscale, grads_out, op, colsum=None, jobs=None):
+    def _weight_update_sparse(self, i, vals, Bm, ldb, N, gscale, grads_out, op, colsum=None, jobs=None, issue=True):
         """EPI_OPTIM / EPI_GRAD for a first/last layer whose A operand (the batch entries: deltas or
         inputs, [B][N] transposed) is built in LDS from the target CSR's column-sorted view"""
         if grads_out is None and not self.trainable[i]:
@@ -926,8 +934,9 @@ class Engine:
             o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
             if self._rtag_live and self.sparse_dw and op.kind == _lib.OPT_ADAGRAD and op.l2 == 0:
                 sp.update(row_live=self._live_ptrs[0 if i == 0 else 1])
-            self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0], s2=sw[1],
-                       ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp, **(jobs or {}))
+            return self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_OPTIM, p=self.W[i], s1=sw[0],
+                              s2=sw[1], ld_out=N, opt=o, p_shadow=self.Wsh[i], shadow_blocked=self._wblk(i), **sp,
+                              **(jobs or {}), _issue=issue)
         else:
             self._gemm(A, 1, M, Bm, self.cdt, 1, ldb, M, N, K, _lib.EPI_GRAD, out=grads_out[2 * i], ld_out=N,
                        opt=_lib.OcfOptParams(0, 0, 0, 0, 0, 0, gscale), h_dtype=self._grad_dt(grads_out[2 * i]),
@@ -996,12 +1005,22 @@ class Engine:
                 sp, n_sp, rs, n_rs, M, dst = self._stats_pending
                 late.update(js_sp=sp, js_nparts=n_sp, js_rs=rs, js_ntiles=n_rs, js_M=M, js_out=dst)
                 self._stats_pending = None
-            with self.phase("dW_out"):
-                self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op, self.db_out_col,
-                                           jobs=jobs_out)
-            with self.phase("dW_in"):
-                self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op,
-                                           jobs=jobs_in)
+            if self.pair_dw:
+                # both updates as one launch (ocf_gemm_pair): dW_in's workgroups wait in the kernel for the
+                # row reduction riding in dW_out's, instead of a kernel boundary
+                g_out = self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op,
+                                                   self.db_out_col, jobs=jobs_out, issue=False)
+                g_in = self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out,
+                                                  op, jobs=jobs_in, issue=False)
+                with self.phase("dW_pair"):
+                    call("ocf_gemm_pair", g_out, g_in, ptr(self.pair_sync), cur_stream())
+            else:
+                with self.phase("dW_out"):
+                    self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op,
+                                               self.db_out_col, jobs=jobs_out)
+                with self.phase("dW_in"):
+                    self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op,
+                                               jobs=jobs_in)
             self._reduce_job = None
             self.opt.iterations += 1
             return
@@ -1137,7 +1156,8 @@ class Engine:
     # fields and issue ocf_train_step_rows.  The template is checked before use: a second recorded step
     # must equal the template rewritten for that step, byte for byte (any field that varies and is not
     # rewritten fails the check and the engine stays on the general path).
-    _STEP_CALLS = ("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm", "ocf_gemm")
+    _STEP_CALLS = (("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm_pair"),
+                   ("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm", "ocf_gemm"))
     # generator step fields (BatchGenerator.step_fields): rows, lboff, ch_row, ch_j0, ch_j1, n_chunks,
     # row_cptr, max_chunks, entries, row_ptr, row_ent, live, xval, tflag -> template fields
     _F_ROWS, _F_LBOFF, _F_CHR, _F_J0, _F_J1, _F_NCH, _F_CPTR, _F_MAXCH, _F_E, _F_RPTR, _F_RENT, _F_LIVE, \
@@ -1159,7 +1179,7 @@ class Engine:
                self.row_skip, self.shadow_blocked, self.keep,
                self.seed, self.act, self.comm, self.dp_world, self.use_sparse, self.sparse_dw, self.epoch_row_lists,
                self.epoch_scatter, self.fold_jobs, self.fold_reduce, self.fuse_enc_epilogue, self.l2,
-               tuple(self.trainable), self.grad_hook, self.master_sync)
+               tuple(self.trainable), self.grad_hook, self.master_sync, self.pair_dw)
         pl = self._plan
         if pl is not None and pl["key"] == key:
             return key
@@ -1192,7 +1212,7 @@ class Engine:
         calls = self._recorded_step(gen, bi)
         key = self._fast_key(gen)              # (buffers may have grown during the step)
         f = gen.step_fields(bi, self.Np)
-        if key is None or f is None or tuple(n for n, _ in calls) != self._STEP_CALLS:
+        if key is None or f is None or tuple(n for n, _ in calls) not in self._STEP_CALLS:
             self._plan = None
             return True
         if pl is not None and pl["key"] == key and not pl.get("ready") and pl.get("bad", 0) < 2:
@@ -1239,7 +1259,7 @@ class Engine:
 
     def _template(self, key, calls, f):
         st = _lib.OcfRowStepArgs()
-        enc, dec, g_out, g_in = [c[1][0] for c in calls]
+        enc, dec, g_out, g_in, sync = self._step_blocks(calls)
         ctypes.memmove(ctypes.addressof(st.enc), ctypes.addressof(enc), ctypes.sizeof(enc))
         ctypes.memmove(ctypes.addressof(st.dec), ctypes.addressof(dec), ctypes.sizeof(dec))
         ctypes.memmove(ctypes.addressof(st.dw_out), ctypes.addressof(g_out), ctypes.sizeof(g_out))
@@ -1248,11 +1268,20 @@ class Engine:
             ctypes.memmove(ctypes.addressof(st.jr), g_out.jr, ctypes.sizeof(st.jr))
             st.jr_on = 1
         st.dw_out.jr = None
+        st.pair_sync = sync
         pl = dict(key=key, st=st, cap_enc=self._gbuf["part_enc"].numel() // self.Hp[0],
                   cap_dec=min(self._gbuf["part_dec"].numel() // self.Hp[-1], self._gbuf["chunk_stats"].numel() // 4),
                   cap_e=self._gbuf["delta_e"].numel())
         self._bind(pl)
         return pl
+
+    @staticmethod
+    def _step_blocks(calls):
+        """(encoder, decoder, dW_out, dW_in argument blocks, pair sync pointer or None) of a recorded step"""
+        if len(calls) == 3:
+            (g_out, g_in, sync, _) = calls[2][1]
+            return calls[0][1][0], calls[1][1][0], g_out, g_in, sync
+        return calls[0][1][0], calls[1][1][0], calls[2][1][0], calls[3][1][0], None
 
     def _bind(self, pl):
         st = pl["st"]
@@ -1286,7 +1315,9 @@ class Engine:
 
     def _same(self, pl, calls):
         st = pl["st"]
-        enc, dec, g_out, g_in = [c[1][0] for c in calls]
+        enc, dec, g_out, g_in, sync = self._step_blocks(calls)
+        if (sync or None) != (st.pair_sync or None):
+            return False
         b = lambda x: ctypes.string_at(ctypes.addressof(x), ctypes.sizeof(x))
         o = type(g_out).from_buffer_copy(g_out)
         jr_ok = (not g_out.jr and not st.jr_on) or (
@@ -1294,24 +1325,27 @@ class Engine:
         o.jr = None
         return jr_ok and b(enc) == b(st.enc) and b(dec) == b(st.dec) and b(o) == b(st.dw_out) and b(g_in) == b(st.dw_in)
 
-    _EV_PHASES = ("enc_gemm", "dec_gemm_mse", "dW_out", "dW_in")
+    # phase -> (event slot before, after) in OcfRowStepArgs.ev; dW_pair with ocf_gemm_pair
+    _EV_SLOTS = {"enc_gemm": (0, 1), "dec_gemm_mse": (2, 3), "dW_out": (4, 5), "dW_in": (6, 7), "dW_pair": (4, 7)}
 
     def _issue(self, pl, f):
         self._rewrite(pl, f, self._per_step())
         st = pl["st"]
         timed = []
         if self.timers is not None:            # bench.py's per-kernel HIP events, recorded by the library
-            for k, name in enumerate(self._EV_PHASES):
+            names = ("enc_gemm", "dec_gemm_mse") + (("dW_pair",) if st.pair_sync else ("dW_out", "dW_in"))
+            for name in names:
                 if self.timer_only is None or name in self.timer_only:
                     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     a.record()                 # (creates the events; the library records them again)
                     b.record()
-                    st.ev[2 * k], st.ev[2 * k + 1] = a.cuda_event, b.cuda_event
-                    timed.append((k, name, a, b))
+                    i0, i1 = self._EV_SLOTS[name]
+                    st.ev[i0], st.ev[i1] = a.cuda_event, b.cuda_event
+                    timed.append((i0, i1, name, a, b))
         call("ocf_train_step_rows", st, cur_stream())
-        for k, name, a, b in timed:
+        for i0, i1, name, a, b in timed:
             self.timers.setdefault(name, []).append((a, b))
-            st.ev[2 * k] = st.ev[2 * k + 1] = None
+            st.ev[i0] = st.ev[i1] = None
         # the general path's bookkeeping (load_batch + train_step)
         self._fused_step = True
         self._xin_clean = False

@@ -46,7 +46,7 @@ STRUCTS = {
                                              "xval1", "tb_cnt", "tb_nk", "rtag_in", "rtag_out", "rtag", "col_cnt", "ecb"]),
     "OcfGatherArgs": (_lib.OcfGatherArgs, ["rows", "n_chunks", "ldw", "w_blocked", "H", "part", "aux", "delta_e",
                                            "ld_d", "enc_part", "enc_cptr", "bias_h", "act", "keep", "seed",
-                                           "stream", "a_out", "mask_out", "m_real", "n_real"]),
+                                           "stream", "a_out", "mask_out", "m_real", "n_real", "zero_word"]),
     "OcfRowsReduceArgs": (_lib.OcfRowsReduceArgs, ["mode", "out", "keep", "seed", "stream", "n_real", "gscale",
                                                    "row_sse"]),
     "OcfGemmArgs": (_lib.OcfGemmArgs, ["a_col", "lda", "ldb", "epi", "split_stride", "keep", "seed", "h_dtype",
@@ -55,7 +55,7 @@ STRUCTS = {
                                        "sp_lboff", "sp_krows", "sp_colsum", "sp_bptr", "sp_ent", "cb_op", "jb_part",
                                        "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
                                        "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
-    "OcfRowStepArgs": (_lib.OcfRowStepArgs, ["enc", "dec", "dw_out", "dw_in", "jr", "jr_on", "ev"]),
+    "OcfRowStepArgs": (_lib.OcfRowStepArgs, ["enc", "dec", "dw_out", "dw_in", "jr", "jr_on", "ev", "pair_sync"]),
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
                                                        "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",
                                                        "row_ptr", "row_ent"]),

@@ -49,10 +49,12 @@ def _model(opt, dropout, data):
     return om
 
 
-@pytest.mark.parametrize("opt,dropout,sparsity", [("adagrad", 0.2, [1.0, 1.0]), ("adagrad", None, [0.3, 0.7]),
-                                                  ("adam", 0.2, [0.5, 0.9]), ("adagrad_decay", 0.2, [1.0, 1.0]),
-                                                  ("rmsprop", None, [1.0, 1.0])])
-def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
+@pytest.mark.parametrize("opt,dropout,sparsity,pair", [("adagrad", 0.2, [1.0, 1.0], True),
+                                                       ("adagrad", None, [0.3, 0.7], True),
+                                                       ("adam", 0.2, [0.5, 0.9], True),
+                                                       ("adagrad_decay", 0.2, [1.0, 1.0], False),
+                                                       ("rmsprop", None, [1.0, 1.0], False)])
+def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity, pair):
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
     r, c, v = synthetic_ratings(400, 300, 9000, half_stars=True, seed=3)
@@ -62,6 +64,7 @@ def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
                      device=torch.device("cpu"))
     om = _model(opt, dropout, data)
     eng = om.engine
+    eng.pair_dw = pair
     checked = fast = 0
     for epoch in range(5):
         gen = rd.data_gen(32, sparsity, "train", True, None, -1, pass_through_input_training=False)
@@ -82,7 +85,7 @@ def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
                 eng._grow_stats(eng.n_stats + 1)
                 eng._rewrite(cand, f, eng._per_step())
                 calls = eng._recorded_step(gen, bi)
-                assert [n for n, _ in calls] == list(eng._STEP_CALLS)
+                assert tuple(n for n, _ in calls) == eng._STEP_CALLS[0 if pair else 1]
                 assert eng._same(cand, calls), (epoch, bi)
                 checked += 1
             else:

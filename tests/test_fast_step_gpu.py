@@ -50,3 +50,49 @@ def test_fast_step_bit_identical(gpu, cd, opt, sparsity):
     assert h_f == h_g and all(np.isfinite(v).all() and v[0] > 0 for h in h_f for v in h.values())
     for a, b in zip(w_f + s_f + sh_f, w_g + s_g + sh_g):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
+
+
+def _run_pair(pair, cd, opt, shape):
+    import torch
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B = shape
+    data = dataset(rows=rows, cols=cols, nnz=nnz)
+    np.random.seed(8)
+    rd = data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split", rng="numpy")
+    om = omni_model(1, 500 if cd != "float32" else 200, data.num_cols, B, dense_activation="sigmoid",
+                    use_causal_info=False, dropout_probability=0.2, compute_dtype=cd, seed=5)
+    m = om.model
+    mk = {"adagrad": lambda: O.Adagrad(lr=0.01, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=0.001),
+          "adam": lambda: O.Adam(lr=0.001)}[opt]
+    m.compile(mk(), "mean_squared_error", metrics=["mae"])
+    eng = om.engine
+    eng.pair_dw = pair
+    gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    h = m.fit_generator(gen, min(6, gen.num_batches - 1), epochs=1, verbose=0).history
+    torch.cuda.synchronize()
+    # the pair launch's producer count (the decoder clears it before every launch): the pair ran on weights of
+    # more than 170 row tiles (smaller ones keep two launches)
+    ran = eng.pair_sync.cpu().tolist() == [(eng.Bp + 3) // 4, 0]
+    assert ran == (pair and eng.Np // 128 > 170) and eng.pair_sync[1].item() == 0
+    st = [t.cpu().numpy().copy() for sw, sb in eng.slots for t in sw + sb if t is not None]
+    sh = [t.float().cpu().numpy() for t in eng.Wsh if t is not None]
+    return h, m.get_weights(), st, sh, eng._rtag_live
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd,opt,shape", [
+    ("float16", "adagrad", (2000, 40000, 120000, 256)),   # sparse weight rows: live-row records, 12 parts
+    ("bfloat16", "adagrad", (1000, 22000, 500000, 256)),  # ~5 entries per weight row: LONG, records
+    ("float32", "rmsprop", (1200, 30000, 150000, 128)),
+    ("float16", "adam", (2000, 40000, 120000, 256)),
+    ("bfloat16", "adagrad", (1500, 3000, 120000, 256))])  # small dense weight: two launches (no records)
+def test_pair_launch_bit_identical(gpu, cd, opt, shape):
+    """ocf_gemm_pair (dW_out + dW_in in one launch, dW_in's workgroups waiting in the kernel for the row
+    reduction) against the two ocf_gemm launches: identical history, weights, slots and shadows"""
+    a = _run_pair(True, cd, opt, shape)
+    b = _run_pair(False, cd, opt, shape)
+    assert a[0] == b[0] and a[4] == b[4]
+    for x, y in zip(a[1] + a[2] + a[3], b[1] + b[2] + b[3]):
+        assert np.array_equal(x, y), float(np.abs(x - y).max())
