@@ -477,6 +477,58 @@ int ocf_recip_keep(OcfRecipKeepArgs* args, void* stream);
 int ocf_mt_host_random_sample(uint32_t* key, int32_t* pos, int64_t n, double* out);
 int ocf_mt_host_jump(const uint32_t* key_in, int64_t n_blocks, uint32_t* key_out);
 
+/*
+ * Model ABI: one omni_model (/root/reference/model.py:43-99) trained by five calls per step,
+ *   ocf_forward -> ocf_masked_mse -> ocf_backward -> ocf_opt_step (per parameter)
+ * the Keras train_on_batch that fit_generator runs (train.py:157) split at the points a binding drives:
+ * forward (model.py:64-86), the masked MSE and its per-row sums (train.py:49, 102-121), the backward pass to
+ * raw fp32 gradients, and the elementwise Keras update (train.py:50-51).  Parameters and gradients are
+ * caller-owned fp32 device arrays in the padded Keras layout: W[i] is rows[i] x cols[i] (ocf_model_dims:
+ * layer 0 has k_blocks * roundup(N, 128) rows -- input block j's column n at row j * roundup(N, 128) + n --,
+ * hidden widths and N rounded up to 128), b[i] has cols[i] elements, padding zero.  A context holds only
+ * the per-batch activations / dropout masks / split-K slabs of up to max_batch rows (allocated by
+ * ocf_ctx_create, the only call that allocates or synchronises).  Batches are the reference's dense data_gen
+ * arrays (data_reader.py:354-361): k_blocks fp32 [B][N] input blocks (inputs, then the mask to feed /
+ * missing-data mask, model.py:47-56 concatenate), the output mask and the targets.
+ */
+#define OCF_MAX_HIDDEN 8
+typedef struct OcfModelDesc {
+  int n_hidden;              /* hidden layers, 1..OCF_MAX_HIDDEN (model.py:64 layers)                    */
+  int N;                     /* output width (items or users, data_reader.py:24-28)                     */
+  int k_blocks;              /* input blocks 1..3 (1 + use_causal_info + 'both', model.py:47-56)        */
+  int hidden[OCF_MAX_HIDDEN];
+  int act;                   /* OCF_ACTV_* of the hidden layers (train.py:52 'sigmoid')                  */
+  float dropout;             /* model.py:70 Dropout rate, 0 = none                                       */
+  int compute_dtype;         /* OCF_DT_F32 (exact fp32) / OCF_DT_F16 / OCF_DT_BF16 MFMA operands          */
+  int max_batch;             /* batch rows per call, at most                                             */
+  uint64_t seed;             /* dropout mask stream (Philox; step s draws stream 16 s + layer)           */
+  float* W[OCF_MAX_HIDDEN + 1];
+  float* b[OCF_MAX_HIDDEN + 1];
+} OcfModelDesc;
+typedef struct OcfCtx OcfCtx;
+
+/* padded shape of every W[i] (n_hidden + 1 entries each) */
+int ocf_model_dims(const OcfModelDesc* desc, int64_t* rows, int64_t* cols);
+int ocf_ctx_create(const OcfModelDesc* desc, OcfCtx** ctx);
+int ocf_ctx_destroy(OcfCtx* ctx);
+/* ocf_forward -- pred[b][n] = out_mask[b][n] * (h_L[b] . W_L[:, n] + b_L[n]) for b < B, n < N (model.py:81-86;
+ * out_mask nullable = unmasked).  training: dropout with the masks of step `step` (else none); masks_out
+ * (nullable array of n_hidden nullable device pointers): each layer's keep flags as u8 [B][hidden[i]]. */
+int ocf_forward(OcfCtx* ctx, const float* const* inputs, int64_t ld_in, int B, int training, uint64_t step,
+                const float* out_mask, int64_t ld_mask, float* pred, int64_t ld_pred, uint8_t* const* masks_out,
+                void* stream);
+/* ocf_masked_mse -- the Keras loss on the masked prediction (train.py:49): e = pred - T over [B][N];
+ * out_stats (4 + 3 B floats): {sum e^2, sum |e|, count_nonzero(T + pred), loss = sum e^2 / (B N)}, then the
+ * per-row sums e^2 [B], |e| [B], count_nonzero [B] (train.py:102-121's batch metrics); out_grad (nullable)
+ * [B][ld_grad] = e * out_mask (out_mask nullable = 1): the loss gradient with respect to the unmasked output
+ * divided by gscale = 2 / (B N) -- kept unscaled so 16-bit operands do not underflow. */
+int ocf_masked_mse(const float* pred, const float* T, const float* out_mask, int64_t ld, int B, int N,
+                   float* out_grad, int64_t ld_grad, float* out_stats, void* stream);
+/* ocf_backward -- the gradients of the last ocf_forward (same B) from out_grad: gW[i] / gb[i] (shapes of
+ * W[i] / b[i]) = gscale * the backward pass of model.py:64-86 (dropout masks of that forward). */
+int ocf_backward(OcfCtx* ctx, const float* grad, int64_t ld_grad, int B, float gscale, float* const* gW,
+                 float* const* gb, void* stream);
+
 /* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on
  *               [K][M] x [K][N] operands with 16-bit compute run on the persistent role-split kernel

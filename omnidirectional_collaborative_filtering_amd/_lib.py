@@ -147,6 +147,17 @@ class OcfRecipKeepArgs(ctypes.Structure):
     ]
 
 
+MAX_HIDDEN = 8                 # ocf.h OCF_MAX_HIDDEN
+
+
+class OcfModelDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_hidden", I32), ("N", I32), ("k_blocks", I32), ("hidden", I32 * MAX_HIDDEN), ("act", I32),
+        ("dropout", F32), ("compute_dtype", I32), ("max_batch", I32), ("seed", U64),
+        ("W", P * (MAX_HIDDEN + 1)), ("b", P * (MAX_HIDDEN + 1)),
+    ]
+
+
 # every symbol include/ocf.h declares, with its ctypes signature
 SIGNATURES = {
     "ocf_scatter_batch": (I32, [ctypes.POINTER(OcfScatterArgs), P]),
@@ -174,6 +185,12 @@ SIGNATURES = {
     "ocf_recip_keep": (I32, [ctypes.POINTER(OcfRecipKeepArgs), P]),
     "ocf_mt_host_random_sample": (I32, [P, P, I64, P]),
     "ocf_mt_host_jump": (I32, [P, I64, P]),
+    "ocf_model_dims": (I32, [ctypes.POINTER(OcfModelDesc), P, P]),
+    "ocf_ctx_create": (I32, [ctypes.POINTER(OcfModelDesc), ctypes.POINTER(P)]),
+    "ocf_ctx_destroy": (I32, [P]),
+    "ocf_forward": (I32, [P, P, I64, I32, I32, U64, P, I64, P, I64, P, P]),
+    "ocf_masked_mse": (I32, [P, P, P, I64, I32, I32, P, I64, P, P]),
+    "ocf_backward": (I32, [P, P, I64, I32, F32, P, P, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),

@@ -65,6 +65,8 @@ STRUCTS = {
                                                        "ebase", "cnt", "row_ptr", "row_ent", "live"]),
     "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
                                                        "xval", "tflag"]),
+    "OcfModelDesc": (_lib.OcfModelDesc, ["n_hidden", "N", "k_blocks", "hidden", "act", "dropout", "compute_dtype",
+                                         "max_batch", "seed", "W", "b"]),
     "OcfOptStepArgs": (_lib.OcfOptStepArgs, ["p", "g", "g_dtype", "s1", "s2", "n", "opt", "shadow", "shadow_dtype"]),
     "OcfRecipKeepArgs": (_lib.OcfRecipKeepArgs, ["key", "pos", "nb", "B", "n_entries", "boff", "ebase", "s0", "s1",
                                                  "keep", "doubles", "workspace", "workspace_bytes"]),
@@ -102,3 +104,37 @@ def test_errors_are_reported_not_silent():
     a.A = a.B = 1
     with pytest.raises(_lib.OcfError, match="multiples of 128"):
         _lib.call("ocf_gemm", a, None)
+
+
+def test_model_abi_is_plain_c(tmp_path):
+    """the model ABI compiles and links from C (gcc, no C++ / HIP headers): what a cgo / JNI / N-API binding
+    or a C training loop includes"""
+    src = tmp_path / "drive.c"
+    src.write_text(r'''
+#include "ocf.h"
+int drive(float** W, float** b, float** gW, float** gb, const float* x, const float* mo, const float* t,
+          float* pred, float* grad, float* stats, float* slots[][2], int64_t* sizes, void* stream) {
+  OcfModelDesc d = {0};
+  d.n_hidden = 1; d.N = 333; d.k_blocks = 1; d.hidden[0] = 100; d.act = OCF_ACTV_SIGMOID; d.dropout = 0.2f;
+  d.compute_dtype = OCF_DT_F16; d.max_batch = 128; d.seed = 1;
+  for (int i = 0; i < 2; ++i) { d.W[i] = W[i]; d.b[i] = b[i]; }
+  OcfCtx* ctx = 0;
+  if (ocf_ctx_create(&d, &ctx)) return 1;
+  const float* in[1] = {x};
+  OcfOptParams op = {OCF_OPTK_ADAGRAD, 0.005f, 1e-8f, 0.f, 0.f, 0.f, 1.f};
+  int rc = ocf_forward(ctx, in, 333, 128, 1, 0, mo, 333, pred, 333, 0, stream)
+        || ocf_masked_mse(pred, t, mo, 333, 128, 333, grad, 333, stats, stream)
+        || ocf_backward(ctx, grad, 333, 128, 2.f / (128 * 333), gW, gb, stream);
+  for (int i = 0; i < 2 && !rc; ++i)
+    rc = ocf_opt_step(W[i], gW[i], slots[2 * i][0], 0, sizes[2 * i], &op, stream)
+      || ocf_opt_step(b[i], gb[i], slots[2 * i + 1][0], 0, sizes[2 * i + 1], &op, stream);
+  ocf_ctx_destroy(ctx);
+  return rc;
+}
+int main(void) { return 0; }
+''')
+    exe = tmp_path / "drive"
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(src),
+                        "-o", str(exe), _lib.LIB_PATH, "-Wl,--unresolved-symbols=ignore-in-shared-libs"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
