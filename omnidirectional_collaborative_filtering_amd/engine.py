@@ -1051,9 +1051,19 @@ class Engine:
                                 self.Hp[i], gscale, grads_out, op)
             self._grad_ready(i, grads_out)
             db_last, parts_last = self.db_h[i - 1], parts_next
-        self._bias_update(0, db_last, parts_last, self.Hp[0], self.Hp[0], grads_out, op)
+        jobs_in = None
+        if fused and L == 1 and self.comm is not None and self.fold_jobs and self.trainable[0]:
+            # feature parallelism: the hidden-bias update from the δh partial rows rides in the input layer's
+            # launch as a job (the same sums) instead of a kernel ahead of it on the critical path (8-way rank:
+            # 512 partial rows, 40 us as a separate launch)
+            sb = self.slots[0][1]
+            jobs_in = dict(jb_part=db_last, jb_parts=parts_last, jb_ld=HpL, jb_n=HpL, jb_p=self.b[0], jb_s1=sb[0],
+                           jb_s2=sb[1], jb_op=self._bias_op)
+        else:
+            self._bias_update(0, db_last, parts_last, self.Hp[0], self.Hp[0], grads_out, op)
         with self.phase("dW_in"):
-            self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op)
+            self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out, op,
+                                       jobs=jobs_in)
         self._grad_ready(0, grads_out)
         if fused:
             self.opt.iterations += 1
