@@ -602,6 +602,12 @@ def main():
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
                      if epoch_lists else "per step (ocf_row_lists)" if eng.sparse_dw else "n/a",
     }
+    if world > 1 and fp and args.config == "ml20m" and B == 256:
+        # weak scaling grows the global batch with the ranks; the same global batch on ONE GPU (measured on
+        # this build, row-stream path) is the reference point for the speed-up, not the B = 256 line
+        line["same_global_batch_1gpu"] = {
+            "global_batch": B * world, "ms_per_step": {2: 0.636, 4: 0.843, 8: 1.1188}.get(world),
+            "source": "profiles/r03_slab_rejected/b2048_S0.json (B=2,048); DESIGN.md §5 batch sweep (512, 1,024)"}
     if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
         line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)
     if world == 1 and args.epoch and not args.emulate_shards:
