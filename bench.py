@@ -3,10 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-One step = one pass of the hot path over one batch resident in HBM: K1 scatter of B item-rows of
-the rating CSR -> encoder GEMM (split-K) + bias/sigmoid/dropout -> decoder GEMM with the fused
-masked-MSE epilogue -> backward GEMMs -> Adagrad (fused into the weight-gradient GEMMs at N=1;
-all-reduce of the gradients + elementwise Adagrad at N>1).  Configuration = train.py's
+One step = one pass of the hot path over one batch resident in HBM: the epoch's batch
+preparation for the timed batches, the row-gather encoder, the row-gather decoder with the hidden layer's
+epilogue and the fused masked MSE, and both weight updates (row-stream dW + Adagrad, one launch) -- at N>1
+each rank runs its column shard of the same step with two [B*G, H] all-reduces (feature layout, default)
+or the data-parallel step (--parallel dp).  Configuration = train.py's
 (sigmoid, dropout 0.2, Adagrad lr 0.005, pass-through training, data_sparsity [1,1]) at
 BASELINE.json configs[2]: ML-20M I-AutoRec (26,744 item rows x 138,493 users), 500 hidden units,
 batch 256, fp16 MFMA with fp32 accumulation.  Data: synthetic, ML-20M density, seeded.
@@ -555,7 +556,9 @@ def main():
                 "kernel_mean_us": round(ms * 1e3, 1), "kernel_samples": dom_timed["n"],
                 "alg_bytes_per_launch": int(alg[dom]), "live_row_frac": round(live, 4)}
         # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
-        pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic.json")))
+        # the latest round's PMC summary that measured this kernel (r03_, r03b_, r03c_ ... sort in round order)
+        pmcs = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")))
+                if dom in json.load(open(f))]
         # (measured on the default headline workload only: ML-20M, B = 256, f16, one GPU)
         if pmcs and world == 1 and args.config == "ml20m" and args.batch == 256 and args.dtype == "float16" \
                 and not args.emulate_shards:
