@@ -63,7 +63,11 @@ class ModelABI:
     def __del__(self):
         ctx = getattr(self, "ctx", None)
         if ctx:
-            _lib.load().ocf_ctx_destroy(ctx)
+            try:
+                _lib.load().ocf_ctx_destroy(ctx)
+            except Exception:          # interpreter shutdown: the module globals may already be gone
+                pass
+            self.ctx = None
 
     # Keras-layout weights in / out (padding stripped; layer 0's block j at rows j * Np ...)
     def _rows0(self):
