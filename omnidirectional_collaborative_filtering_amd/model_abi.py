@@ -111,6 +111,10 @@ class ModelABI:
 
     def masked_mse(self, pred, targets, out_mask, B):
         s = torch.cuda.current_stream().cuda_stream
+        # ocf_masked_mse takes one row stride for pred / targets / mask: [B][N] contiguous (data_gen's arrays are
+        # views with a padded stride)
+        targets = targets if targets.stride(0) == self.N else targets.contiguous()
+        out_mask = out_mask if out_mask is None or out_mask.stride(0) == self.N else out_mask.contiguous()
         self.grad = torch.zeros(B, self.N, device=self.dev)
         self.stats = torch.zeros(4 + 3 * B, device=self.dev)
         call("ocf_masked_mse", ptr(pred), ptr(targets), ptr(out_mask), self.N, B, self.N, ptr(self.grad), self.N,
