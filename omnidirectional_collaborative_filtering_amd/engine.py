@@ -376,9 +376,19 @@ class Engine:
         return Engine._Phase(self, name)
 
     # ---------------------------------------------------------------- side stream
+    # one reusable event per direction: a stream wait takes the event's latest record at the time of the wait
+    # call, so re-recording it for the next fork / join is safe (creating an event per fork cost ~15 us of
+    # host time, twice per feature-parallel step)
+    def _sync_event(self, name):
+        ev = getattr(self, name, None)
+        if ev is None:
+            ev = torch.cuda.Event()          # timing disabled (the default): a plain sync event
+            setattr(self, name, ev)
+        return ev
+
     def _fork(self):
         """side stream waits for everything issued so far on the current stream"""
-        ev = torch.cuda.Event()
+        ev = self._sync_event("_ev_fork")
         ev.record()
         self.side.wait_event(ev)
         self._side_busy = True
@@ -386,7 +396,7 @@ class Engine:
     def _join(self):
         """current stream waits for the side stream"""
         if self._side_busy:
-            ev = torch.cuda.Event()
+            ev = self._sync_event("_ev_join")
             ev.record(self.side)
             torch.cuda.current_stream().wait_event(ev)
             self._side_busy = False
