@@ -138,3 +138,25 @@ int main(void) { return 0; }
                         "-o", str(exe), _lib.LIB_PATH, "-Wl,--unresolved-symbols=ignore-in-shared-libs"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_model_dims_and_descriptor_checks():
+    """ocf_model_dims (host-only): the padded Keras-layout shapes, and the descriptor checks the model ABI
+    applies before touching the device"""
+    d = _lib.OcfModelDesc()
+    d.n_hidden, d.N, d.k_blocks = 2, 333, 2
+    d.hidden[0], d.hidden[1] = 100, 130
+    d.act, d.dropout, d.compute_dtype, d.max_batch = 1, 0.2, 1, 128
+    rows, cols = (ctypes.c_int64 * 3)(), (ctypes.c_int64 * 3)()
+    _lib.call("ocf_model_dims", d, rows, cols)
+    assert list(rows) == [2 * 384, 128, 256] and list(cols) == [128, 256, 384]
+    for field, bad in (("n_hidden", 0), ("n_hidden", 9), ("k_blocks", 4), ("dropout", 1.0), ("compute_dtype", 7),
+                       ("max_batch", 0), ("act", 9)):
+        e = _lib.OcfModelDesc.from_buffer_copy(d)
+        setattr(e, field, bad)
+        with pytest.raises(_lib.OcfError):
+            _lib.call("ocf_model_dims", e, rows, cols)
+    # a context needs every parameter pointer
+    ctx = ctypes.c_void_p()
+    with pytest.raises(_lib.OcfError, match="null parameter"):
+        _lib.call("ocf_ctx_create", d, ctypes.byref(ctx))
