@@ -10,7 +10,8 @@ Tolerances (stated here, used by every parity test):
     which amplifies the operand rounding of g by G_i / |g_i| (G = the gradient's magnitude sum,
     OmniOracle.grad_magnitudes).  Elements with a well-conditioned gradient must match tightly;
     only elements whose gradient is within rounding distance of zero may differ by up to 2 lr per
-    step (the update's sign there is not determined by 16-bit operands).
+    step (the update's sign there is not determined by 16-bit operands); and the bulk must sit far
+    inside: 99th / 99.9th percentile errors within 0.02 / 0.15 of lr * steps.
 """
 from __future__ import annotations
 
@@ -349,7 +350,14 @@ def assert_low_precision(res, tol):
         assert ratio <= 1.0, ("param %d" % j, float(err.max()), int((err > lim).sum()))
         errs.append(err.ravel())
         envs.append(np.asarray(e).ravel())
-    _record_envelope_stats(res, np.concatenate(errs), np.concatenate(envs))
+    err, env = np.concatenate(errs), np.concatenate(envs)
+    _record_envelope_stats(res, err, env)
+    # the envelope bounds every element; the bulk must sit far inside it: in units of lr * steps, the 99th /
+    # 99.9th percentile errors within 0.02 / 0.15 (measured: f16 <= 4.5e-4 / 5.4e-3, bf16 <= 3.0e-3 / 4.6e-2,
+    # profiles/r03c_envelope_stats.jsonl; the runs are seeded and the kernels deterministic)
+    unit = float(getattr(res, "lr", None) or 0.005) * max(1, len(res.step_losses_o))
+    q99, q999 = np.quantile(err, [0.99, 0.999]) / unit
+    assert q99 <= 0.02 and q999 <= 0.15, ("error quantiles / (lr * steps)", float(q99), float(q999))
     return worst
 
 
