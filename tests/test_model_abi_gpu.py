@@ -13,13 +13,13 @@ from tests import parity
 pytestmark = pytest.mark.gpu
 
 
-def _run(dtype, opt_name, hidden, act, dropout, causal, steps=3, B=128, seed=3):
+def _run(dtype, opt_name, hidden, act, dropout, causal, steps=3, B=128, seed=3, max_batch=None):
     from omnidirectional_collaborative_filtering_amd.model_abi import ModelABI
     data = parity.dataset()
     N = data.num_cols
     k = 2 if causal else 1
     ora = parity.OmniOracle([k * N] + hidden + [N], activation=act, dropout=dropout or None).init(seed)
-    m = ModelABI(N, hidden, B, k_blocks=k, activation=act, dropout=dropout, compute_dtype=dtype, seed=11,
+    m = ModelABI(N, hidden, max_batch or B, k_blocks=k, activation=act, dropout=dropout, compute_dtype=dtype, seed=11,
                  optimizer=parity.our_opt(opt_name))
     m.set_weights([x.astype(np.float32) for x in ora.params()])
     assert all(np.array_equal(a, b.astype(np.float32)) for a, b in zip(m.get_weights(), ora.params()))
@@ -71,6 +71,11 @@ def _run(dtype, opt_name, hidden, act, dropout, causal, steps=3, B=128, seed=3):
 ])
 def test_model_abi_fp32_vs_oracle(opt_name, hidden, act, dropout, causal):
     _run("float32", opt_name, hidden, act, dropout, causal)
+
+
+def test_model_abi_batch_below_max():
+    """B = 100 rows in a context sized for 256 (padded rows of the activations must not leak into any gradient)"""
+    _run("float32", "adagrad", [100, 60], "tanh", 0.2, False, B=100, max_batch=256)
 
 
 @pytest.mark.parametrize("dtype", ["float16", "bfloat16"])
