@@ -37,6 +37,8 @@ AUX_FEED = {None: 0, "dropout": 1, "both": 1, "causal": 2, "zeros": 3}
 # (more workgroups, each a few dependent steps), large batches the long ones (fewer partial sums)
 GATHER_CHUNK = 256
 GATHER_CHUNK_SMALL = 64
+GATHER_CHUNK_MID = 96
+GATHER_CHUNK_MID_MIN_CHUNKS = 512
 GATHER_BIG = 100_000
 ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the library takes up to 65,535)
 ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
@@ -257,6 +259,11 @@ class BatchGenerator(object):
         if chunk is None:
             per_batch = L.sum() / max(nb, 1)
             chunk = GATHER_CHUNK if per_batch >= GATHER_BIG else GATHER_CHUNK_SMALL
+            # mid-size batches (ML-1M I: ~55 K entries) keep >= 512 chunks at 96 entries -- fewer redundant hidden
+            # epilogues in the decoder: ML-1M 0.093 -> 0.089 ms/step; ML-1M U (~34 K) and ML-100K (~12 K) stay
+            # at 64, where 96 was neutral / 5 % slower (tools/exp_chunk_small.sh, profiles/r03c_chunk_small/; same-box A/B of the rule: tools/exp_chunk_ab.sh, 0.0931 -> 0.0898 ms mean of 3, profiles/r03c_chunk_mid/)
+            if chunk == GATHER_CHUNK_SMALL and per_batch >= GATHER_CHUNK_MID_MIN_CHUNKS * GATHER_CHUNK_MID:
+                chunk = GATHER_CHUNK_MID
         nc = (L + chunk - 1) // chunk
         row_cptr = np.zeros((nb, B + 1), dtype=np.int32)
         np.cumsum(nc.reshape(nb, B), axis=1, out=row_cptr[:, 1:])
