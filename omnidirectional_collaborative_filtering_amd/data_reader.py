@@ -261,7 +261,8 @@ class BatchGenerator(object):
             chunk = GATHER_CHUNK if per_batch >= GATHER_BIG else GATHER_CHUNK_SMALL
             # mid-size batches (ML-1M I: ~55 K entries) keep >= 512 chunks at 96 entries -- fewer redundant hidden
             # epilogues in the decoder: ML-1M 0.093 -> 0.089 ms/step; ML-1M U (~34 K) and ML-100K (~12 K) stay
-            # at 64, where 96 was neutral / 5 % slower (tools/exp_chunk_small.sh, profiles/r03c_chunk_small/; same-box A/B of the rule: tools/exp_chunk_ab.sh, 0.0931 -> 0.0898 ms mean of 3, profiles/r03c_chunk_mid/)
+            # at 64, where 96 was neutral / 5 % slower (tools/exp_chunk_small.sh, profiles/r03c_chunk_small/;
+            # same-box A/B of the rule: tools/exp_chunk_ab.sh, 0.0931 -> 0.0898 ms, profiles/r03c_chunk_mid/)
             if chunk == GATHER_CHUNK_SMALL and per_batch >= GATHER_CHUNK_MID_MIN_CHUNKS * GATHER_CHUNK_MID:
                 chunk = GATHER_CHUNK_MID
         nc = (L + chunk - 1) // chunk
