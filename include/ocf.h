@@ -158,8 +158,8 @@ typedef struct OcfGatherArgs {
    * arithmetic; the first chunk of each batch row also stores a_out, mask_out and h (h is then written) */
   const float* enc_part; const int32_t* enc_cptr; const float* bias_h; int act; float keep;
   uint64_t seed, stream; float* a_out; uint8_t* mask_out; int m_real, n_real;
-  /* decoder, optional: a word the launch sets to zero (ocf_gemm_pair's sync word for the step's pair launch
-   * that follows: the engine lets the decoder clear it instead of a separate memset) */
+  /* decoder, optional: a device word the launch sets to zero (a caller's flag cleared for free; the
+   * engine no longer needs it: ocf_gemm_pair's counter never needs clearing) */
   uint64_t* zero_word;
 } OcfGatherArgs;
 
@@ -300,11 +300,27 @@ int ocf_gemm(const OcfGemmArgs* args, void* stream);
  * and job inputs that reduction writes: train.py:50-51 for both kernels).  When both take the row-stream
  * kernel with the same instance they run as ONE launch: b's workgroups wait, in the kernel, for a's
  * row-reduction workgroups (agent-scope release / acquire on sync[0]), so the two row streams run back to
- * back without a kernel boundary.  sync: device uint64[2]; sync[0] must be zero when the launch starts
- * (the caller clears it: the engine's decoder gather does, OcfGatherArgs zero_word); NULL = two launches.
- * Results are identical to the two ocf_gemm calls.
+ * back without a kernel boundary.  sync (NULL = two launches): the hand-off counter below.  Results are
+ * identical to the two ocf_gemm calls.
+ *
+ * The counter only grows, so nothing is reset between launches: word is a device uint64 that is zero
+ * when first passed (one hipMemset after allocating it) and that only the library writes afterwards;
+ * count is its host-side twin (zero with it): the producer workgroups counted on *word before this
+ * launch.  A pair launch makes its input-layer workgroups wait for *word >= count + n_prod and
+ * advances count by n_prod (the number of row-reduction workgroups); a call that falls back to two
+ * launches leaves both unchanged.  The wait is bounded (ocf_set_tuning "pair_wait_polls"): a workgroup
+ * that gives up skips its update and the next ocf_* call fails with OCF_ASYNC_PAIR_WAIT's message
+ * (a word written by someone else, or a count that does not match it).
  */
-int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, void* sync, void* stream);
+typedef struct OcfPairSync {
+  uint64_t* word;      /* device */
+  uint64_t count;      /* host, in/out */
+} OcfPairSync;
+int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, OcfPairSync* sync, void* stream);
+
+/* codes of the asynchronous error word (kernels that detect a fault without stopping; reported by the
+ * next entry point through its status and ocf_last_error()) */
+#define OCF_ASYNC_PAIR_WAIT 1
 
 /*
  * ocf_train_step_rows -- one whole single-GPU training step of a one-hidden-layer model on a sparse
@@ -329,8 +345,9 @@ typedef struct OcfRowStepArgs {
   /* (nullable) hipEvent_t recorded on `stream` before / after each launch: encoder, decoder, dW_out, dW_in
    * (the per-kernel timing bench.py reports; recorded only where set) */
   void* ev[8];
-  /* (nullable) ocf_gemm_pair's sync words: dW_out and dW_in as one launch (events 4 and 7 bracket it) */
-  void* pair_sync;
+  /* (nullable) ocf_gemm_pair's hand-off counter: dW_out and dW_in as one launch (events 4 and 7 bracket
+   * it); its count advances with every pair launch */
+  OcfPairSync* pair_sync;
 } OcfRowStepArgs;
 int ocf_train_step_rows(const OcfRowStepArgs* args, void* stream);
 

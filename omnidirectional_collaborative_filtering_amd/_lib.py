@@ -119,6 +119,14 @@ class OcfGemmArgs(ctypes.Structure):
     ]
 
 
+class OcfPairSync(ctypes.Structure):
+    """ocf.h OcfPairSync: ocf_gemm_pair's hand-off counter (device word + its host-side running count)"""
+    _fields_ = [("word", P), ("count", U64)]
+
+
+ASYNC_PAIR_WAIT = 1            # ocf.h OCF_ASYNC_PAIR_WAIT
+
+
 class OcfRowStepArgs(ctypes.Structure):
     _fields_ = [("enc", OcfGatherArgs), ("dec", OcfGatherArgs), ("dw_out", OcfGemmArgs), ("dw_in", OcfGemmArgs),
                 ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8), ("pair_sync", P)]
@@ -164,7 +172,7 @@ SIGNATURES = {
     "ocf_dense_targets": (I32, [P, P, I64, I32, I32, I32, P, P, P, P, P, P, P, P]),
     "ocf_pack_input": (I32, [P, P, P, I64, I32, I32, P, I32, I64, I64, I32, P, P]),
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
-    "ocf_gemm_pair": (I32, [ctypes.POINTER(OcfGemmArgs), ctypes.POINTER(OcfGemmArgs), P, P]),
+    "ocf_gemm_pair": (I32, [ctypes.POINTER(OcfGemmArgs), ctypes.POINTER(OcfGemmArgs), P, P]),   # P: OcfPairSync*
     "ocf_train_step_rows": (I32, [ctypes.POINTER(OcfRowStepArgs), P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),

@@ -1,5 +1,7 @@
 // Split-K reductions fused with the layer epilogues, elementwise optimizers, stats reduction,
 // and the library's error state.
+#include <cstring>
+#include <mutex>
 #include <string>
 #include <type_traits>
 
@@ -10,6 +12,43 @@ namespace ocf {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+namespace {
+std::mutex g_async_mu;
+uint32_t* g_async_host = nullptr;   // hipHostMalloc'd, coherent: kernels store to it, the host polls it
+uint32_t* g_async_dev = nullptr;
+const char* async_error_text(uint32_t code) {
+  switch (code) {
+    case OCF_ASYNC_PAIR_WAIT:
+      return "ocf_gemm_pair: an input-layer workgroup gave up waiting for the row reduction (sync word behind its "
+             "target: the word was written by someone else, or the count passed does not match it) and skipped "
+             "its update; the weights of that launch are not a valid step";
+    default:
+      return "asynchronous kernel error";
+  }
+}
+}  // namespace
+
+uint32_t* async_error_word() {
+  std::lock_guard<std::mutex> lk(g_async_mu);
+  if (!g_async_dev) {
+    void* h = nullptr;
+    OCF_HIP(hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+    std::memset(h, 0, 64);
+    void* d = nullptr;
+    OCF_HIP(hipHostGetDevicePointer(&d, h, 0));
+    g_async_host = static_cast<uint32_t*>(h);
+    g_async_dev = static_cast<uint32_t*>(d);
+  }
+  return g_async_dev;
+}
+
+void check_async_errors() {
+  uint32_t* h = g_async_host;
+  if (!h) return;
+  const uint32_t code = __atomic_exchange_n(h, 0u, __ATOMIC_ACQ_REL);
+  if (code) throw std::runtime_error(std::string("error from an earlier launch: ") + async_error_text(code));
+}
 
 // Split-K reductions: grid (N/64, M/4); 256 threads = 64 columns x 4 rows, one output element per
 // thread, slabs summed in a fixed order (4 independent partial sums for memory-level parallelism).

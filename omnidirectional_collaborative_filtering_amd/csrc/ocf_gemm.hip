@@ -54,6 +54,7 @@ int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (
 int g_optim_ws = 1;      // role-split kernel for dense-A EPI_OPTIM (ocf_set_tuning "optim_ws")
 int g_rows_long = -1;   // row-stream LONG variant: -1 by entries per row, 0 never, 1 always ("rows_long")
 int g_rows_small_waves = 8192;   // row-stream kernel: 32 parts per tile below this many waves at 12 ("rows_small_waves")
+int g_pair_wait_polls = 1 << 22;   // ocf_gemm_pair's bounded wait (ocf_set_tuning "pair_wait_polls"): seconds
 int g_optim_ws_max_k = 512;   // K = 512 (2-way feature parallel): 0.453 vs 0.509 ms/step on the generic kernel; K = 1,024: 0.42 vs 0.38
 bool optim_ws_on() { return g_optim_ws != 0; }
 
@@ -394,6 +395,10 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   } else if (k == "optim_ws") {
     if (previous) *previous = optim_ws_on() ? 1 : 0;
     g_optim_ws = value ? 1 : 0;
+  } else if (k == "pair_wait_polls") {    // ocf_gemm_pair's bounded hand-off wait (tests shorten it)
+    if (previous) *previous = g_pair_wait_polls;
+    OCF_CHECK(value > 0, "ocf_set_tuning: pair_wait_polls > 0");
+    g_pair_wait_polls = value;
   } else if (k == "optim_ws_max_k") {
     if (previous) *previous = g_optim_ws_max_k;
     g_optim_ws_max_k = value;
@@ -441,7 +446,7 @@ bool rows_pair_ok(const OcfGemmArgs& g) {
          (!g.p_shadow || g.compute_dtype != OCF_F32) && (!g.row_live || (g.opt.kind == OCF_OPT_ADAGRAD && g.opt.l2 == 0.f));
 }
 template <typename CT>
-bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, unsigned long long* sync, hipStream_t s) {
+bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& sync, hipStream_t s) {
   if (!g_optim_rows || !rows_pair_ok(a) || !rows_pair_ok(b)) return false;
   RowsLaunch A, B;
   if (!rows_setup(a, optim_params(a), A) || !rows_setup(b, optim_params(b), B)) return false;
@@ -451,11 +456,15 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, unsigned long 
   // ML-100K 25.8 vs 21.7; ML-20M 303 vs 307: tools/step_parts_probe.py)
   if (A.small) return false;
   RsPair ps;
-  ps.sync = sync;
+  ps.word = reinterpret_cast<unsigned long long*>(sync.word);
   ps.n_a = A.grid;
   ps.n_prod = A.jb.jr_on ? (A.jb.jr.Bp + 3) / 4 : 0;   // the job-only workgroups holding the row reduction
+  ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
+  ps.err = async_error_word();
+  ps.max_polls = g_pair_wait_polls;
   rows_dispatch<CT>(A, RowsPair{A, B, ps, s});
   OCF_HIP(hipGetLastError());
+  sync.count = ps.want;
   return true;
 }
 }  // namespace
@@ -474,19 +483,19 @@ extern "C" int ocf_gemm(const OcfGemmArgs* args, void* stream) {
   OCF_TRY_END
 }
 
-extern "C" int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, void* sync, void* stream) {
+extern "C" int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, OcfPairSync* sync, void* stream) {
   OCF_TRY_BEGIN
   OCF_CHECK(a && b, "ocf_gemm_pair: null arguments");
+  OCF_CHECK(!sync || sync->word, "ocf_gemm_pair: OcfPairSync without a device word");
   check_gemm(*a);
   check_gemm(*b);
   hipStream_t s = (hipStream_t)stream;
-  auto* sy = reinterpret_cast<unsigned long long*>(sync);
   bool done = false;
-  if (sy && a->compute_dtype == b->compute_dtype) {
+  if (sync && a->compute_dtype == b->compute_dtype) {
     switch (a->compute_dtype) {
-      case OCF_F16: done = launch_rows_pair<_Float16>(*a, *b, sy, s); break;
-      case OCF_BF16: done = launch_rows_pair<__bf16>(*a, *b, sy, s); break;
-      case OCF_F32: done = launch_rows_pair<float>(*a, *b, sy, s); break;
+      case OCF_F16: done = launch_rows_pair<_Float16>(*a, *b, *sync, s); break;
+      case OCF_BF16: done = launch_rows_pair<__bf16>(*a, *b, *sync, s); break;
+      case OCF_F32: done = launch_rows_pair<float>(*a, *b, *sync, s); break;
       default: break;
     }
   }

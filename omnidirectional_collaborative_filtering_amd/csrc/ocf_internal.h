@@ -10,9 +10,13 @@
 namespace ocf {
 using ScatterArgs = OcfScatterArgs;
 void set_error(const std::string& msg);
+// Faults a kernel detects without stopping (ocf_gemm_pair's bounded hand-off wait) are written to a
+// pinned, host-coherent word; every entry point reports a pending one (once) before doing anything.
+uint32_t* async_error_word();        // device-visible address of the word (allocated on first use)
+void check_async_errors();
 }  // namespace ocf
 
-#define OCF_TRY_BEGIN try {
+#define OCF_TRY_BEGIN try { ocf::check_async_errors();
 #define OCF_TRY_END                                       \
   return 0;                                               \
   }                                                       \

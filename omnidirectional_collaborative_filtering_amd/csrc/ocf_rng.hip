@@ -569,10 +569,10 @@ extern "C" int ocf_recip_keep(OcfRecipKeepArgs* a, void* stream) {
     for (int64_t j = 0; j < draws; ++j) a->doubles[j] = to_double(h[2 * j], h[2 * j + 1]);
   }
   uint32_t raw[NW];
-  if (p.bq >= 0) {
-    OCF_HIP(hipMemcpyAsync(raw, fin, NW * 4, hipMemcpyDeviceToHost, s));
-    OCF_HIP(hipStreamSynchronize(s));
-  }
+  if (p.bq >= 0) OCF_HIP(hipMemcpyAsync(raw, fin, NW * 4, hipMemcpyDeviceToHost, s));
+  // always: the keep flags (and the workspace the caller frees next) must be complete when the call
+  // returns, also when every draw fits in the current 624-word block (no end-state copy to wait for)
+  OCF_HIP(hipStreamSynchronize(s));
   end_state(p, a->key, a->pos, raw, a->key, &a->pos);
   OCF_TRY_END
 }

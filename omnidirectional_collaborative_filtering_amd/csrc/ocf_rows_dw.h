@@ -360,15 +360,20 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra
 // layer's.  The input layer's operand B (the hidden delta) and its jobs' inputs (bias-gradient rows,
 // stats rows) are written by the output layer's folded row reduction -- the first n_prod job-only
 // workgroups.  Those publish with an agent-scope release (their XCD's L2 written back) and count in
-// sync[0]; every input-layer workgroup waits for sync[0] == n_prod before it starts (see the wait).  Deadlock-free: workgroups are dispatched in index order, so every
-// producer is resident or done before a consumer can wait, and producers wait on nothing.  The wait is
-// bounded anyway (it never ends a kernel by hanging).  The last consumer to pass resets both counters
-// (sync[1] counts the passed consumers), so the next launch finds them zero.  The two layers' rows then
-// stream back to back without a kernel boundary, and on small weights (about one row per wave, each a
-// chain of dependent loads) their latency chains overlap.
+// *word; every input-layer workgroup waits for *word >= want (= the count before this launch + n_prod)
+// before it starts.  The word only grows -- no launch resets it, so no caller has to clear it between
+// launches (ocf.h OcfPairSync: the host keeps the running count).  Deadlock-free: workgroups are
+// dispatched in index order, so every producer is resident or done before a consumer can wait, and
+// producers wait on nothing.  The wait is bounded: a workgroup that gives up (a word someone else wrote,
+// a count that does not match it) records OCF_ASYNC_PAIR_WAIT in the library's error word and skips
+// its rows instead of updating them from a stale delta; the next library call reports it.  The two
+// layers' rows then stream back to back without a kernel boundary, and on small weights (about one row
+// per wave, each a chain of dependent loads) their latency chains overlap.
 struct RsPair {
-  unsigned long long* sync;   // [0]: completed producer workgroups (zero at the launch)
-  int n_a, n_prod;
+  unsigned long long* word;   // completed producer workgroups, over all launches on this word
+  unsigned long long want;    // the count this launch's consumers wait for
+  uint32_t* err;              // the library's asynchronous error word (host-coherent)
+  int n_a, n_prod, max_polls;
 };
 
 template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
@@ -382,7 +387,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
       // a release per wave made the wait cost ~15 us) publishes them with the count
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.sync, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ps.word, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -393,17 +398,19 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
   // 0.31.  No invalidation is needed: the data the wait guards (the row reduction's outputs) is read in
   // this kernel only after the wait and the kernel start invalidated every L1 / L2 line from before it, so
   // a consumer's caches hold no stale copy -- its reads miss to memory, which the producers' release (L2
-  // write-back) has updated, or hit lines a producer on the same XCD wrote.  sync[0] is zeroed by the
-  // caller before the launch (the engine's decoder gather does it: OcfGatherArgs zero_word).
+  // write-back) has updated, or hit lines a producer on the same XCD wrote.
+  __shared__ int gave_up;
   if (threadIdx.x == 0) {
-    const unsigned long long want = (unsigned long long)ps.n_prod;
-    if (*reinterpret_cast<volatile unsigned long long*>(ps.sync) < want)
-      for (int it = 0; it < (1 << 22); ++it) {
-        if (__hip_atomic_load(ps.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
+    bool ok = *reinterpret_cast<volatile unsigned long long*>(ps.word) >= ps.want;
+    for (int it = 0; !ok && it < ps.max_polls; ++it) {
+      ok = __hip_atomic_load(ps.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ps.want;
+      if (!ok) __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(ps.err, (uint32_t)OCF_ASYNC_PAIR_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    gave_up = ok ? 0 : 1;
   }
   __syncthreads();
+  if (gave_up) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(rb, jb, bx - ps.n_a);
 }

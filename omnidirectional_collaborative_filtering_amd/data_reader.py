@@ -48,6 +48,16 @@ ROWS_DENSE_MAX_COLS = 170 * 128  # the row-stream kernel's small regime (ocf_gem
 _RNG_STREAMS = {}
 
 
+def _h2d(x, dev):
+    """Upload a host array without draining the current stream: a pageable copy makes torch synchronise
+    the stream (every queued training step), so the epoch's tables go through pinned memory (the caching
+    host allocator keeps the pinned block until the copy on the current stream is done)."""
+    t = torch.as_tensor(np.ascontiguousarray(x))
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _rng_stream(dev):
     """one stream per device for ocf_recip_keep (created on first use)"""
     key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
@@ -198,20 +208,23 @@ class BatchGenerator(object):
         a.pos, a.nb, a.B, a.n_entries = int(st[2]), nb, B, E
         a.s0, a.s1 = s0, s1
         keep = None
-        ebase = None
-        if not (s0 >= 1.0 and s1 >= 1.0) and E:
-            keep = torch.empty(E, dtype=torch.uint8, device=dev)
-            ebase = torch.as_tensor(np.concatenate([[0], np.cumsum(boff[:, -1])]).astype(np.int64), device=dev)
-            a.keep, a.boff, a.ebase = ptr(keep), ptr(self.boff_dev), ptr(ebase)
         nbytes = _lib.load().ocf_recip_keep_workspace(nb, B, E, a.pos)
         if nbytes < 0:
             raise _lib.OcfError("ocf_recip_keep_workspace: " + _lib.load().ocf_last_error().decode())
-        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
-        a.workspace, a.workspace_bytes = ptr(ws), int(nbytes)
-        # its own stream (the call synchronises it to hand the state back): the main stream's queued steps
-        # are not waited for
+        # its own stream, with its own copies of the batch offsets (uploaded on it, pinned): the call
+        # synchronises that stream to hand the state back -- and the keep flags / workspace are complete when
+        # it returns --, while the main stream's queued steps are not waited for
         with torch.cuda.stream(_rng_stream(dev)):
+            ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+            a.workspace, a.workspace_bytes = ptr(ws), int(nbytes)
+            if not (s0 >= 1.0 and s1 >= 1.0) and E:
+                keep = torch.empty(E, dtype=torch.uint8, device=dev)
+                boff_r = _h2d(boff, dev)
+                ebase = _h2d(np.concatenate([[0], np.cumsum(boff[:, -1])]).astype(np.int64), dev)
+                a.keep, a.boff, a.ebase = ptr(keep), ptr(boff_r), ptr(ebase)
             _lib.call("ocf_recip_keep", a, cur_stream())
+        if keep is not None and keep.is_cuda:   # allocated on the RNG stream, read on the main stream from here on
+            keep.record_stream(torch.cuda.current_stream(dev))
         np.random.set_state((st[0], np.frombuffer(a.key, dtype=np.uint32).copy(), int(a.pos), st[3], st[4]))
         return keep
 
@@ -230,14 +243,14 @@ class BatchGenerator(object):
         self.rows_host = rows
         self.nnz_full = boff[:, -1].copy()
         self.nnz1 = self.src1.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)   # entries held here
-        self.rows_dev = torch.as_tensor(rows.astype(np.int32), device=r.device)
-        self.boff_dev = torch.as_tensor(boff, device=r.device)
+        self.rows_dev = _h2d(rows.astype(np.int32), r.device)
+        self.boff_dev = _h2d(boff, r.device)
         keep = self._draw_keep(boff) if (self.split == "train" and r.rng == "numpy") else None
         # batch-local offsets of the entries held by this CSR (one scatter thread per entry)
-        self.lboff1_dev = torch.as_tensor(self._local_offsets(self.src1.lens, rows), device=r.device)
+        self.lboff1_dev = _h2d(self._local_offsets(self.src1.lens, rows), r.device)
         if self.src2 is not None:
             self.tlocal = self.src2.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)
-            self.lboff2_dev = torch.as_tensor(self._local_offsets(self.src2.lens, rows), device=r.device)
+            self.lboff2_dev = _h2d(self._local_offsets(self.src2.lens, rows), r.device)
         # row-gather chunk tables (inputs from source 1; targets from source 1 in training, else source 2)
         self.chunks1 = self._chunk_tables(self.src1.lens, rows, r.device)
         self.chunks2 = self.chunks1 if self.src2 is None else self._chunk_tables(self.src2.lens, rows, r.device)
@@ -278,7 +291,7 @@ class BatchGenerator(object):
         Lr = L[rep]
         j0 = k * Lr // ncr                 # equal-length chunks within a row
         j1 = (k + 1) * Lr // ncr
-        t = lambda x: torch.as_tensor(np.ascontiguousarray(x, dtype=np.int32), device=dev)
+        t = lambda x: _h2d(np.ascontiguousarray(x, dtype=np.int32), dev)
         max_chunks = nc.reshape(nb, B).max(axis=1) if nb else np.zeros(0, np.int64)
         return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase,
                     max_chunks=max_chunks)
@@ -344,7 +357,7 @@ class BatchGenerator(object):
             if k not in bufs or bufs[k].numel() < n:
                 bufs[k] = torch.empty(n, dtype=dt, device=dev)
         self._rl_bufs = bufs
-        keep = dict(sel=torch.as_tensor(sel.astype(np.int32), device=dev), ebase=torch.as_tensor(ebase, device=dev),
+        keep = dict(sel=_h2d(sel.astype(np.int32), dev), ebase=_h2d(ebase, dev),
                     row_ptr=bufs["row_ptr"], row_ent=bufs["row_ent"], live=bufs["live"])
         a = _lib.OcfEpochRowListArgs()
         a.n_sel, a.B, a.n_cols = len(sel), self.B, n_cols
@@ -358,7 +371,7 @@ class BatchGenerator(object):
         base = self.scatter_args(0) if nb else _lib.OcfScatterArgs()
         es = _lib.OcfEpochScatterArgs()
         if self.keep_dev is not None:
-            keep["keep_off"] = torch.as_tensor(np.ascontiguousarray(self.keep_off, dtype=np.int64), device=dev)
+            keep["keep_off"] = _h2d(np.ascontiguousarray(self.keep_off, dtype=np.int64), dev)
             es.keep_off = ptr(keep["keep_off"])
         es.n_sel, es.sel, es.ebase = len(sel), ptr(keep["sel"]), ptr(keep["ebase"])
         es.max_e = int(self.nnz1[sel].max()) if len(sel) else 0

@@ -337,9 +337,11 @@ class Engine:
         # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
         self.fold_reduce = True
         self._reduce_job = None
-        # ... and dW_out + dW_in as one launch (ocf_gemm_pair; its two sync words stay zero between launches)
+        # ... and dW_out + dW_in as one launch (ocf_gemm_pair: a device word the launches count up, never
+        # cleared, and its host-side running count)
         self.pair_dw = True
-        self.pair_sync = torch.zeros(2, device=d, dtype=torch.int64)
+        self.pair_sync = torch.zeros(1, device=d, dtype=torch.int64)
+        self.pair_state = _lib.OcfPairSync(ptr(self.pair_sync), 0)
         self._fused_step = False
         self._live_ptrs = None
         if self.comm is not None:   # feature parallel: reduced pre-activations, summed over ranks
@@ -764,8 +766,6 @@ class Engine:
         g.flag = self.gt.get("flag") or ptr(self.tflag)
         g.h, g.h_dtype, g.bias, g.aux = ptr(self.h[L - 1]), self.cdt, ptr(self.b[L]), self.gt["aux"]
         g.chunk_stats = ptr(cst)
-        if with_grad and self._fused_step and self.pair_dw:
-            g.zero_word = ptr(self.pair_sync)      # cleared for this step's ocf_gemm_pair launch
         ef, self._enc_fused = self._enc_fused, None
         if ef is not None:
             g.enc_part, g.enc_cptr, g.keep, g.stream = ef["enc_part"], ef["enc_cptr"], ef["keep"], ef["stream"]
@@ -1023,7 +1023,7 @@ class Engine:
                 g_in = self._weight_update_sparse(0, xval, self.dh[0], self.Hp[0], self.Hp[0], gscale, grads_out,
                                                   op, jobs=jobs_in, issue=False)
                 with self.phase("dW_pair"):
-                    call("ocf_gemm_pair", g_out, g_in, ptr(self.pair_sync), cur_stream())
+                    call("ocf_gemm_pair", g_out, g_in, ctypes.addressof(self.pair_state), cur_stream())
             else:
                 with self.phase("dW_out"):
                     self._weight_update_sparse(1, delta, self.h[0], HpL, HpL, gscale, grads_out, op,

@@ -55,6 +55,7 @@ STRUCTS = {
                                        "sp_lboff", "sp_krows", "sp_colsum", "sp_bptr", "sp_ent", "cb_op", "jb_part",
                                        "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
                                        "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
+    "OcfPairSync": (_lib.OcfPairSync, ["word", "count"]),
     "OcfRowStepArgs": (_lib.OcfRowStepArgs, ["enc", "dec", "dw_out", "dw_in", "jr", "jr_on", "ev", "pair_sync"]),
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
                                                        "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",

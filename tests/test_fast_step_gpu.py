@@ -72,10 +72,11 @@ def _run_pair(pair, cd, opt, shape):
     gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     h = m.fit_generator(gen, min(6, gen.num_batches - 1), epochs=1, verbose=0).history
     torch.cuda.synchronize()
-    # the pair launch's producer count (the decoder clears it before every launch): the pair ran on weights of
-    # more than 170 row tiles (smaller ones keep two launches)
-    ran = eng.pair_sync.cpu().tolist() == [(eng.Bp + 3) // 4, 0]
-    assert ran == (pair and eng.Np // 128 > 170) and eng.pair_sync[1].item() == 0
+    # the pair launches' producer count (never cleared; the host keeps its running twin): the pair ran on
+    # weights of more than 170 row tiles (smaller ones keep two launches), every launch on the same word
+    ran = eng.pair_state.count > 0
+    assert ran == (pair and eng.Np // 128 > 170)
+    assert eng.pair_sync[0].item() == eng.pair_state.count and eng.pair_state.count % ((eng.Bp + 3) // 4) == 0
     st = [t.cpu().numpy().copy() for sw, sb in eng.slots for t in sw + sb if t is not None]
     sh = [t.float().cpu().numpy() for t in eng.Wsh if t is not None]
     return h, m.get_weights(), st, sh, eng._rtag_live

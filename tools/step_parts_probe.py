@@ -85,11 +85,10 @@ o4 = cp(out)
 o4.row_live = live0.data_ptr()
 res["dw_out_jobs_only"] = timed(gemm(o4))
 print(json.dumps(dict(config=cfg, dtype=cd, us=res)))
-# the pair launch (ocf_gemm_pair): without the row reduction (nothing to wait for) and with it (the sync word
-# cleared before each launch, as the decoder does; the clear alone timed too)
-sync = eng.pair_sync
-res["pair_no_jr"] = timed(lambda: _lib.call("ocf_gemm_pair", o2, st.dw_in, sync.data_ptr(), s))
-res["clear_only"] = timed(lambda: sync.zero_())
-res["pair_jr_with_clear"] = timed(lambda: (sync.zero_(), _lib.call("ocf_gemm_pair", out, st.dw_in, sync.data_ptr(), s)))
+# the pair launch (ocf_gemm_pair): without the row reduction (nothing to wait for) and with it (the engine's
+# running counter: nothing to clear between launches)
+sync = ctypes.addressof(eng.pair_state)
+res["pair_no_jr"] = timed(lambda: _lib.call("ocf_gemm_pair", o2, st.dw_in, sync, s))
+res["pair_jr"] = timed(lambda: _lib.call("ocf_gemm_pair", out, st.dw_in, sync, s))
 res["two_launches_jr"] = timed(lambda: (_lib.call("ocf_gemm", out, s), _lib.call("ocf_gemm", st.dw_in, s)))
 print(json.dumps(dict(config=cfg, dtype=cd, pair=res)))
