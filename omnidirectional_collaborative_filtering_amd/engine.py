@@ -95,6 +95,7 @@ class Engine:
         self.Hp = [ru(h, TILE) for h in self.H]
         self.B = int(batch_size)
         self.Bp = ru(self.B, TILE)
+        self.rows_real = None         # real rows of a zero-padded dense batch (load_dense), None = B
         self.act = _lib.ACT[activation]
         self.activation = activation
         self.dropout = dropout
@@ -510,6 +511,7 @@ class Engine:
         row's segment per column tile directly -- no bucketing pass, no atomics."""
         if targets["t_ntiles"] != self.n_tiles:
             raise ValueError("target tile index has %d tiles, engine %d" % (targets["t_ntiles"], self.n_tiles))
+        self.rows_real = None
         if targets["E"] > self.tflag.numel():
             self.tflag = torch.zeros(max(targets["E"], 2 * self.tflag.numel()), device=self.dev, dtype=torch.uint8)
         a.tile_cnt = a.bk_ptr = a.bk_cur = a.bk_rc = a.bk_t = a.bk_m = None
@@ -589,12 +591,16 @@ class Engine:
         call("ocf_row_lists", a, cur_stream())
         return dict(sp_rowptr=rptr, sp_rowent=rent, sp_nent=E)
 
-    def load_dense(self, inputs, out_mask, targets, rows=None):
+    def load_dense(self, inputs, out_mask, targets, rows=None, rows_real=None):
         """API path: dense arrays in the model.py input order.  rows (device int64 [B]): the batch is rows
         `rows` of device-resident fp32 [n][ld] arrays (Model.fit uploads its arrays once), gathered by the
         packing and target kernels -- no per-step copy and no host synchronisation; otherwise [B, N]
-        host or device arrays are staged into one device buffer first."""
+        host or device arrays are staged into one device buffer first.  rows_real: the batch's real row
+        count when its last rows are all-zero padding (Keras' trailing partial batch): the MSE's 2/(b N)."""
         B, N = self.B, self.N
+        if rows_real is not None and not (1 <= int(rows_real) <= B):
+            raise ValueError("load_dense: rows_real must be in [1, %d]" % B)
+        self.rows_real = None if rows_real is None or int(rows_real) == B else int(rows_real)
         s = cur_stream()
         if rows is not None:
             srcs = list(inputs) + [out_mask, targets]
@@ -800,7 +806,7 @@ class Engine:
         """Decoder (dense GEMM with the fused masked-MSE epilogue, or the row gather for sparse
         batches); stats -> stats_hist[n_stats]."""
         L = len(self.H)
-        gscale = 2.0 / (self.B * self.N_total)
+        gscale = 2.0 / ((self.rows_real or self.B) * self.N_total)
         with self.phase("dec_gemm_mse"):
             if self.gt is not None:
                 self._output_gather(with_grad, gscale)
@@ -861,7 +867,7 @@ class Engine:
         the caller all-reduces and calls apply_grads()."""
         s = cur_stream()
         L, Bp = len(self.H), self.Bp
-        gscale = 2.0 / (self.B * self.N_total)
+        gscale = 2.0 / ((self.rows_real or self.B) * self.N_total)
         fused = grads_out is None
         op = self.opt.step_params(1.0, self.l2) if fused else None
         self._bias_op = self.opt.step_params(1.0, 0.0) if fused else None   # l2 regularises kernels only
@@ -1215,6 +1221,7 @@ class Engine:
     def fast_train_step(self, gen, bi):
         """Model._train_one's step on generator batch bi through ocf_train_step_rows; False when this step
         must take the general path (then nothing was done)."""
+        self.rows_real = None         # a generator batch: always B rows
         if not self.fast_steps or (self.timers is not None and self.timer_only is None):
             return False
         key = self._fast_key(gen)
@@ -1272,7 +1279,7 @@ class Engine:
         if self.opt.kind != _lib.OPT_ADAM and not self.opt.decay and self._plan is not None \
                 and self._plan.get("ready"):
             return stream, row, None, None     # constant optimizer scalars: the template's stand
-        gscale = 2.0 / (self.B * self.N_total)
+        gscale = 2.0 / ((self.rows_real or self.B) * self.N_total)
         op = self.opt.step_params(1.0, self.l2)
         o = _lib.OcfOptParams(op.kind, op.lr, op.eps, op.rho, op.beta2, op.l2, gscale)
         return stream, row, o, self.opt.step_params(1.0, 0.0)

@@ -4,12 +4,15 @@ Each batch's masked-MSE epilogue returns SSE, SAE, count_nonzero(y_true + y_pred
 per-row SSE; every metric of the reference is a closed form of those (Keras wraps each metric in
 a mean over the batch axis, so the per-row sqrt of accurate_RMSE is kept):
 
-  loss / mse           SSE / (B N)
-  mean_absolute_error  SAE / (B N)                        ('mae')
-  accurate_MAE         SAE / cnt
-  nMAE                 SAE / cnt / rating_range
-  accurate_MSE         SSE / cnt
-  accurate_RMSE        mean_b sqrt(B * SSE_b / cnt)
+  loss / mse           SSE / (b N)
+  mean_absolute_error  SAE / (b N)                        ('mae')
+  accurate_MAE         SAE B / (b cnt)
+  nMAE                 SAE B / (b cnt) / rating_range
+  accurate_MSE         SSE B / (b cnt)
+  accurate_RMSE        mean over the b rows of sqrt(B * SSE_row / cnt)
+where b is the batch's row count and B the script's global batch_size constant the metrics multiply
+by (train.py:105,111,116,121: ``MAE*num_items*batch_size``): b = B except for the trailing partial
+batch of Keras' Model.fit (train_jester.py:78-79), where the reference's own formulas give these.
 The functions below exist so user code can pass them by name exactly as train.py does
 (``metrics=['mae', accurate_MAE, nMAE, accurate_RMSE, accurate_MSE]``); calling them on host
 arrays evaluates the same closed forms.
@@ -30,21 +33,23 @@ def metric_name(m):
     return name
 
 
-def from_stats(name, sse, sae, cnt, row_sse, B, N, rating_range):
-    BN = float(B) * float(N)
+def from_stats(name, sse, sae, cnt, row_sse, B, N, rating_range, rows=None):
+    b = int(rows) if rows is not None else int(B)
+    bN = float(b) * float(N)
+    f = float(B) / float(b)
     with np.errstate(divide="ignore", invalid="ignore"):
         if name == "mean_absolute_error":
-            return sae / BN
+            return sae / bN
         if name == "mean_squared_error":
-            return sse / BN
+            return sse / bN
         if name == "accurate_MAE":
-            return np.float64(sae) / cnt
+            return np.float64(sae) * f / cnt
         if name == "nMAE":
-            return np.float64(sae) / cnt / rating_range
+            return np.float64(sae) * f / cnt / rating_range
         if name == "accurate_MSE":
-            return np.float64(sse) / cnt
+            return np.float64(sse) * f / cnt
         if name == "accurate_RMSE":
-            return float(np.mean(np.sqrt(np.asarray(row_sse[:B], np.float64) * B / cnt)))
+            return float(np.mean(np.sqrt(np.asarray(row_sse[:b], np.float64) * B / cnt)))
     raise ValueError(name)
 
 

@@ -113,17 +113,22 @@ class Model(object):
         return ["loss"] + list(self.metric_names)
 
     def _logs_from_stats(self, st, rows=None):
-        """st: [steps, 4 + Bp] device stats -> epoch-mean logs (Keras weights batches by size)."""
+        """st: [steps, 4 + Bp] device stats -> epoch-mean logs.  rows: the row count of every step's batch
+        (None: all full) -- Keras weights each batch's values by its size (BaseLogger for the training
+        logs, _test_loop for evaluation), which matters only for Model.fit's trailing partial batch."""
         e = self.engine
         B = e.B
+        rows = [B] * len(st) if rows is None else list(rows)
+        assert len(rows) == len(st)
         out = {k: [] for k in self.metrics_names}
-        for row in st:
+        for row, b in zip(st, rows):
             sse, sae, cnt = row[0], row[1], row[2]
             # Keras' total loss = MSE + the kernels' l2 penalty (row[3], 0 without l2); metrics have none
-            out["loss"].append(sse / (B * e.N_total) + row[3])
+            out["loss"].append(sse / (b * e.N_total) + row[3])
             for name in self.metric_names:
-                out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N_total, self.rating_range))
-        return {k: float(np.mean(v)) if v else float("nan") for k, v in out.items()}
+                out[name].append(M.from_stats(name, sse, sae, cnt, row[4:], B, e.N_total, self.rating_range, rows=b))
+        w = np.asarray(rows, np.float64)
+        return {k: float(np.dot(v, w) / w.sum()) if v else float("nan") for k, v in out.items()}
 
     # ------------------------------------------------------------------ batch plumbing
     def _split_inputs(self, x):
@@ -261,40 +266,60 @@ class Model(object):
 
     def fit(self, x, y, batch_size=None, epochs=1, verbose=1, callbacks=None, validation_split=0.0, shuffle=True,
             **kw):
-        """Keras Model.fit on dense arrays (train_jester.py:78-79): last validation_split fraction held out,
-        np.random.shuffle of the training indices each epoch; full batches only (fixed noise_shape)."""
+        """Keras 2.0.4 Model.fit on dense arrays (train_jester.py:78-79): the last validation_split fraction
+        held out (split_at = int(n (1 - validation_split))), np.random.shuffle of the training indices each
+        epoch, ceil(n / batch_size) batches -- the last one partial --, epoch logs weighted by batch size
+        (BaseLogger) and the validation logs by sample over every held-out row (_test_loop).  With a Dropout
+        layer the reference fixes noise_shape = [batch_size, H] (model.py:73), so a partial batch cannot run
+        there: with dropout only full batches are taken."""
         e = self.engine
         bs = int(batch_size or e.B)
         if bs != e.B:
             raise ValueError("batch_size must equal the model batch_size (Dropout noise_shape, model.py:73)")
-        # the arrays go to the device once; every batch is then gathered there by row index (no per-step
+        partial = e.keep >= 1.0
+        # the arrays go to the device once, plus one all-zero row that pads a partial batch (its input, output
+        # mask and target are zero, so it adds nothing to the loss, the statistics or any gradient; the
+        # gradient scale uses the real row count); every batch is then gathered there by row index (no per-step
         # host copies, no synchronisation between steps)
         dev = e.dev
 
         def on_dev(a):
             t = a if torch.is_tensor(a) else torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32))
-            return t.to(dev, torch.float32).contiguous()
+            out = torch.zeros(t.shape[0] + 1, t.shape[1], device=dev, dtype=torch.float32)
+            out[:-1] = t.to(dev, torch.float32)
+            return out
         xd = [on_dev(a) for a in x]
         yd = on_dev(y)
-        n = len(xd[0])
+        n = xd[0].shape[0] - 1
         split_at = int(n * (1.0 - validation_split)) if validation_split else n
         hist = History()
         callbacks = callbacks or []
+
+        def batches(m):
+            full, rest = divmod(m, bs)
+            return [(s * bs, bs) for s in range(full)] + ([(full * bs, rest)] if rest and partial else [])
+
+        def rows_of(ix, b):
+            if b == bs:
+                return ix
+            return torch.cat([ix, torch.full((bs - b,), n, dtype=torch.int64, device=dev)])
         val_rows = torch.arange(split_at, n, dtype=torch.int64, device=dev)
         for epoch in range(epochs):
             idx = np.arange(split_at)
             if shuffle:
                 np.random.shuffle(idx)
             idx_d = torch.as_tensor(idx, dtype=torch.int64).to(dev)
-            for s in range(split_at // bs):
-                self._load_rows(xd, yd, idx_d[s * bs:(s + 1) * bs])
+            tb = batches(split_at)
+            for s0, b in tb:
+                self._load_rows(xd, yd, rows_of(idx_d[s0:s0 + b], b), b)
                 e.train_step()
-            logs = self._logs_from_stats(e.take_stats())
-            if split_at < n and (n - split_at) >= bs:
-                for s in range((n - split_at) // bs):
-                    self._load_rows(xd, yd, val_rows[s * bs:(s + 1) * bs])
+            logs = self._logs_from_stats(e.take_stats(), [b for _, b in tb])
+            vb = batches(n - split_at)
+            if vb:
+                for s0, b in vb:
+                    self._load_rows(xd, yd, rows_of(val_rows[s0:s0 + b], b), b)
                     e.eval_step()
-                vl = self._logs_from_stats(e.take_stats())
+                vl = self._logs_from_stats(e.take_stats(), [b for _, b in vb])
                 for k, v in vl.items():
                     logs["val_" + k] = v
             for k, v in logs.items():
@@ -307,10 +332,10 @@ class Model(object):
                 break
         return hist
 
-    def _load_rows(self, xd, yd, rows):
-        """batch = rows `rows` of the device-resident arrays of Model.fit"""
+    def _load_rows(self, xd, yd, rows, real=None):
+        """batch = rows `rows` of the device-resident arrays of Model.fit (the first `real` of them real)"""
         blocks, out_mask = self._split_inputs(xd)
-        self.engine.load_dense(blocks, out_mask, yd, rows=rows)
+        self.engine.load_dense(blocks, out_mask, yd, rows=rows, rows_real=real)
 
     # ------------------------------------------------------------------ weights / checkpoints
     def get_weights(self):

@@ -9,9 +9,13 @@ timestamp); with reverse_user_item_data the first two columns swap roles (I-Auto
 rating-level permutation from NumPy's global RNG (:74; --seed seeds it first) splits 80/10/10
 (:76-83); every split's rows are keyed in dict-insertion order (first appearance in that split's
 ratings, build_user_item_dict :121-149) with the row keys as strings (movielens: str(int(id)),
-:127), lists in rating order; valid inputs = the row's train list, test inputs = its train + valid
-list, or none (map_inputs_to_targets :183-195).  Columns are the other id in order of first
-appearance in the CSV (the reference's unique_*_list, :106-118).
+:127; the others str(id)), lists in rating order; valid inputs = the row's train list, test inputs =
+its train + valid list, or none (map_inputs_to_targets :183-195).  Columns are the other id in order
+of first appearance in the CSV (the reference's unique_*_list, :106-118).  Ids are what the
+reference's pandas row holds (:125): in an all-numeric CSV with float ratings every id is a float
+(list ids 1193.0; netflix row keys '6.0'), with string ids they stay strings.  (An all-integer CSV --
+integer ratings too -- makes the reference's json.dump fail on np.int64 ids, :154; here it works, ids
+as ints.)
 
 Differences that are deliberate: the JSON writer names the files the way data_reader.py reads them
 (ratingsByItem_* + unique_users_list for I-AutoRec; the reference's split writes ratingsByUser_*
@@ -32,11 +36,23 @@ from .dataset import FixedSplit, split_ratings
 SCHEMAS = {"movielens": 4, "amazon": 4, "beeradvocate": 4, "yelp": 4, "netflix": 3}
 
 
-def _key(schema):
+def _row_scalar(df):
+    """What the reference's ``ratings.iloc[i]`` makes of one id (TrainValidTestSplit.py:125): a row of a frame
+    whose columns are all numeric is a single-dtype Series (np.result_type of the columns -- float64 as soon
+    as the ratings are floats), so numeric ids come out as floats (movielens item ids land in the lists as
+    1193.0, netflix row keys as '6.0'); a frame with a string column gives an object row (ids unchanged)."""
+    kinds = [np.dtype(d) for d in df.dtypes]
+    if all(k.kind in "iuf" for k in kinds):
+        common = np.result_type(*kinds)
+        return float if common.kind == "f" else int
+    return lambda x: _plain(x)
+
+
+def _key(schema, scalar=lambda x: x):
     """the row key the reference's build_user_item_dict writes (TrainValidTestSplit.py:126-135)"""
     if schema == "movielens":
-        return lambda x: str(int(x))
-    return lambda x: str(x)
+        return lambda x: str(int(scalar(x)))
+    return lambda x: str(scalar(x))
 
 
 def _plain(v):
@@ -58,9 +74,10 @@ def split_csv(path, schema="movielens", reverse_user_item_data=False, split=(0.8
     vals = df.iloc[:, 2].to_numpy(dtype=np.float64)
     row_codes, row_uniq = pd.factorize(row_raw, sort=False)
     col_codes, col_uniq = pd.factorize(col_raw, sort=False)          # first appearance = pd.unique order
-    key = _key(schema)
+    scalar = _row_scalar(df)
+    key = _key(schema, scalar)
     row_keys = [key(x) for x in row_uniq]
-    col_ids = [_plain(x) for x in col_uniq]
+    col_ids = [scalar(_plain(x)) for x in col_uniq]                  # the ids the reference's lists carry
     return split_ratings(row_codes.astype(np.int64), col_codes.astype(np.int32), vals.astype(np.float32),
                          len(row_uniq), len(col_uniq), split=split, rng=rng, row_keys=row_keys, col_ids=col_ids)
 

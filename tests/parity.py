@@ -220,27 +220,42 @@ def with_duplicates(rows, cols, nnz, dup_frac=0.03, half_stars=True, seed=0):
     return data
 
 
+def aux_model_input(aux_type, x, m_in, m_miss):
+    """the first dense layer's input for a data_gen batch (model.py:47-56 concatenates in the order of
+    data_reader.py:341-361): x alone (aux None), [x, mask_to_feed] (causal: the missing-data mask; dropout:
+    the input mask; zeros: zeros) or [x, m_in, m_miss] (both, use_both_masks)"""
+    if aux_type is None:
+        return x
+    feed = {"causal": m_miss, "dropout": m_in, "both": m_in, "zeros": np.zeros_like(m_in)}[aux_type]
+    return np.concatenate([x, feed] + ([m_miss] if aux_type == "both" else []), 1)
+
+
 def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_dtype, dropout, seed, oracle_batch,
-                         eval_batches=4, envelope=False, lr=0.005, epoch_lists=True):
+                         eval_batches=4, envelope=False, lr=0.005, epoch_lists=True, aux_type=None):
     """The DEFAULT training path (data_reader with rng='numpy' -> fit_generator, one hidden layer,
     aux None = k=1 row gathers, the per-epoch row lists and scatter outputs, row-stream dW with
     live-row skipping) on the reference's data semantics: reciprocal split with s<1, pass-through
-    on or off, duplicate (row, col) ratings, unsorted lists.  oracle_batch(bi, rows) -> (x, m_out, t)
-    is the oracle's dense batch (reference goldens or scatter_rows_numpy over the replayed draws).
+    on or off, duplicate (row, col) ratings, unsorted lists.  With aux_type (causal / dropout / zeros /
+    both) the generator feeds the aux-mask inputs and the model concatenates them (use_causal_info,
+    use_both_masks for 'both': k = 2 / 3 input blocks, the dense scatter + MFMA path).
+    oracle_batch(bi, rows) -> (x, m_out, t) is the oracle's dense batch, x already the concatenated
+    model input (reference goldens or scatter_rows_numpy over the replayed draws).
     Per step: loss and accurate_MSE (count_nonzero(T + y) denominators) vs the oracle; after the run
     every weight, and compute_full_RMSE on the test split (train.py:243-255)."""
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     from omnidirectional_collaborative_filtering_amd.optimizers import Adagrad
     from oracle.model_oracle import batch_metrics
     N = rd.num_items
-    om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype=compute_dtype,
-                    seed=11, dropout_probability=dropout)
+    k = 1 + int(aux_type is not None) + int(aux_type == "both")
+    om = omni_model(1, H, N, B, dense_activation="sigmoid", use_causal_info=aux_type is not None,
+                    use_both_masks=aux_type == "both", compute_dtype=compute_dtype, seed=11,
+                    dropout_probability=dropout)
     m = om.model
     om.engine.epoch_row_lists = om.engine.epoch_scatter = epoch_lists
     m.compile(Adagrad(lr=lr, epsilon=1e-8), "mean_squared_error", metrics=["accurate_MSE"])
     w0 = m.get_weights()
     np.random.seed(seed)
-    gen = rd.data_gen(B, sparsity, "train", True, None, aux, pass_through_input_training=pass_through)
+    gen = rd.data_gen(B, sparsity, "train", True, aux_type, aux, pass_through_input_training=pass_through)
     assert gen.r.rng == "numpy"
     steps = min(steps, gen.num_batches)
     masks, gl, gm = [], [], []
@@ -251,18 +266,21 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
         if dropout:
             masks.append([om.engine.mask[0][:B, :H].cpu().numpy().astype(np.float64)])
     e = om.engine
-    # the default path really ran: row gathers, the epoch's row lists + scatter outputs, live-row records
-    if epoch_lists:
+    if k > 1:                              # aux-mask inputs: the dense k-block scatter + MFMA path
+        assert e.k == k and not e.sparse_ok and e.gt is None
+    elif epoch_lists:
+        # the default path really ran: row gathers, the epoch's row lists + scatter outputs, live-row records
         assert e.gt is not None and "xval" in e.gt and "flag" in e.gt, "epoch scatter outputs not used"
         assert getattr(gen, "_rl", None) is not None
     else:                                  # per-step ocf_scatter_batch + ocf_row_lists
         assert e.gt is not None and getattr(gen, "_rl", None) is None
-    assert e.tb is not None and "sp_rowptr" in e.tb
-    assert e._rtag_live == (e.row_skip == "always" or getattr(gen, "_rl", None) is None or
-                            not gen.gather_tables(0)["rows_dense"]), "live-row records expected (Adagrad, l2 = 0)"
+    if k == 1:
+        assert e.tb is not None and "sp_rowptr" in e.tb
+        assert e._rtag_live == (e.row_skip == "always" or getattr(gen, "_rl", None) is None or
+                                not gen.gather_tables(0)["rows_dense"]), "live-row records expected (Adagrad, l2 = 0)"
     w_gpu = m.get_weights()
-    ora = OmniOracle([N, H, N], activation="sigmoid", dropout=dropout, dtype=np.float64).set_params(w0[0::2],
-                                                                                                   w0[1::2])
+    ora = OmniOracle([k * N, H, N], activation="sigmoid", dropout=dropout, dtype=np.float64).set_params(w0[0::2],
+                                                                                                       w0[1::2])
     opt = AdagradOracle(lr=lr, epsilon=1e-8)
     u = UNIT_ROUNDOFF[compute_dtype]
     env = [np.zeros_like(p) for p in ora.params()] if envelope else None
@@ -283,7 +301,7 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
         ora.set_flat(opt.step(ora.params(), grads))
     # compute_full_RMSE over test batches; the oracle replays the test permutation itself
     np.random.seed(seed + 1)
-    tgen = rd.data_gen(B, None, "test", True, None, aux, return_target_count=True)
+    tgen = rd.data_gen(B, None, "test", True, aux_type, aux, return_target_count=True)
     nb = min(eval_batches, rd.test_set_size // B)
     sse, cnt = m.evaluate_sse(tgen, nb)
     np.random.seed(seed + 1)
@@ -293,10 +311,13 @@ def run_semantics_parity(rd, B, H, steps, sparsity, pass_through, aux, compute_d
     for bi in range(nb):
         rows = order[bi * B:(bi + 1) * B]
         assert np.array_equal(rows, tgen.rows_host[bi])
-        _, _, xe, _, _ = scatter_rows_numpy(data.test_in.row_ptr, data.test_in.col, data.test_in.val, rows, N, aux=aux)
-        _, mo, _, te, _ = scatter_rows_numpy(data.test_tgt.row_ptr, data.test_tgt.col, data.test_tgt.val, rows, N,
-                                             aux=aux)
-        y, _ = ora.forward(xe, mo)
+        mi, _, xe, _, mm1 = scatter_rows_numpy(data.test_in.row_ptr, data.test_in.col, data.test_in.val, rows, N,
+                                               aux=aux)
+        _, mo, _, te, mm2 = scatter_rows_numpy(data.test_tgt.row_ptr, data.test_tgt.col, data.test_tgt.val, rows, N,
+                                               aux=aux)
+        # fixed split (data_reader.py:250-266): the missing-data mask covers the input and the target ratings
+        miss = np.where((mm1 != 0) | (mm2 != 0), aux, 0.0)
+        y, _ = ora.forward(aux_model_input(aux_type, xe, mi, miss), mo)
         sse_o += float(((y - te) ** 2).sum())
         cnt_o += int(data.test_tgt.row_lengths()[rows].sum())          # data_reader.py:268: every list entry
     assert cnt == cnt_o, (cnt, cnt_o)

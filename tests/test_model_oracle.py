@@ -81,6 +81,16 @@ def test_metrics_closed_forms():
     assert np.isclose(M.from_stats("accurate_RMSE", sse, sae, cnt, rs, B, N, 4.0), ref["accurate_RMSE"])
     assert np.isclose(M.from_stats("mean_absolute_error", sse, sae, cnt, rs, B, N, 4.0), ref["mean_absolute_error"])
     assert np.isclose(compute_full_RMSE([y], [t], cnt), np.sqrt(sse / cnt))
+    # Keras' trailing partial batch of Model.fit (b = 4 rows; the metrics still multiply by the script's
+    # batch_size constant B, train.py:105-121): the per-batch values the reference's formulas give
+    b = 4
+    ref = batch_metrics(t[:b], y[:b], N, B, 4.0)
+    e = e[:b]
+    sse, sae, cnt = (e * e).sum(), np.abs(e).sum(), np.count_nonzero(t[:b] + y[:b])
+    rs = np.concatenate([(e * e).sum(1), np.zeros(B - b)])      # the padding rows carry nothing
+    for name in ("accurate_MSE", "accurate_MAE", "nMAE", "accurate_RMSE", "mean_absolute_error"):
+        assert np.isclose(M.from_stats(name, sse, sae, cnt, rs, B, N, 4.0, rows=b), ref[name]), name
+    assert np.isclose(M.from_stats("mean_squared_error", sse, sae, cnt, rs, B, N, 4.0, rows=b), ref["loss"])
 
 
 @pytest.mark.parametrize("dropout", [None, 0.2])

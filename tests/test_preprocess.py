@@ -70,3 +70,55 @@ def test_cli(tmp_path):
     ref = load_reference_json(os.path.join(SPLIT, "I"), reverse_user_item_data=False)
     _same(FixedSplit.load(str(tmp_path / "d.npz")), ref)
     _same(load_reference_json(str(tmp_path / "j"), reverse_user_item_data=True), ref)
+
+
+def _ref_dicts(d):
+    out = {}
+    for part in ("train", "valid", "test"):
+        with open(os.path.join(d, "ratingsByUser_dicts_%s.json" % part)) as f:
+            out[part] = json.load(f)
+    return out
+
+
+def _same_json(a, b):
+    """equal JSON structures with the same key order and the same id types (float ids stay floats)"""
+    if isinstance(a, dict):
+        assert isinstance(b, dict) and list(a) == list(b)
+        for k in a:
+            _same_json(a[k], b[k])
+    elif isinstance(a, list):
+        assert isinstance(b, list) and len(a) == len(b)
+        for x, y in zip(a, b):
+            _same_json(x, y)
+    else:
+        assert a == b and type(a) is type(b), (a, b)
+
+
+@pytest.mark.parametrize("sub", ["split_ml", "split_nf"])
+@pytest.mark.parametrize("orient", ["U", "I"])
+def test_numeric_schemas_match_reference(tmp_path, sub, orient):
+    """'movielens' (row keys str(int(id)), :127) and 'netflix' (3 columns, :64-69; keys str(id) of the float
+    row, e.g. '31.0') on numeric-id CSVs, against the reference's own split of the same CSV (make_split_golden
+    .py; save_users_and_items False): the JSON files save_reference_json writes equal the reference's -- same
+    row keys in the same order, the same lists in the same order, item ids as the floats the reference writes"""
+    d = os.path.join(ROOT, "tests", "golden", sub)
+    with open(os.path.join(d, "meta.json")) as f:
+        meta = json.load(f)
+    rev = orient == "I"
+    np.random.seed(meta["seeds"][orient])
+    fs = split_csv(os.path.join(d, meta["csv"]), meta["schema_type"], reverse_user_item_data=rev)
+    save_reference_json(fs, str(tmp_path / "j"), reverse_user_item_data=rev)
+    ours = {}
+    base = "ratingsByItem" if rev else "ratingsByUser"
+    for part in ("train", "valid", "test"):
+        with open(str(tmp_path / "j" / ("%s_dicts_%s.json" % (base, part)))) as f:
+            ours[part] = json.load(f)
+    ref = _ref_dicts(os.path.join(d, orient))
+    _same_json(ref, ours)
+    ids = [e[0] for lst in ref["train"].values() for e in lst]
+    assert all(isinstance(i, float) for i in ids)      # the reference's float ids (all-numeric float frame)
+    if meta["schema_type"] == "netflix":
+        assert all(k.endswith(".0") for k in ref["train"])
+    # ... and data_reader reads them back (float ids find their columns in the id list)
+    fs2 = load_reference_json(str(tmp_path / "j"), reverse_user_item_data=rev)
+    _same(fs2, fs)

@@ -17,7 +17,12 @@ order.
     exactly as data_reader.py does, so the two must see the same batches;
   * test_train_parity_duplicates: an ML-1M-shaped (3,706 x 6,040) synthetic set with 3 % duplicate
     pairs, 0.0 ratings and shuffled lists; the oracle replays the reference's np.random calls itself
-    (tests/parity.py replay_train_draws) and scatters with scatter_rows_numpy.
+    (tests/parity.py replay_train_draws) and scatters with scatter_rows_numpy;
+  * test_train_parity_golden_aux_inputs / test_train_parity_aux_inputs_ml1m: the omnidirectional inputs
+    (model.py:47-56 use_causal_info / use_both_masks fed by data_reader.py:341-361's auxilliary_mask_type
+    causal / dropout / zeros / both: k = 2 or 3 input blocks) trained against the oracle -- on the
+    reference's own golden batches (the oracle's input is the golden in0 | in1 [| in3] concatenation, the
+    output mask in2), and on the ML-1M shape with the reciprocal split (m_in != m_miss) and duplicates.
 
 Tolerances (tests/parity.py): fp32 -- per-step loss and accurate_MSE within 1e-5 relative, test
 RMSE within 1e-5, every weight within 1e-5 max-abs; f16 -- loss / accurate_MSE / RMSE within 2e-3
@@ -29,7 +34,7 @@ import numpy as np
 import pytest
 
 from oracle.batch_oracle import scatter_rows_numpy
-from parity import (assert_fp32, assert_low_precision, replay_train_draws, run_semantics_parity,
+from parity import (assert_fp32, assert_low_precision, aux_model_input, replay_train_draws, run_semantics_parity,
                     with_duplicates)
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -138,6 +143,74 @@ def test_train_parity_golden_toy(gpu, ci, cd):
                                lambda bi, rows: _gold_batch(gold, name, "train1", bi, aux_type),
                                envelope=cd != "float32")
     assert len(res.step_losses_g) == rd.train_set_size // B
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 2e-3)
+
+
+def _gold_model_batch(gold, name, tag, bi, aux_type):
+    """(model input, M_out, T) of a golden batch in data_gen's input order (data_reader.py:354-361): without
+    aux [in0 = X, in1 = M_out]; with aux [in0 = X, in1 = mask_to_feed, in2 = M_out (, in3 = missing-data mask
+    for 'both')] -> X | mask_to_feed (| in3), the concatenation model.py:50,56 forms"""
+    p = "%s/%s/%d/" % (name, tag, bi)
+    if aux_type is None:
+        return gold[p + "in0"], gold[p + "in1"], gold[p + "targets"]
+    blocks = [gold[p + "in0"], gold[p + "in1"]] + ([gold[p + "in3"]] if aux_type == "both" else [])
+    return np.concatenate(blocks, 1), gold[p + "in2"], gold[p + "targets"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+@pytest.mark.parametrize("ci", [1, 2, 3, 4])
+def test_train_parity_golden_aux_inputs(gpu, ci, cd):
+    """the golden configurations WITH their aux-mask inputs: recip_drop (dropout mask, s in [0.3, 0.7], no
+    pass-through: m_in != m_miss), recip_both (k = 3, aux +1), half_causal (the missing-data mask), low_zeros
+    (a zero block, aux +1) -- the model concatenates the aux blocks (k = 2 / 3, dense path), the oracle is
+    fed the reference's own in0 | in1 (| in3) arrays"""
+    cfg = _cfg()
+    name, sp, pt, aux_type, auxv = cfg["train_configs"][ci]
+    assert aux_type is not None
+    B = cfg["B"]
+    rd, gold = _toy_reader("I")
+    res = run_semantics_parity(rd, B, 16, 99, sp, pt, float(auxv), cd, 0.2, cfg["seed_base"] + ci,
+                               lambda bi, rows: _gold_model_batch(gold, name, "train1", bi, aux_type),
+                               envelope=cd != "float32", aux_type=aux_type)
+    assert len(res.step_losses_g) == rd.train_set_size // B
+    assert res.ora.W[0].shape[0] == (3 if aux_type == "both" else 2) * rd.num_items
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float32", "float16"])
+@pytest.mark.parametrize("aux_type,sp,pt", [("dropout", [0.3, 0.7], False), ("both", [0.3, 0.7], False),
+                                            ("causal", [0.5, 0.5], True), ("zeros", [1.0, 1.0], True)])
+def test_train_parity_aux_inputs_ml1m(gpu, aux_type, sp, pt, cd):
+    """ML-1M I-AutoRec shape (3,706 x 6,040, B = 256, H = 500) with the aux-mask inputs: k = 2 (dropout /
+    causal / zeros) or 3 (both) input blocks of 6,040, the reciprocal split replayed from the reference's
+    own np.random calls, 3 % duplicate pairs, 0.0 ratings, shuffled lists"""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    data = _dup_data(0.25)
+    N = data.num_cols
+    B, seed = 256, 41
+    rd = data_reader(N, data.train.n_rows, dataset=data, eval_mode="fixed_split")
+    tr = data.train
+    np.random.seed(seed)
+    rows_o, keeps = replay_train_draws(tr.row_lengths()[np.arange(tr.n_rows)], rd.train_set_size, B, sp)
+
+    def oracle_batch(bi, rows):
+        assert np.array_equal(rows, rows_o[bi])
+        m_in, mo, x, t, m_miss = scatter_rows_numpy(tr.row_ptr, tr.col, tr.val, rows_o[bi], N, keep=keeps[bi],
+                                                    aux=-1.0, pass_through=pt)
+        if aux_type == "dropout" and sp[1] < 1:
+            assert (m_in != m_miss).any()       # the two masks really differ under the split
+        return aux_model_input(aux_type, x, m_in, m_miss), mo, t
+
+    res = run_semantics_parity(rd, B, 500, 3, sp, pt, -1.0, cd, 0.2, seed, oracle_batch, eval_batches=2,
+                               envelope=cd != "float32", aux_type=aux_type)
     if cd == "float32":
         assert_fp32(res)
     else:
