@@ -124,3 +124,34 @@ def test_state_only_path(gpu, nb, B, mean_len):
     wst = np.random.get_state()
     assert p2 == int(wst[2])
     np.testing.assert_array_equal(k2, wst[1])
+
+
+@pytest.mark.gpu
+def test_tiny_epoch_flags_ready_when_the_call_returns(gpu):
+    """every draw inside the caller's current 624-word block (no end-state copy to wait for): the call still
+    synchronises its stream, so flags written on a side stream (data_reader's RNG stream) are complete when it
+    returns -- read here on the main stream with no torch.cuda.synchronize in between"""
+    import torch
+    nb, B = 2, 8
+    lens, boff, ebase = _epoch(nb, B, 3.0, 4)
+    E = int(ebase[-1])
+    np.random.seed(7)
+    np.random.random_sample(3)
+    pos = int(np.random.get_state()[2])
+    assert 2 * (nb * B + E) <= 624 - pos, "the tiny epoch must fit in the current block"
+    side = torch.cuda.Stream(device=gpu)
+    with torch.cuda.stream(side):
+        boff_d = torch.as_tensor(boff, device=gpu)
+        ebase_d = torch.as_tensor(ebase, device=gpu)
+        keep = torch.full((E,), 7, dtype=torch.uint8, device=gpu)
+        a, st, ws = _args(nb, B, boff_d, ebase_d, E, 0.3, 0.7, keep, None, gpu)
+        k2, p2 = _run(a)
+    got = keep.cpu().numpy()                 # main stream: no wait on `side` besides the call's own
+    np.random.set_state(st)
+    want = []
+    for bi in range(nb):
+        s = np.random.uniform(low=0.3, high=0.7, size=B)
+        u = np.random.random_sample(int(boff[bi, -1]))
+        want.append(u >= np.repeat((1.0 - s) / ((1.0 - s) + s), lens[bi]))
+    assert np.array_equal(got.astype(bool), np.concatenate(want)) and set(np.unique(got)) <= {0, 1}
+    assert p2 == int(np.random.get_state()[2])
