@@ -109,9 +109,11 @@ template <typename CT, int CW, int NCH, int E0, bool ADAM, bool LONG> struct RpR
 // entries as one vector (lane i = entry i, up to 64 at a time), stage D their values as one gather, and
 // stage E walks them in groups of RS_ETL whose B rows are all in flight at once -- the entry indices come
 // from the vector by readlane, so a group waits for its B rows only, not for an entry -> value -> B chain.
-// the workgroup body of one weight matrix's launch: workgroup wbx of [job-only workgroups][row workgroups]
-template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
-__device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs& jobs, const int wbx) {
+// The row pipeline of one wave over the ranks k0 + stride i (i < nr) of a weight matrix's live rows;
+// row_of(k) maps a rank to its weight row (called with increasing ranks, valid ones only).
+template <typename CT, int KIND, int CW, int NCH, bool LONG, typename RowOf>
+__device__ __forceinline__ void rowpipe_ranks(const RowsDwArgs& ra, const WsJobs& jobs, const int k0, const int stride,
+                                              const int nr, RowOf&& row_of) {
   using V = RsVec<CW>;
   using F = typename V::F;
   using H = RsH<CT, CW>;
@@ -119,36 +121,7 @@ __device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs&
   constexpr int E0 = RS_E0;
   using Row = RpRow<CT, CW, NCH, E0, ADAM, LONG>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // folded small jobs (the decoder's row reduction, hidden-bias update, the step's stats): one per wave of
-  // the FIRST workgroups, which take no rows -- the row workgroups start at once on the other CUs instead
-  // of behind a job (a job is a chain of dependent loads: 10-20 us; ML-1M's dW launches were ~25 us of
-  // which the jobs' were the floor)
-  const int njwg = (jobs.count() + 3) / 4;
-  if (wbx < njwg) {
-    const int j = wbx * 4 + wave;
-    if (j < jobs.count()) jobs.run<KIND>(j, lane);
-    return;
-  }
-  const int wb = wbx - njwg;
-  const int t = wb / PARTS, part = wb % PARTS;
-  if (t >= ra.M / 128) return;
-  const int m0 = t * 128;
-  const uint8_t* rec = ra.live ? ra.live + (int64_t)t * OCF_LIVE_REC : nullptr;
-  const int L = rec ? *reinterpret_cast<const int*>(rec) : (ra.M - m0 < 128 ? ra.M - m0 : 128);
-  auto row_of = [&](int k) { return rec ? (int)rec[16 + (k & 7) * 16 + (k >> 3)] : k; };
-  if (ra.colsum && rec && part == 0) {      // rows without entries: zero output-bias gradient
-    __shared__ uint8_t live_fl[128];
-    if (tid < 128) live_fl[tid] = 0;
-    __syncthreads();
-    if (tid < L) live_fl[row_of(tid)] = 1;
-    __syncthreads();
-    if (tid < 128 && !live_fl[tid]) ra.colsum[m0 + tid] = 0.f;
-  }
-  // this part's ranks [kb, ke), this wave's: kb + wave + 4 i, i < nr
-  const int kb = part * L / PARTS, ke = (part + 1) * L / PARTS;
-  const int nr = __builtin_amdgcn_readfirstlane(ke - kb - wave > 0 ? (ke - kb - wave + 3) / 4 : 0);
   if (nr == 0) return;
-
   const __amdgpu_buffer_rsrc_t rp = wt_rsrc(ra.p), r1 = wt_rsrc(ra.s1), r2 = wt_rsrc(ra.s2);
   const CT* Bg = reinterpret_cast<const CT*>(ra.B);
   auto col = [&](int j) { return (lane + 64 * j) * CW; };
@@ -156,7 +129,7 @@ __device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs&
   auto bpiece = [&](int k, int j) { return *reinterpret_cast<const H*>(Bg + (int64_t)k * ra.ldb + col(j)); };
   auto stA = [&](Row& r, int i) {
     r.lv = i < nr;
-    r.m = m0 + __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * (i < nr ? i : 0)));
+    r.m = r.lv ? __builtin_amdgcn_readfirstlane(row_of(k0 + stride * i)) : 0;
   };
   auto ld_pa = [&](Row& r) {
 #pragma unroll
@@ -350,6 +323,42 @@ __device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs&
   }
 }
 
+// the workgroup body of one weight matrix's launch: workgroup wbx of [job-only workgroups][row workgroups],
+// the row workgroups PARTS per 128-row tile (a part of the tile's live rows each)
+template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
+__device__ __forceinline__ void rowpipe_body(const RowsDwArgs& ra, const WsJobs& jobs, const int wbx) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // folded small jobs (the decoder's row reduction, hidden-bias update, the step's stats): one per wave of
+  // the FIRST workgroups, which take no rows -- the row workgroups start at once on the other CUs instead
+  // of behind a job (a job is a chain of dependent loads: 10-20 us; ML-1M's dW launches were ~25 us of
+  // which the jobs' were the floor)
+  const int njwg = (jobs.count() + 3) / 4;
+  if (wbx < njwg) {
+    const int j = wbx * 4 + wave;
+    if (j < jobs.count()) jobs.run<KIND>(j, lane);
+    return;
+  }
+  const int wb = wbx - njwg;
+  const int t = wb / PARTS, part = wb % PARTS;
+  if (t >= ra.M / 128) return;
+  const int m0 = t * 128;
+  const uint8_t* rec = ra.live ? ra.live + (int64_t)t * OCF_LIVE_REC : nullptr;
+  const int L = rec ? *reinterpret_cast<const int*>(rec) : (ra.M - m0 < 128 ? ra.M - m0 : 128);
+  auto row_of = [&](int k) { return m0 + (rec ? (int)rec[16 + (k & 7) * 16 + (k >> 3)] : k); };
+  if (ra.colsum && rec && part == 0) {      // rows without entries: zero output-bias gradient
+    __shared__ uint8_t live_fl[128];
+    if (tid < 128) live_fl[tid] = 0;
+    __syncthreads();
+    if (tid < L) live_fl[row_of(tid) - m0] = 1;
+    __syncthreads();
+    if (tid < 128 && !live_fl[tid]) ra.colsum[m0 + tid] = 0.f;
+  }
+  // this part's ranks [kb, ke), this wave's: kb + wave + 4 i, i < nr
+  const int kb = part * L / PARTS, ke = (part + 1) * L / PARTS;
+  const int nr = __builtin_amdgcn_readfirstlane(ke - kb - wave > 0 ? (ke - kb - wave + 3) / 4 : 0);
+  rowpipe_ranks<CT, KIND, CW, NCH, LONG>(ra, jobs, kb + wave, 4, nr, row_of);
+}
+
 template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_kernel(RowsDwArgs ra, WsJobs jobs) {
   rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(ra, jobs, blockIdx.x);
@@ -376,6 +385,32 @@ struct RsPair {
   int n_a, n_prod, max_polls;
 };
 
+// The wait: one plain load first (L2-cached: once a consumer of this XCD has seen the count complete, the
+// later ones find it there), then relaxed agent-scope loads until the count is complete.  Measured and
+// rejected: an agent-scope acquire per consumer (it invalidates the XCD's L2) and a consumer count for a
+// self-reset (thousands of atomics on one word): the ML-20M pair launch took 1.0-1.3 ms instead of 0.31.
+// No invalidation is needed: the data the wait guards (the row reduction's outputs) is read in this kernel
+// only after the wait and the kernel start invalidated every L1 / L2 line from before it, so a consumer's
+// caches hold no stale copy -- its reads miss to memory, which the producers' release (L2 write-back) has
+// updated, or hit lines a producer on the same XCD wrote.  Returns true when the producers' count is
+// complete, false (error word set) when the bounded wait gave up.
+__device__ __forceinline__ bool pair_wait(const RsPair& ps) {
+  __shared__ int ok_sh;
+  if (threadIdx.x == 0) {
+    bool ok = *reinterpret_cast<volatile unsigned long long*>(ps.word) >= ps.want;
+    for (int it = 0; !ok && it < ps.max_polls; ++it) {
+      ok = __hip_atomic_load(ps.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ps.want;
+      if (!ok) __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(ps.err, (uint32_t)OCF_ASYNC_PAIR_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ok_sh = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const bool ok = ok_sh != 0;
+  if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return ok;
+}
+
 template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwArgs ra, WsJobs ja, RowsDwArgs rb,
                                                                         WsJobs jb, RsPair ps) {
@@ -391,27 +426,8 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
     }
     return;
   }
-  // The wait: one plain load first (L2-cached: once a consumer of this XCD has seen the count complete,
-  // the later ones find it there), then relaxed agent-scope loads until the count is complete.  Measured
-  // and rejected: an agent-scope acquire per consumer (it invalidates the XCD's L2) and a consumer count
-  // for a self-reset (thousands of atomics on one word): the ML-20M pair launch took 1.0-1.3 ms instead of
-  // 0.31.  No invalidation is needed: the data the wait guards (the row reduction's outputs) is read in
-  // this kernel only after the wait and the kernel start invalidated every L1 / L2 line from before it, so
-  // a consumer's caches hold no stale copy -- its reads miss to memory, which the producers' release (L2
-  // write-back) has updated, or hit lines a producer on the same XCD wrote.
-  __shared__ int gave_up;
-  if (threadIdx.x == 0) {
-    bool ok = *reinterpret_cast<volatile unsigned long long*>(ps.word) >= ps.want;
-    for (int it = 0; !ok && it < ps.max_polls; ++it) {
-      ok = __hip_atomic_load(ps.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ps.want;
-      if (!ok) __builtin_amdgcn_s_sleep(2);
-    }
-    if (!ok) __hip_atomic_store(ps.err, (uint32_t)OCF_ASYNC_PAIR_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    gave_up = ok ? 0 : 1;
-  }
-  __syncthreads();
-  if (gave_up) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (!pair_wait(ps)) return;
   rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(rb, jb, bx - ps.n_a);
 }
+
 }  // namespace ocf

@@ -1,0 +1,105 @@
+// The row-stream launch templates (ocf_rows.hip's host logic + ocf_rows_dw.h's kernels), instantiated once
+// per compute dtype in ocf_rows_f16.hip / ocf_rows_bf16.hip / ocf_rows_f32.hip (the kernel instances take
+// minutes to compile: one translation unit per dtype builds them in parallel).
+#pragma once
+#include "ocf_internal.h"
+#include "ocf_rows.h"
+#include "ocf_rows_dw.h"
+
+namespace ocf {
+
+struct RowsLaunch {
+  RowsDwArgs ra;
+  WsJobs jb;
+  int grid, parts, N;
+  bool lng, small;
+  int kind;
+};
+
+bool rows_setup(const OcfGemmArgs& g, const EpiOptim::Params& ep, RowsLaunch& L);
+EpiOptim::Params optim_params(const OcfGemmArgs& g);
+bool rows_pair_ok(const OcfGemmArgs& g);
+
+// the kernel instance for (optimizer, N, parts, LONG): f(kernel template tag) launches it
+template <typename CT, typename F>
+void rows_dispatch(const RowsLaunch& L, F&& f) {
+  auto go = [&](auto kind_tag, auto cw_tag, auto nch_tag) {
+    constexpr int KIND = decltype(kind_tag)::value, CW = decltype(cw_tag)::value;
+    constexpr int NCH = decltype(nch_tag)::value;
+    if (L.lng && L.small) f.template go<CT, KIND, CW, NCH, 32, true>();
+    else if (L.lng) f.template go<CT, KIND, CW, NCH, 12, true>();
+    else if (L.small) f.template go<CT, KIND, CW, NCH, 32, false>();
+    else f.template go<CT, KIND, CW, NCH, 12, false>();
+  };
+  using std::integral_constant;
+  auto by_n = [&](auto k) {
+    switch (L.N) {
+      case 128: go(k, integral_constant<int, 2>{}, integral_constant<int, 1>{}); break;
+      case 256: go(k, integral_constant<int, 4>{}, integral_constant<int, 1>{}); break;
+      case 384: go(k, integral_constant<int, 2>{}, integral_constant<int, 3>{}); break;
+      default: go(k, integral_constant<int, 4>{}, integral_constant<int, 2>{});
+    }
+  };
+  switch (L.kind) {
+    case OCF_OPT_ADAGRAD: by_n(integral_constant<int, OCF_OPT_ADAGRAD>{}); break;
+    case OCF_OPT_RMSPROP: by_n(integral_constant<int, OCF_OPT_RMSPROP>{}); break;
+    default: by_n(integral_constant<int, OCF_OPT_ADAM>{});
+  }
+}
+
+struct RowsOne {
+  const RowsLaunch& L;
+  hipStream_t s;
+  template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
+    hipLaunchKernelGGL((optim_rowpipe_kernel<CT, KIND, CW, NCH, PARTS, LONG>), dim3(L.grid), dim3(RS_THREADS), 0, s,
+                       L.ra, L.jb);
+  }
+};
+struct RowsPair {
+  const RowsLaunch& A;
+  const RowsLaunch& B;
+  RsPair ps;
+  hipStream_t s;
+  template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
+    hipLaunchKernelGGL((optim_rowpipe_pair_kernel<CT, KIND, CW, NCH, PARTS, LONG>), dim3(A.grid + B.grid),
+                       dim3(RS_THREADS), 0, s, A.ra, A.jb, B.ra, B.jb, ps);
+  }
+};
+
+template <typename CT>
+bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
+  RowsLaunch L;
+  if (!rows_setup(g, ep, L)) return false;
+  rows_dispatch<CT>(L, RowsOne{L, s});
+  OCF_HIP(hipGetLastError());
+  return true;
+}
+
+template <typename CT>
+bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& sync, hipStream_t s) {
+  if (!g_optim_rows || !rows_pair_ok(a) || !rows_pair_ok(b)) return false;
+  RowsLaunch A, B;
+  if (!rows_setup(a, optim_params(a), A) || !rows_setup(b, optim_params(b), B)) return false;
+  if (A.kind != B.kind || A.N != B.N || A.parts != B.parts || A.lng != B.lng || A.small != B.small) return false;
+  // small weights (about one row per wave) keep two launches: there the in-kernel wait (the producers'
+  // L2 write-back, the consumers' polling) cost more than the boundary it replaces (ML-1M 36.9 vs 36.8 us,
+  // ML-100K 25.8 vs 21.7; ML-20M 303 vs 307: tools/step_parts_probe.py)
+  if (A.small) return false;
+  RsPair ps;
+  ps.word = reinterpret_cast<unsigned long long*>(sync.word);
+  ps.n_a = A.grid;
+  ps.n_prod = A.jb.jr_on ? (A.jb.jr.Bp + 3) / 4 : 0;   // the job-only workgroups holding the row reduction
+  ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
+  ps.err = async_error_word();
+  ps.max_polls = g_pair_wait_polls;
+  rows_dispatch<CT>(A, RowsPair{A, B, ps, s});
+  OCF_HIP(hipGetLastError());
+  sync.count = ps.want;
+  return true;
+}
+
+#define OCF_ROWS_INSTANTIATE(CT)                                                                           \
+  template bool launch_rows<CT>(const OcfGemmArgs&, const EpiOptim::Params&, hipStream_t);                  \
+  template bool launch_rows_pair<CT>(const OcfGemmArgs&, const OcfGemmArgs&, OcfPairSync&, hipStream_t);
+
+}  // namespace ocf
