@@ -176,6 +176,47 @@ def cpu_baseline(data, rows_batches, N, H, w0, lr, n_steps, config):
     return out
 
 
+def same_batch_one_gpu(args, data_full, n_rows, Bg, dev, steps=10, warmup=3):
+    """The reference point for a weak-scaling feature-parallel line: the SAME global batch (B x G rows) on ONE
+    GPU with the whole model -- measured in this run, on rank 0 before the timed region (the other ranks wait
+    in their first collective)."""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    st = np.random.get_state()
+    np.random.seed(4321)
+    rd = data_reader(data_full.num_cols, n_rows, dataset=data_full, eval_mode="fixed_split", rng="numpy", device=dev)
+    om = omni_model(1, args.hidden, data_full.num_cols, Bg, dense_activation="sigmoid", use_causal_info=False,
+                    dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev)
+    m = om.model
+    m.compile(optim(args.optimizer, 0.005 if args.optimizer == "adagrad" else 0.001), "mean_squared_error")
+    gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    gen._start()
+    nb = gen.num_batches
+    eng = om.engine
+    gen.prepare_row_lists(eng.Np, [i % nb for i in range(warmup + steps)])
+
+    def step(i):
+        bi = i % nb
+        if not eng.fast_train_step(gen, bi):
+            m._load(None, gen, bi)
+            eng.train_step()
+        return int(gen.nnz1[bi])
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nnz = sum(step(warmup + i) for i in range(steps))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.take_stats()
+    np.random.set_state(st)
+    out = {"global_batch": Bg, "ms_per_step": round(dt / steps * 1e3, 4), "ratings_per_s": round(nnz / dt, 1),
+           "steps": steps, "source": "measured in this run: rank 0, one GPU, the whole model, before the timed region"}
+    del om, m, eng, gen, rd
+    torch.cuda.empty_cache()
+    return out
+
+
 def fp32_mode(args, data, rd, n_rows, dev, steps):
     """ms/step of the exact-fp32 parity mode (compute_dtype float32, v_mfma_f32_32x32x2_f32; the mode the
     1e-5 parity bar is tested in) on the same workload, N=1"""
@@ -437,6 +478,9 @@ def main():
     dpo = DataParallel(eng, rank, world, mode=args.dp_mode, grad_dtype=args.dp_grad_dtype) \
         if (world > 1 and not fp) else None
     nnz_of = gen.nnz1
+    same_batch = None
+    if fp and world > 1 and rank == 0 and not args.emulate_shards:
+        same_batch = same_batch_one_gpu(args, data_full, n_rows, B * world, dev)
     setup_s = time.time() - t0
 
     def step(i):
@@ -605,12 +649,10 @@ def main():
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
                      if epoch_lists else "per step (ocf_row_lists)" if eng.sparse_dw else "n/a",
     }
-    if world > 1 and fp and args.config == "ml20m" and B == 256:
-        # weak scaling grows the global batch with the ranks; the same global batch on ONE GPU (measured on
-        # this build, row-stream path) is the reference point for the speed-up, not the B = 256 line
-        line["same_global_batch_1gpu"] = {
-            "global_batch": B * world, "ms_per_step": {2: 0.636, 4: 0.843, 8: 1.1188}.get(world),
-            "source": "profiles/r03_slab_rejected/b2048_S0.json (B=2,048); DESIGN.md §5 batch sweep (512, 1,024)"}
+    if same_batch is not None:
+        # weak scaling grows the global batch with the ranks; the same global batch on ONE GPU is the reference
+        # point for the speed-up, not the B = 256 line
+        line["same_global_batch_1gpu"] = same_batch
     if world == 1 and args.fp32_steps > 0 and args.dtype != "float32" and not args.emulate_shards:
         line["fp32_parity_mode"] = fp32_mode(args, data, rd, n_rows, dev, args.fp32_steps)
     if world == 1 and args.epoch and not args.emulate_shards:

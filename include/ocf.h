@@ -351,6 +351,51 @@ typedef struct OcfRowStepArgs {
 } OcfRowStepArgs;
 int ocf_train_step_rows(const OcfRowStepArgs* args, void* stream);
 
+/*
+ * ocf_rank_step -- one feature-parallel rank step (SURVEY.md 8(e) N-sharding: this rank owns a column
+ * shard of W1's rows and W_out's, one hidden layer, generator batches) as one library call per phase,
+ * the collectives between them issued by the host (train.py:157 per step; model.py:64-86 forward,
+ * train.py:49-51 loss and update):
+ *   phase 0  ocf_gather_encoder(enc); ocf_rows_reduce(enc_sum)        -> partial pre-activations; the host
+ *            all-reduces them over the ranks
+ *   phase 1  ocf_splitk_bias_act(hidden); ocf_gather_decoder(dec); ocf_rows_reduce(dec_sum) -> partial
+ *            hidden deltas; ocf_stats_finalize(stats) on `side` -- the host starts the deltas' all-reduce
+ *   phase 2  (on `side`, overlapping that all-reduce) ocf_gemm(dw_out); ocf_bias_opt_from_partials(out_bias)
+ *   phase 3  (after the host waited for it) ocf_splitk_grad_act(hidden_grad); ocf_gemm(dw_in); `stream`
+ *            waits for `side`
+ * Each member is exactly what the single call takes (the same checks run).  side = NULL runs every phase on
+ * `stream`; with side, fork[0..1] / join are hipEvent_t the library records (side waits on fork[k] recorded
+ * on stream before phases 1 / 2; stream waits on join recorded on side in phase 3).  ev[8] (nullable):
+ * events recorded on stream before / after phase 0, 1, 2 (on side when set), 3.  The host keeps one of
+ * these per model and rewrites only the batch's table pointers, the dropout stream and the stats slot
+ * between steps (engine.Engine.fast_rank_step), so a rank step costs four calls instead of ten argument
+ * blocks built in Python. */
+typedef struct OcfBiasActArgs {         /* ocf_splitk_bias_act's arguments, in order (without the stream) */
+  const float* slabs; int splits; int64_t split_stride; int M, N; int64_t ld; const float* bias; int act;
+  float keep; uint64_t seed, stream; const uint8_t* mask_in; uint8_t* mask_out; float* a_out; void* h_out;
+  int h_dtype, m_real, n_real;
+} OcfBiasActArgs;
+typedef struct OcfGradActArgs {         /* ocf_splitk_grad_act's arguments, in order */
+  const float* slabs; int splits; int64_t split_stride; int M, N; int64_t ld; const float* a_in;
+  const uint8_t* mask; float keep; int act; void* d_out; int d_dtype; float* db; float gscale; int m_real, n_real;
+} OcfGradActArgs;
+typedef struct OcfStatsArgs {           /* ocf_stats_finalize's arguments, in order */
+  const float* stats_part; int n_parts; const float* row_sse_part; int n_tiles, M; float* out;
+} OcfStatsArgs;
+typedef struct OcfBiasOptArgs {         /* ocf_bias_opt_from_partials' arguments, in order (opt by value) */
+  float* b; const float* db_part; int parts; int64_t ld; int n; float* s1; float* s2; float* g_out;
+  OcfOptParams opt;
+} OcfBiasOptArgs;
+typedef struct OcfRankStepArgs {
+  OcfGatherArgs enc; OcfRowsReduceArgs enc_sum;
+  OcfBiasActArgs hidden; OcfGatherArgs dec; OcfRowsReduceArgs dec_sum; OcfStatsArgs stats;
+  OcfGemmArgs dw_out; OcfBiasOptArgs out_bias;
+  OcfGradActArgs hidden_grad; OcfGemmArgs dw_in;
+  void* side; void* fork[2]; void* join;
+  void* ev[8];
+} OcfRankStepArgs;
+int ocf_rank_step(const OcfRankStepArgs* args, int phase, void* stream);
+
 /* split-K reductions fused with the layer epilogue (see OCF_EPI_BIAS_ACT / OCF_EPI_GRAD_ACT).
  * ocf_splitk_grad_act writes bias-gradient partials db[M/4][ld] (one row per 4 batch rows,
  * already * gscale) for ocf_bias_opt_from_partials. */

@@ -132,6 +132,38 @@ class OcfRowStepArgs(ctypes.Structure):
                 ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8), ("pair_sync", P)]
 
 
+class OcfBiasActArgs(ctypes.Structure):
+    """ocf.h: ocf_splitk_bias_act's arguments as a block (without the stream)"""
+    _fields_ = [("slabs", P), ("splits", I32), ("split_stride", I64), ("M", I32), ("N", I32), ("ld", I64),
+                ("bias", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64), ("mask_in", P),
+                ("mask_out", P), ("a_out", P), ("h_out", P), ("h_dtype", I32), ("m_real", I32), ("n_real", I32)]
+
+
+class OcfGradActArgs(ctypes.Structure):
+    """ocf.h: ocf_splitk_grad_act's arguments as a block"""
+    _fields_ = [("slabs", P), ("splits", I32), ("split_stride", I64), ("M", I32), ("N", I32), ("ld", I64),
+                ("a_in", P), ("mask", P), ("keep", F32), ("act", I32), ("d_out", P), ("d_dtype", I32), ("db", P),
+                ("gscale", F32), ("m_real", I32), ("n_real", I32)]
+
+
+class OcfStatsArgs(ctypes.Structure):
+    """ocf.h: ocf_stats_finalize's arguments as a block"""
+    _fields_ = [("stats_part", P), ("n_parts", I32), ("row_sse_part", P), ("n_tiles", I32), ("M", I32), ("out", P)]
+
+
+class OcfBiasOptArgs(ctypes.Structure):
+    """ocf.h: ocf_bias_opt_from_partials' arguments as a block (opt by value)"""
+    _fields_ = [("b", P), ("db_part", P), ("parts", I32), ("ld", I64), ("n", I32), ("s1", P), ("s2", P),
+                ("g_out", P), ("opt", OcfOptParams)]
+
+
+class OcfRankStepArgs(ctypes.Structure):
+    _fields_ = [("enc", OcfGatherArgs), ("enc_sum", OcfRowsReduceArgs), ("hidden", OcfBiasActArgs),
+                ("dec", OcfGatherArgs), ("dec_sum", OcfRowsReduceArgs), ("stats", OcfStatsArgs),
+                ("dw_out", OcfGemmArgs), ("out_bias", OcfBiasOptArgs), ("hidden_grad", OcfGradActArgs),
+                ("dw_in", OcfGemmArgs), ("side", P), ("fork", P * 2), ("join", P), ("ev", P * 8)]
+
+
 class OcfTileBucketArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
@@ -174,6 +206,7 @@ SIGNATURES = {
     "ocf_gemm": (I32, [ctypes.POINTER(OcfGemmArgs), P]),
     "ocf_gemm_pair": (I32, [ctypes.POINTER(OcfGemmArgs), ctypes.POINTER(OcfGemmArgs), P, P]),   # P: OcfPairSync*
     "ocf_train_step_rows": (I32, [ctypes.POINTER(OcfRowStepArgs), P]),
+    "ocf_rank_step": (I32, [ctypes.POINTER(OcfRankStepArgs), I32, P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),

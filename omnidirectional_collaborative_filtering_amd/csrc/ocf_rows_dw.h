@@ -120,7 +120,7 @@ __device__ __forceinline__ void rowpipe_ranks(const RowsDwArgs& ra, const WsJobs
   constexpr bool ADAM = KIND == OCF_OPT_ADAM;
   constexpr int E0 = RS_E0;
   using Row = RpRow<CT, CW, NCH, E0, ADAM, LONG>;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lane = threadIdx.x & 63;
   if (nr == 0) return;
   const __amdgpu_buffer_rsrc_t rp = wt_rsrc(ra.p), r1 = wt_rsrc(ra.s1), r2 = wt_rsrc(ra.s2);
   const CT* Bg = reinterpret_cast<const CT*>(ra.B);

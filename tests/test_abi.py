@@ -56,6 +56,15 @@ STRUCTS = {
                                        "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
                                        "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
     "OcfPairSync": (_lib.OcfPairSync, ["word", "count"]),
+    "OcfBiasActArgs": (_lib.OcfBiasActArgs, ["slabs", "splits", "split_stride", "M", "N", "ld", "bias", "act", "keep",
+                                             "seed", "stream", "mask_in", "mask_out", "a_out", "h_out", "h_dtype",
+                                             "m_real", "n_real"]),
+    "OcfGradActArgs": (_lib.OcfGradActArgs, ["slabs", "splits", "split_stride", "M", "N", "ld", "a_in", "mask", "keep",
+                                             "act", "d_out", "d_dtype", "db", "gscale", "m_real", "n_real"]),
+    "OcfStatsArgs": (_lib.OcfStatsArgs, ["stats_part", "n_parts", "row_sse_part", "n_tiles", "M", "out"]),
+    "OcfBiasOptArgs": (_lib.OcfBiasOptArgs, ["b", "db_part", "parts", "ld", "n", "s1", "s2", "g_out", "opt"]),
+    "OcfRankStepArgs": (_lib.OcfRankStepArgs, ["enc", "enc_sum", "hidden", "dec", "dec_sum", "stats", "dw_out",
+                                               "out_bias", "hidden_grad", "dw_in", "side", "fork", "join", "ev"]),
     "OcfRowStepArgs": (_lib.OcfRowStepArgs, ["enc", "dec", "dw_out", "dw_in", "jr", "jr_on", "ev", "pair_sync"]),
     "OcfTileBucketArgs": (_lib.OcfTileBucketArgs, ["rows", "lboff", "krows", "nk", "cnt", "ent", "cap", "counted",
                                                        "cnt_clear", "rtag_in", "rtag", "live_in", "live_out",

@@ -25,6 +25,8 @@ def stubbed(monkeypatch):
         if name == "ocf_train_step_rows":
             st = args[0]
             seen.append(ctypes.string_at(ctypes.addressof(st), ctypes.sizeof(st)))
+        if name == "ocf_rank_step" and args[1] == 0:
+            seen.append(ctypes.string_at(ctypes.addressof(args[0]), ctypes.sizeof(args[0])))
         return 0
     monkeypatch.setattr(_lib, "call", fake_call)
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
@@ -122,3 +124,69 @@ def test_fast_step_declines_other_layouts(stubbed):
     ok = _model("adagrad", None, data).engine
     assert not ok.fast_train_step(vg, vg.next_batch_index())
     assert not stubbed
+
+
+class _Comm:
+    """feature-parallel collectives of one rank alone (no-ops with the real call shape: comm(t) and the
+    asynchronous start(t).wait())"""
+
+    class _W:
+        def wait(self):
+            pass
+
+    def __call__(self, t):
+        pass
+
+    def start(self, t):
+        return self._W()
+
+
+@pytest.mark.parametrize("opt,dropout,sparsity", [("adagrad", 0.2, [1.0, 1.0]), ("rmsprop", None, [0.3, 0.7])])
+def test_rank_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
+    """the feature-parallel rank step's template (ocf.h OcfRankStepArgs, Engine._fast_rank_step) rewritten for
+    each step equals the ten argument blocks the general path builds for it, byte for byte, across epochs,
+    row-list windows and the reciprocal split; the real one-call steps issue four ocf_rank_step phases"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    from omnidirectional_collaborative_filtering_amd.parallel import feature_shard_range
+    r, c, v = synthetic_ratings(400, 600, 12000, half_stars=True, seed=3)
+    data = split_ratings(r, c, v, 400, 600, rng=np.random.RandomState(3), dup_free=True)
+    c0, c1 = feature_shard_range(data.num_cols, 1, 4)
+    ds = data.column_shard(c0, c1)
+    np.random.seed(5)
+    rd = data_reader(ds.num_cols, data.train.n_rows, dataset=ds, eval_mode="fixed_split", rng="numpy",
+                     device=torch.device("cpu"))
+    om = omni_model(1, 100, ds.num_cols, 32, dense_activation="sigmoid", use_causal_info=False,
+                    dropout_probability=dropout, compute_dtype="float16", seed=7, device=torch.device("cpu"),
+                    shard=(c0, c1, data.num_cols), comm=_Comm())
+    om.model.compile({"adagrad": lambda: O.Adagrad(lr=0.005), "rmsprop": lambda: O.RMSprop(lr=0.001)}[opt](),
+                     "mean_squared_error")
+    eng = om.engine
+    b = lambda x: ctypes.string_at(ctypes.addressof(x), ctypes.sizeof(x))
+    checked = fast = 0
+    for epoch in range(5):
+        gen = rd.data_gen(32, sparsity, "train", True, None, -1, pass_through_input_training=sparsity[0] >= 1.0)
+        while True:
+            bi = gen.next_batch_index()
+            if bi is None:
+                break
+            pl = eng._rplan
+            f = gen.step_fields(bi, eng.Np)
+            if pl is not None and pl.get("ready") and eng._rank_key(gen) == pl["key"] and f is not None \
+                    and eng._rank_fits(pl, f):
+                if (bi + epoch) % 3 == 0:
+                    assert eng.fast_train_step(gen, bi)
+                    fast += 1
+                    continue
+                st = _lib.OcfRankStepArgs.from_buffer_copy(pl["st"])
+                eng._grow_stats(eng.n_stats + 1)
+                eng._rank_rewrite(st, f, eng._rank_stream(eng.step_count), eng._stats_row(eng.n_stats), pl["live"])
+                calls = eng._recorded_step(gen, bi)
+                assert tuple(n for n, _ in calls) == eng._RANK_CALLS
+                assert b(st) == b(eng._rank_template(pl["key"], calls)["st"]), (epoch, bi)
+                checked += 1
+            else:
+                assert eng.fast_train_step(gen, bi)
+    assert checked >= 12 and fast >= 5, (checked, fast)

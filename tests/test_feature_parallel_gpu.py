@@ -1,7 +1,8 @@
 """GPU, 2 ranks sharing cuda:0 over gloo: feature-parallel training (column-sharded W1 / W_out,
 two [B,H] all-reduces per step) equals single-engine training on the full model -- with the
 reciprocal input/output split (s < 1, NumPy RNG via full-row positions), the causal/dropout mask
-concat (k = 2 input blocks) and dropout (same Philox stream on every rank)."""
+concat (k = 2 input blocks) and dropout (same Philox stream on every rank).  With k = 1 the rank steps
+after the first two run as four ocf_rank_step phase calls (Engine._fast_rank_step)."""
 import os
 import socket
 
@@ -9,7 +10,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-ROWS, COLS, NNZ, B, H, STEPS = 700, 333, 14000, 128, 100, 4
+ROWS, COLS, NNZ, B, H, STEPS = 900, 333, 18000, 128, 100, 6
 
 
 def _free_port():
@@ -42,7 +43,9 @@ def _train(data, shard=None, comm=None, causal=True):
     np.random.seed(99)
     tg = rd.data_gen(B, None, "test", True, aux, -1, return_target_count=True)
     sse, cnt = m.evaluate_sse(tg, rd.test_set_size // B)
-    return h.history["loss"][0], h.history["accurate_MSE"][0], float(np.sqrt(sse / cnt)), m.get_weights()
+    pl = om.engine._rplan
+    one_call = bool(pl is not None and pl.get("ready"))    # the rank steps ran as ocf_rank_step phases
+    return h.history["loss"][0], h.history["accurate_MSE"][0], float(np.sqrt(sse / cnt)), m.get_weights(), one_call
 
 
 def _worker(rank, world, port, q, causal):
@@ -77,9 +80,11 @@ def test_feature_parallel_equals_single_engine(gpu, causal):
         p.join(timeout=120)
         assert p.exitcode == 0
     data = _dataset()
-    loss, amse, rmse, w = _train(data, causal=causal)
+    loss, amse, rmse, w, _ = _train(data, causal=causal)
     N = data.num_cols
-    for rank, c0, c1, l_r, a_r, rmse_r, w_r in res:
+    for rank, c0, c1, l_r, a_r, rmse_r, w_r, one_call in res:
+        # the row-gather layout (k = 1) takes the one-call-per-phase rank step after two recorded steps
+        assert one_call == (not causal)
         assert abs(l_r - loss) <= 1e-5 * loss, (l_r, loss)
         assert abs(a_r - amse) <= 1e-5 * amse
         assert abs(rmse_r - rmse) <= 1e-5, (rmse_r, rmse)
