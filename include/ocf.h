@@ -321,6 +321,7 @@ int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, OcfPairSync* sync,
 /* codes of the asynchronous error word (kernels that detect a fault without stopping; reported by the
  * next entry point through its status and ocf_last_error()) */
 #define OCF_ASYNC_PAIR_WAIT 1
+#define OCF_ASYNC_MLP_BARRIER 2   /* ocf_mlp_step: a grid barrier gave up (workgroups not all resident) */
 
 /*
  * ocf_train_step_rows -- one whole single-GPU training step of a one-hidden-layer model on a sparse
@@ -590,6 +591,45 @@ int ocf_masked_mse(const float* pred, const float* T, const float* out_mask, int
  * W[i] / b[i]) = gscale * the backward pass of model.py:64-86 (dropout masks of that forward). */
 int ocf_backward(OcfCtx* ctx, const float* grad, int64_t ld_grad, int B, float gscale, float* const* gW,
                  float* const* gb, void* stream);
+
+/*
+ * ocf_mlp_step -- one whole training step of a SMALL dense model (train_jester.py's 200 -> 256 -> 256 -> 100,
+ * Model.fit's batches: train_jester.py:44-79 with model.py:64-86, train.py:49 and the Keras update) in ONE
+ * launch: a persistent grid of `wgs` workgroups runs the forward layers, the masked MSE with the step's
+ * statistics, the backward pass and every weight / bias update as phases separated by grid barriers
+ * (2 L + 1 barriers for L hidden layers).  Each phase's work is 32 x 32 output tiles, one per wave, on MFMA
+ * (v_mfma_f32_32x32x16_{f16,bf16} on operands rounded to the compute dtype, v_mfma_f32_32x32x2_f32 in the
+ * exact-fp32 mode); a layer's weights are updated only after the phase that still reads them.  For models
+ * whose weights fit in L2 (0.14 M parameters) the step is latency-bound: one launch instead of ~14.
+ * The batch is gathered from device-resident arrays by row index (Model.fit's data path): input block j of
+ * batch row b is x[j] + rows[b] * ld_x (N values), its output mask / targets out_mask / targets + rows[b] *
+ * ld_t.  Rows b >= B are padding (zero).  Weights in the engine's padded layout: W[0] [k_blocks * Np][hidden_p[0]]
+ * (block j's column n at row j * Np + n), W[i] [hidden_p[i-1]][hidden_p[i]], W[L] transposed [Np][hidden_p[L-1]];
+ * b[i] the padded output width; optimizer slots alike (nullable per the optimizer); shadow[i] (nullable) the
+ * compute-dtype copy of W[i] rewritten by the update (64 x 64-blocked with shadow_blocked).  No dropout, l2 = 0.
+ * stats: {sse, sae, count_nonzero(T + y), 0, row sse [Bp]} (the masked-MSE statistics).  work: scratch of
+ * ocf_mlp_step_workspace bytes.  barrier: device uint32[2], zero before the first launch, left reusable.
+ */
+typedef struct OcfMlpStepArgs {
+  int n_hidden;                                   /* L, 1..OCF_MAX_HIDDEN */
+  int B, Bp;                                      /* batch rows; padded (multiple of 32, <= 512) */
+  int N, Np, k_blocks;                            /* output width / padded (multiple of 32); input blocks */
+  int hidden[OCF_MAX_HIDDEN], hidden_p[OCF_MAX_HIDDEN];   /* hidden widths, padded (multiples of 32) */
+  const float* x[3]; int64_t ld_x; const int64_t* rows;
+  const float* out_mask; const float* targets; int64_t ld_t;
+  float* W[OCF_MAX_HIDDEN + 1]; float* b[OCF_MAX_HIDDEN + 1];
+  float* sW1[OCF_MAX_HIDDEN + 1]; float* sW2[OCF_MAX_HIDDEN + 1];
+  float* sb1[OCF_MAX_HIDDEN + 1]; float* sb2[OCF_MAX_HIDDEN + 1];
+  void* shadow[OCF_MAX_HIDDEN + 1]; int shadow_blocked;
+  int act, compute_dtype;
+  OcfOptParams opt;                               /* gscale = 2 / (B N) */
+  float* stats;
+  void* work; int64_t work_bytes;
+  uint32_t* barrier;
+  int wgs;                                        /* persistent workgroups (0: library choice) */
+} OcfMlpStepArgs;
+int64_t ocf_mlp_step_workspace(const OcfMlpStepArgs* args);
+int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);
 
 /* ocf_set_tuning -- process-wide kernel selection switches (no reference counterpart).
  *   "optim_ws": 1 (default; env OCF_OPTIM_WS=0 turns it off) = EPI_OPTIM weight-gradient GEMMs on

@@ -164,6 +164,20 @@ class OcfRankStepArgs(ctypes.Structure):
                 ("dw_in", OcfGemmArgs), ("side", P), ("fork", P * 2), ("join", P), ("ev", P * 8)]
 
 
+class OcfMlpStepArgs(ctypes.Structure):
+    """ocf.h OcfMlpStepArgs: a small dense model's whole step in one launch (ocf_mlp_step)"""
+    _L = 8 + 1
+    _fields_ = [("n_hidden", I32), ("B", I32), ("Bp", I32), ("N", I32), ("Np", I32), ("k_blocks", I32),
+                ("hidden", I32 * 8), ("hidden_p", I32 * 8), ("x", P * 3), ("ld_x", I64), ("rows", P),
+                ("out_mask", P), ("targets", P), ("ld_t", I64), ("W", P * _L), ("b", P * _L), ("sW1", P * _L),
+                ("sW2", P * _L), ("sb1", P * _L), ("sb2", P * _L), ("shadow", P * _L), ("shadow_blocked", I32),
+                ("act", I32), ("compute_dtype", I32), ("opt", OcfOptParams), ("stats", P), ("work", P),
+                ("work_bytes", I64), ("barrier", P), ("wgs", I32)]
+
+
+ASYNC_MLP_BARRIER = 2          # ocf.h OCF_ASYNC_MLP_BARRIER
+
+
 class OcfTileBucketArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("col", P), ("lidx", P), ("lboff", P),
@@ -207,6 +221,8 @@ SIGNATURES = {
     "ocf_gemm_pair": (I32, [ctypes.POINTER(OcfGemmArgs), ctypes.POINTER(OcfGemmArgs), P, P]),   # P: OcfPairSync*
     "ocf_train_step_rows": (I32, [ctypes.POINTER(OcfRowStepArgs), P]),
     "ocf_rank_step": (I32, [ctypes.POINTER(OcfRankStepArgs), I32, P]),
+    "ocf_mlp_step_workspace": (I64, [ctypes.POINTER(OcfMlpStepArgs)]),
+    "ocf_mlp_step": (I32, [ctypes.POINTER(OcfMlpStepArgs), P]),
     "ocf_splitk_bias_act": (I32, [P, I32, I64, I32, I32, I64, P, I32, F32, U64, U64, P, P, P, P, I32, I32, I32, P]),
     "ocf_splitk_grad_act": (I32, [P, I32, I64, I32, I32, I64, P, P, F32, I32, P, I32, P, F32, I32, I32, P]),
     "ocf_opt_step": (I32, [P, P, P, P, I64, ctypes.POINTER(OcfOptParams), P]),

@@ -96,6 +96,10 @@ class Engine:
         self.B = int(batch_size)
         self.Bp = ru(self.B, TILE)
         self.rows_real = None         # real rows of a zero-padded dense batch (load_dense), None = B
+        # dense batches gathered by row (Model.fit): packing deferred to the layer-wise path; small models take
+        # the fused one-launch step (ocf_mlp_step) instead
+        self._pending_pack = self._mlp_batch = self._mlp_args = None
+        self.fused_mlp = True
         self.act = _lib.ACT[activation]
         self.activation = activation
         self.dropout = dropout
@@ -512,6 +516,7 @@ class Engine:
         if targets["t_ntiles"] != self.n_tiles:
             raise ValueError("target tile index has %d tiles, engine %d" % (targets["t_ntiles"], self.n_tiles))
         self.rows_real = None
+        self._pending_pack = self._mlp_batch = None     # the scatter writes this batch's layer-0 input
         if targets["E"] > self.tflag.numel():
             self.tflag = torch.zeros(max(targets["E"], 2 * self.tflag.numel()), device=self.dev, dtype=torch.uint8)
         a.tile_cnt = a.bk_ptr = a.bk_cur = a.bk_rc = a.bk_t = a.bk_m = None
@@ -612,9 +617,11 @@ class Engine:
             if rows.numel() != B or rows.dtype != torch.int64 or not rows.is_cuda:
                 raise ValueError("load_dense(rows=...): rows must be %d device int64 indices" % B)
             p = [ptr(t) for t in inputs] + [None] * (3 - len(inputs))
-            call("ocf_pack_input", p[0], p[1], p[2], ld, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
-                 self.Bp, ptr(rows), s)
+            # packed into xin when a layer-wise path needs it (forward); the fused small-model step
+            # (ocf_mlp_step) gathers the rows itself
+            self._pending_pack = (p, ld, ptr(rows))
             T, M, rp = targets, out_mask, ptr(rows)
+            self._mlp_batch = (p, ld, ptr(rows), ptr(out_mask), ptr(targets))
         else:
             if self.dense_in is None:
                 self.dense_in = torch.zeros(5, self.B, self.Np, device=self.dev, dtype=torch.float32)
@@ -633,6 +640,7 @@ class Engine:
             call("ocf_pack_input", p0, p1, p2, self.Np, B, N, ptr(self.xin), self.cdt, self.pad_dims[0], self.Np,
                  self.Bp, None, s)
             T, M, rp, ld = buf[4], buf[3], None, self.Np
+            self._pending_pack = self._mlp_batch = None
         self._xin_clean = False      # xin written densely
         self.tb = None
         self.gt = None                 # dense batch: the GEMM path, never a previous batch's gather tables
@@ -641,6 +649,66 @@ class Engine:
         # the arrays alive while the step is queued
         self.tseg = dict(dn_t=ptr(T), dn_m=ptr(M), ld_dn=ld, dn_rows=rp, n_real=N)
         self._dense_keep = (T, M, rows)
+
+    def _pack_pending(self):
+        """ocf_pack_input for a row-gathered dense batch whose packing load_dense deferred"""
+        pp = self._pending_pack
+        if pp is not None:
+            p, ld, rp = pp
+            call("ocf_pack_input", p[0], p[1], p[2], ld, self.B, self.N, ptr(self.xin), self.cdt, self.pad_dims[0],
+                 self.Np, self.Bp, rp, cur_stream())
+            self._pending_pack = None
+
+    # ---------------------------------------------------------------- fused small-model step
+    # A small dense model (train_jester.py: 0.14 M parameters, batch 128) on a row-gathered dense batch
+    # (Model.fit) takes ONE persistent launch for the whole step (ocf.h ocf_mlp_step) instead of the
+    # layer-wise path's ~14 latency-bound launches.  No dropout, no l2, every layer trainable, one GPU.
+    MLP_MAX_PARAMS = 4 << 20
+
+    def _mlp_ok(self):
+        return (self.fused_mlp and self._mlp_batch is not None and self._pending_pack is not None
+                and self.comm is None and self.dp_world == 1 and self.keep >= 1.0 and not self.l2
+                and all(self.trainable) and self.grad_hook is None and self.master_sync is None
+                and self.Bp <= 512 and self.opt is not None and self.opt.kind != _lib.OPT_SGD
+                and sum(w.numel() for w in self.W) <= self.MLP_MAX_PARAMS)
+
+    def _mlp_step(self):
+        a = self._mlp_args
+        if a is None:
+            a = _lib.OcfMlpStepArgs()
+            L = len(self.H)
+            a.n_hidden, a.Bp, a.N, a.Np, a.k_blocks = L, self.Bp, self.N, self.Np, self.k
+            for i, h in enumerate(self.H):
+                a.hidden[i], a.hidden_p[i] = h, self.Hp[i]
+            for i in range(L + 1):
+                sw, sb = self.slots[i]
+                a.W[i], a.b[i] = ptr(self.W[i]), ptr(self.b[i])
+                a.sW1[i], a.sW2[i], a.sb1[i], a.sb2[i] = ptr(sw[0]), ptr(sw[1]), ptr(sb[0]), ptr(sb[1])
+                a.shadow[i] = ptr(self.Wsh[i])
+            a.shadow_blocked = int(self.shadow_blocked)
+            a.act, a.compute_dtype = self.act, self.cdt
+            n = _lib.load().ocf_mlp_step_workspace(a)
+            if n < 0:
+                raise _lib.OcfError("ocf_mlp_step_workspace: " + _lib.load().ocf_last_error().decode())
+            self._mlp_work = torch.empty(max(int(n), 1), dtype=torch.uint8, device=self.dev)
+            self._mlp_bar = torch.zeros(2, dtype=torch.int32, device=self.dev)
+            a.work, a.work_bytes, a.barrier = ptr(self._mlp_work), int(n), ptr(self._mlp_bar)
+            self._mlp_args = a
+        p, ld, rp, om, tg = self._mlp_batch
+        a.B = self.rows_real or self.B
+        a.x[0], a.x[1], a.x[2] = p[0], p[1], p[2]
+        a.ld_x, a.rows, a.out_mask, a.targets, a.ld_t = ld, rp, om, tg, ld
+        o = self.opt.step_params(2.0 / ((self.rows_real or self.B) * self.N_total), 0.0)
+        a.opt = o
+        self._grow_stats(self.n_stats + 1)
+        a.stats = self._stats_row(self.n_stats)
+        with self.phase("mlp_step"):
+            call("ocf_mlp_step", a, cur_stream())
+        self._pending_pack = None
+        self._xin_clean = False
+        self.n_stats += 1
+        self.opt.iterations += 1
+        self.step_count += 1
 
     # ---------------------------------------------------------------- GEMM helper
     def _gemm(self, A, a_col, lda, Bm, b_dtype, b_col, ldb, M, N, K, epi, **kw):
@@ -670,6 +738,7 @@ class Engine:
     # ---------------------------------------------------------------- forward
     def forward(self, training):
         """Encoder stack; leaves h[-1] (compute dtype) for the output layer."""
+        self._pack_pending()
         s = cur_stream()
         Bp, L = self.Bp, len(self.H)
         keep = self.keep if training else 1.0
@@ -1164,6 +1233,8 @@ class Engine:
 
     # ---------------------------------------------------------------- steps
     def train_step(self, grads_out=None):
+        if grads_out is None and self._mlp_ok():
+            return self._mlp_step()
         self._fused_step = grads_out is None
         if self.l2:
             self._l2_penalty()

@@ -56,6 +56,7 @@ class ModelABI:
         self.real = [self.k * self.N] + self.H + [self.N]
         self.Np = self.shapes[-1][1]
         self.step = 0
+        self._bufs = {}
         self.opt = None
         if optimizer is not None:
             self.set_optimizer(optimizer)
@@ -97,10 +98,18 @@ class ModelABI:
         self.slots = [[torch.zeros_like(p) for _ in range(opt.n_slots)] + [None] * (2 - opt.n_slots)
                       for p in self.W + self.b]
 
+    def _out(self, name, *shape):
+        """a reused output buffer: the calls write every element they own (ocf.h: pred / out_grad for b < B,
+        n < N, all 4 + 3 B stats), so nothing is zero-filled per call"""
+        t = self._bufs.get(name)
+        if t is None or tuple(t.shape) != shape:
+            t = self._bufs[name] = torch.empty(*shape, device=self.dev, dtype=torch.float32)
+        return t
+
     # the five calls
     def forward(self, inputs, out_mask, B, training, masks_out=None):
         s = torch.cuda.current_stream().cuda_stream
-        self.pred = torch.zeros(B, self.N, device=self.dev)
+        self.pred = self._out("pred", B, self.N)
         ins = (ctypes.c_void_p * self.k)(*[ptr(x) for x in inputs])
         mo = None
         if masks_out is not None:
@@ -115,8 +124,8 @@ class ModelABI:
         # views with a padded stride)
         targets = targets if targets.stride(0) == self.N else targets.contiguous()
         out_mask = out_mask if out_mask is None or out_mask.stride(0) == self.N else out_mask.contiguous()
-        self.grad = torch.zeros(B, self.N, device=self.dev)
-        self.stats = torch.zeros(4 + 3 * B, device=self.dev)
+        self.grad = self._out("grad", B, self.N)
+        self.stats = self._out("stats", 4 + 3 * B)
         call("ocf_masked_mse", ptr(pred), ptr(targets), ptr(out_mask), self.N, B, self.N, ptr(self.grad), self.N,
              ptr(self.stats), s)
         return self.grad, self.stats
