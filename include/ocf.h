@@ -627,6 +627,8 @@ typedef struct OcfMlpStepArgs {
   void* work; int64_t work_bytes;
   uint32_t* barrier;
   int wgs;                                        /* persistent workgroups (0: library choice) */
+  uint64_t* trace;                                /* (nullable) device uint64[24]: workgroup 0's constant-rate
+                                                   * clock (100 MHz) at the start and after each phase */
 } OcfMlpStepArgs;
 int64_t ocf_mlp_step_workspace(const OcfMlpStepArgs* args);
 int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);

@@ -172,7 +172,7 @@ class OcfMlpStepArgs(ctypes.Structure):
                 ("out_mask", P), ("targets", P), ("ld_t", I64), ("W", P * _L), ("b", P * _L), ("sW1", P * _L),
                 ("sW2", P * _L), ("sb1", P * _L), ("sb2", P * _L), ("shadow", P * _L), ("shadow_blocked", I32),
                 ("act", I32), ("compute_dtype", I32), ("opt", OcfOptParams), ("stats", P), ("work", P),
-                ("work_bytes", I64), ("barrier", P), ("wgs", I32)]
+                ("work_bytes", I64), ("barrier", P), ("wgs", I32), ("trace", P)]
 
 
 ASYNC_MLP_BARRIER = 2          # ocf.h OCF_ASYNC_MLP_BARRIER

@@ -100,6 +100,7 @@ class Engine:
         # the fused one-launch step (ocf_mlp_step) instead
         self._pending_pack = self._mlp_batch = self._mlp_args = None
         self.fused_mlp = True
+        self.mlp_trace = None
         self.act = _lib.ACT[activation]
         self.activation = activation
         self.dropout = dropout
@@ -700,6 +701,7 @@ class Engine:
         a.ld_x, a.rows, a.out_mask, a.targets, a.ld_t = ld, rp, om, tg, ld
         o = self.opt.step_params(2.0 / ((self.rows_real or self.B) * self.N_total), 0.0)
         a.opt = o
+        a.trace = ptr(self.mlp_trace)          # (diagnostics: tools/mlp_trace.py)
         self._grow_stats(self.n_stats + 1)
         a.stats = self._stats_row(self.n_stats)
         with self.phase("mlp_step"):
