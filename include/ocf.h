@@ -597,9 +597,11 @@ int ocf_backward(OcfCtx* ctx, const float* grad, int64_t ld_grad, int B, float g
  * Model.fit's batches: train_jester.py:44-79 with model.py:64-86, train.py:49 and the Keras update) in ONE
  * launch: a persistent grid of `wgs` workgroups runs the forward layers, the masked MSE with the step's
  * statistics, the backward pass and every weight / bias update as phases separated by grid barriers
- * (2 L + 1 barriers for L hidden layers).  Each phase's work is 32 x 32 output tiles, one per wave, on MFMA
- * (v_mfma_f32_32x32x16_{f16,bf16} on operands rounded to the compute dtype, v_mfma_f32_32x32x2_f32 in the
- * exact-fp32 mode); a layer's weights are updated only after the phase that still reads them.  For models
+ * (2 L + 1 barriers for L hidden layers).  Each phase's work is 32 x 32 output tiles, one per workgroup with
+ * the reduction dimension split over its four waves, on MFMA (v_mfma_f32_32x32x16_{f16,bf16} on operands
+ * rounded to the compute dtype, v_mfma_f32_32x32x2_f32 in the exact-fp32 mode); values handed from one phase
+ * to the next are stored write-through; a layer's weights are updated only after the phase that still reads
+ * them.  For models
  * whose weights fit in L2 (0.14 M parameters) the step is latency-bound: one launch instead of ~14.
  * The batch is gathered from device-resident arrays by row index (Model.fit's data path): input block j of
  * batch row b is x[j] + rows[b] * ld_x (N values), its output mask / targets out_mask / targets + rows[b] *
@@ -626,7 +628,8 @@ typedef struct OcfMlpStepArgs {
   float* stats;
   void* work; int64_t work_bytes;
   uint32_t* barrier;
-  int wgs;                                        /* persistent workgroups (0: library choice) */
+  int wgs;                                        /* persistent workgroups (0: one per tile of the busiest
+                                                   * phase, at most 128; never more than the CU count) */
   uint64_t* trace;                                /* (nullable) device uint64[24]: workgroup 0's constant-rate
                                                    * clock (100 MHz) at the start and after each phase */
 } OcfMlpStepArgs;

@@ -17,6 +17,7 @@
 // (Keras computes every gradient from the weights before the step, train.py:50-51: a layer's weights
 // change only after the phase that last reads them.)  Gradients are carried unscaled (e * M) and the
 // MSE's 2 / (B N) applied in fp32 at the update, as on the other paths.
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 
@@ -47,8 +48,9 @@ struct P {
   float* h[MAXL];         // h[i]: [Bp][dim[i+1]] (i < L)
   float* d[MAXL + 1];     // d[i]: delta of layer i's output, [Bp][dim[i+1]] (i <= L)
   float* g[MAXL];         // g[i]: dW_i scratch (1 <= i <= L), W_i's layout
+  float* colp[MAXL + 1];  // colp[i]: [Bp / 32][dim[i+1]] column sums of delta_i per 32-row tile (bias gradients)
   float* rowp;            // [Np / 32][Bp] per column-tile row sse
-  float* totp;            // [tiles][3] per output tile sse / sae / count
+  float* totp;            // [tiles][waves][3] per output tile and wave sse / sae / count
   uint32_t* bar; uint32_t* err; int max_polls;
   uint64_t* trace;
 };
@@ -59,20 +61,27 @@ __device__ __forceinline__ void mark(const P& p, int& n) {
   ++n;
 }
 
-// ---- grid barrier: arrive-count + generation (the last arrival clears the count and bumps the
-// generation, so the words are ready for the next barrier and the next launch); agent-scope release /
-// acquire so every workgroup's stores of the phase are visible to every XCD afterwards.  Bounded: a
-// workgroup that gives up (not all workgroups resident) records the error word and continues.
+// ---- hand-offs between phases.  Every value one workgroup writes for another (activations, deltas, scratch
+// gradients, column / row / tile partials) is stored write-through (sc1: a relaxed agent-scope store), so no
+// workgroup has to write its XCD's L2 back at a barrier; every storing wave drains its stores (vmcnt(0))
+// before the workgroup arrives, and every workgroup invalidates its L1 (agent acquire) when it leaves.
+__device__ __forceinline__ void pub(float* q, float v) {
+  __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// grid barrier: arrive-count + generation (the last arrival clears the count and bumps the generation, so
+// the words are ready for the next barrier and the next launch).  Bounded: a workgroup that gives up (not all
+// workgroups resident) records the error word and continues.
 __device__ __forceinline__ void grid_sync(const P& p, int& tn) {
   mark(p, tn);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's write-through stores have landed
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t gen = __hip_atomic_load(&p.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    const uint32_t arrived = __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    const uint32_t arrived = __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
     if (arrived == gridDim.x) {
       __hip_atomic_store(&p.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&p.bar[1], gen + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&p.bar[1], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       int it = 0;
       while (__hip_atomic_load(&p.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
@@ -84,95 +93,147 @@ __device__ __forceinline__ void grid_sync(const P& p, int& tn) {
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the L1 invalidate has completed
   }
   __syncthreads();
   mark(p, tn);
 }
 
-// ---- one 64 x 64 tile of C = A B per workgroup: K in chunks of KC staged through LDS (every thread issues its
-// 16 loads of a chunk together, in the source's contiguous direction), each wave then runs its 32 x 32
-// quarter on MFMA from LDS.  a(m, k) / b(k, n) return fp32 values, rounded to CT when staged (as the MFMA
-// operand staging of the other paths rounds them); A_MFAST / B_NFAST: the source is contiguous along m / n.
-constexpr int TT = 64, KC = 64;
+// ---- one 32 x 32 tile of C = A B per workgroup, K split over the 4 waves (a wave's quarter of K in chunks of
+// KC staged through the wave's own LDS region, then MFMA from LDS); the four partial tiles are summed in wave
+// order through LDS.  A phase of the Jester model has 16-96 such tiles, so every workgroup of the grid has
+// work and a wave walks one or two chunks instead of a workgroup walking the whole K.
+// a(r, k) / b(n, k) return 4 consecutive fp32 elements along the operand's contiguous direction (r .. r+3 when
+// A_RFAST / B_NFAST, else k .. k+3), rounded to CT when staged (as the MFMA operand staging of the other paths).
+// Every lane issues all of a chunk's loads before it writes any (the accessors are branch-free).
+constexpr int TT = 32;
 template <typename CT> struct Lds {
-  static constexpr int PAD = sizeof(CT) == 2 ? 8 : 4;      // row stride 144 B (16-bit) / 272 B (fp32)
-  static constexpr int STRIDE = KC + PAD;
-  static constexpr int BYTES = 2 * TT * STRIDE * (int)sizeof(CT);
+  static constexpr int KC = sizeof(CT) == 2 ? 64 : 32;     // a wave's K chunk
+  static constexpr int PAD = sizeof(CT) == 2 ? 8 : 4;
+  static constexpr int STRIDE = KC + PAD;                  // row stride 144 B (16-bit) / 144 B (fp32)
+  static constexpr int WAVE = 2 * TT * STRIDE;             // a wave's A + B chunk (elements)
+  static constexpr int STAGE_BYTES = WAVES * WAVE * (int)sizeof(CT);
+  static constexpr int RED_BYTES = WAVES * TT * (TT + 1) * 4;
+  static constexpr int BYTES = (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES) + WAVES * TT * 4;
 };
 
-// f(r, k) returns the element's ADDRESS (always a readable location: masked elements point at a zero word), so
-// all 16 loads of a thread go out together before any is used (a value-returning accessor with branches let
-// the compiler serialise them: one L2 / MALL round trip per element)
 template <typename CT, bool FAST_R, typename F>
-__device__ __forceinline__ void stage(CT* dst, int r0, int k0, F&& f) {
-  constexpr int S = Lds<CT>::STRIDE;
-  const int tid = threadIdx.x;
-  const float* ad[16];
+__device__ __forceinline__ void stage(CT* dst, int r0, int k0, int kc, F&& f) {
+  constexpr int S = Lds<CT>::STRIDE, KC = Lds<CT>::KC, RUNS = TT * KC / 4 / 64;
+  const int lane = threadIdx.x & 63;
+  float4 v[RUNS];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int e = tid * 16 + j;
-    const int r = FAST_R ? e % TT : e / KC, k = FAST_R ? e / TT : e % KC;
-    ad[j] = f(r0 + r, k0 + k);
+  for (int j = 0; j < RUNS; ++j) {
+    const int u = lane + 64 * j;
+    int r, k;
+    if (FAST_R) { r = 4 * (u % (TT / 4)); k = u / (TT / 4); }
+    else { r = u / (KC / 4); k = 4 * (u % (KC / 4)); }
+    v[j] = f(r0 + r, k0 + (k < kc ? k : 0));              // past the chunk's end: a valid address, unused
   }
-  float v[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) v[j] = *ad[j];
+  for (int j = 0; j < RUNS; ++j) {
+    const int u = lane + 64 * j;
+    const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    if (FAST_R) {
+      const int r = 4 * (u % (TT / 4)), k = u / (TT / 4);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int e = tid * 16 + j;
-    const int r = FAST_R ? e % TT : e / KC, k = FAST_R ? e / TT : e % KC;
-    dst[r * S + k] = CvtT<CT>::to(v[j]);
+      for (int q = 0; q < 4; ++q) dst[(r + q) * S + k] = CvtT<CT>::to(e[q]);
+    } else {
+      const int r = u / (KC / 4), k = 4 * (u % (KC / 4));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[r * S + k + q] = CvtT<CT>::to(e[q]);
+    }
   }
 }
 
-template <typename CT, bool A_MFAST, bool B_NFAST, typename FA, typename FB>
-__device__ __forceinline__ ocf_f16v wg_tile(char* lds, int m0, int n0, int K, FA&& a, FB&& b) {
-  constexpr int S = Lds<CT>::STRIDE;
-  CT* sA = reinterpret_cast<CT*>(lds);
-  CT* sB = sA + TT * S;
+// the summed tile: thread t holds rows (t >> 5) + 8 j (j < 4) of column t & 31
+struct Tile {
+  float v[4];
+};
+__device__ __forceinline__ int out_row(int j) { return (threadIdx.x >> 5) + 8 * j; }
+__device__ __forceinline__ int out_col() { return threadIdx.x & 31; }
+
+template <typename CT, bool A_RFAST, bool B_NFAST, typename FA, typename FB>
+__device__ __forceinline__ Tile wg_tile(char* lds, int m0, int n0, int K, FA&& a, FB&& b) {
+  constexpr int S = Lds<CT>::STRIDE, KC = Lds<CT>::KC;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, hf = lane >> 5;
-  const int wm = 32 * (wave >> 1), wn = 32 * (wave & 1);
+  CT* sA = reinterpret_cast<CT*>(lds) + wave * Lds<CT>::WAVE;
+  CT* sB = sA + TT * S;
+  const int kw = K / WAVES, kb = wave * kw;             // K % 64 == 0: kw is a multiple of 16
   ocf_f16v acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-  for (int k0 = 0; k0 < K; k0 += KC) {
-    stage<CT, A_MFAST>(sA, m0, k0, a);
-    stage<CT, B_NFAST>(sB, n0, k0, [&](int n, int k) { return b(k, n); });
+  for (int k0 = 0; k0 < kw; k0 += KC) {
+    const int kc = kw - k0 < KC ? kw - k0 : KC;
+    stage<CT, A_RFAST>(sA, m0, kb + k0, kc, a);
+    stage<CT, B_NFAST>(sB, n0, kb + k0, kc, b);
     __syncthreads();
     if constexpr (sizeof(CT) == 2) {
       using V = typename std::conditional<std::is_same<CT, _Float16>::value, ocf_h8, ocf_b8>::type;
-#pragma unroll
-      for (int ks = 0; ks < KC / 16; ++ks) {
+      for (int ks = 0; ks < kc; ks += 16) {
         V fa, fb;
-        const int kk = 16 * ks + 8 * hf;
-        __builtin_memcpy(&fa, sA + (wm + r) * S + kk, 16);
-        __builtin_memcpy(&fb, sB + (wn + r) * S + kk, 16);
+        const int kk = ks + 8 * hf;
+        __builtin_memcpy(&fa, sA + r * S + kk, 16);
+        __builtin_memcpy(&fb, sB + r * S + kk, 16);
         if constexpr (std::is_same<CT, _Float16>::value)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
         else
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
       }
     } else {
-#pragma unroll
-      for (int ks = 0; ks < KC; ks += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[(wm + r) * S + ks + hf], sB[(wn + r) * S + ks + hf], acc, 0, 0, 0);
+      for (int ks = 0; ks < kc; ks += 2)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[r * S + ks + hf], sB[r * S + ks + hf], acc, 0, 0, 0);
     }
     __syncthreads();
   }
-  return acc;
+  // the four K quarters, summed in wave order (C layout of v_mfma_f32_32x32x*: register q holds row
+  // (q & 3) + 8 (q >> 2) + 4 hf, column r)
+  float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) red[(wave * TT + (q & 3) + 8 * (q >> 2) + 4 * hf) * (TT + 1) + r] = acc[q];
+  __syncthreads();
+  Tile t;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int rr = out_row(j), cc = out_col();
+    float s = red[rr * (TT + 1) + cc];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) s += red[(w * TT + rr) * (TT + 1) + cc];
+    t.v[j] = s;
+  }
+  __syncthreads();
+  return t;
 }
-// accumulator register -> (row, col) of the workgroup tile (C layout of v_mfma_f32_32x32x*, the wave's quarter)
-__device__ __forceinline__ int tile_row(int reg) {
-  return 32 * ((threadIdx.x >> 6) >> 1) + (reg & 3) + 8 * (reg >> 2) + 4 * ((threadIdx.x & 63) >> 5);
+
+// the column sums of the summed tile over its 32 rows (a thread's rows, then the two half-waves, then the
+// waves in order), written to dst[0..31] by threads 0..31
+template <typename CT>
+__device__ __forceinline__ void tile_colsum(char* lds, const Tile& t, float* dst) {
+  float* cs = reinterpret_cast<float*>(lds + Lds<CT>::BYTES - WAVES * TT * 4);
+  float s = (t.v[0] + t.v[1]) + (t.v[2] + t.v[3]);
+  s += __shfl_xor(s, 32, 64);
+  if ((threadIdx.x & 63) < 32) cs[(threadIdx.x >> 6) * TT + out_col()] = s;
+  __syncthreads();
+  if (threadIdx.x < TT) {
+    float c = cs[threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < WAVES; ++w) c += cs[w * TT + threadIdx.x];
+    pub(&dst[threadIdx.x], c);
+  }
 }
-__device__ __forceinline__ int tile_col() { return 32 * ((threadIdx.x >> 6) & 1) + (threadIdx.x & 31); }
+
+__device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast<const float4*>(q); }
 
 // ---- operand views
-// layer-0 input of batch row b, padded column c (block c / Np): its address, or the zero word when padding
-__device__ __forceinline__ const float* x_ptr(const P& p, int b, int c) {
+// layer-0 input of batch row b, padded columns c .. c+3 (one block: Np % 4 == 0); zero past the batch and in
+// the block padding (element loads through selected addresses: no branches, the four loads go out together)
+__device__ __forceinline__ float4 x4(const P& p, int b, int c) {
   const int blk = c / p.Np, n = c - blk * p.Np;
-  const int64_t row = p.rows[b < p.B ? b : p.B - 1];
-  return (b < p.B && n < p.N) ? p.x[blk] + row * p.ld_x + n : g_zero;
+  const float* row = p.x[blk] + p.rows[b < p.B ? b : p.B - 1] * p.ld_x;
+  float e[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) e[q] = *((b < p.B && n + q < p.N) ? row + n + q : g_zero);
+  return make_float4(e[0], e[1], e[2], e[3]);
 }
 __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c) {
   const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
@@ -180,21 +241,21 @@ __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c)
   return ((int64_t)(r >> 6) * (C >> 6) + (c >> 6)) * 4096 + (r & 63) * 64 + (c & 63);
 }
 
-// the update of the 16 elements of weight i an MFMA accumulator covers, from their gradients (rows r[q], column c
-// of a [R][C] weight): every load first, then the updates and the stores
+// the update of a thread's 4 elements of weight i from their gradients (rows r[q], column c of a [R][C] weight):
+// every load first, then the updates and the stores
 template <typename CT, int KIND>
 __device__ __forceinline__ void update_tile(const P& p, int i, const float* g, const int* r, int c) {
   const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
-  float w[16], a[16], bb[16];
+  float w[4], a[4], bb[4];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < 4; ++q) {
     const int64_t e = (int64_t)r[q] * C + c;
     w[q] = p.W[i][e];
     a[q] = p.sW1[i] ? p.sW1[i][e] : 0.f;
     bb[q] = p.sW2[i] ? p.sW2[i][e] : 0.f;
   }
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int q = 0; q < 4; ++q) {
     const int64_t e = (int64_t)r[q] * C + c;
     opt_update_k<KIND>(p.op, g[q], w[q], a[q], bb[q]);
     p.W[i][e] = w[q];
@@ -205,20 +266,18 @@ __device__ __forceinline__ void update_tile(const P& p, int i, const float* g, c
   }
 }
 
-// bias i: db[n] = gscale * sum_b delta_i[b][n] (batch rows in order; loads 16 at a time), then the update
+// bias i: db[n] = gscale * sum over the Bp / 32 row tiles of the column partials the producer of delta_i wrote
+// (tile order), then the update
 template <int KIND>
 __device__ __forceinline__ void bias_update(const P& p, int i, int gtid, int gthreads) {
-  const int W = p.dim[i + 1], realw = p.real[i + 1];
+  const int W = p.dim[i + 1], realw = p.real[i + 1], nb = p.Bp / TT;
   for (int n = gtid; n < realw; n += gthreads) {
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = j < nb ? p.colp[i][(int64_t)j * W + n] : 0.f;
     float s = 0.f;
-    for (int b0 = 0; b0 < p.Bp; b0 += 16) {       // padded rows hold zero deltas
-      float v[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = p.d[i][(int64_t)(b0 + j) * W + n];
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (b0 + j < p.B) s += v[j];
-    }
+    for (int j = 0; j < 16; ++j) s += v[j];
     float w = p.b[i][n], a = p.sb1[i] ? p.sb1[i][n] : 0.f, bb = p.sb2[i] ? p.sb2[i][n] : 0.f;
     opt_update_k<KIND>(p.op, s * p.op.gscale, w, a, bb);
     p.b[i][n] = w;
@@ -262,6 +321,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
   const int gtid = blockIdx.x * THREADS + threadIdx.x, gthreads = gridDim.x * THREADS;
   const int L = p.L, Bt = p.Bp / TT;
   const float gs = p.op.gscale;
+  const int c = out_col();
   int tn = 0;
   mark(p, tn);
 
@@ -270,69 +330,70 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     const int K = p.dim[i], Wd = p.dim[i + 1], nt = Wd / TT;
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
-      ocf_f16v acc;
+      Tile v;
       if (i == 0)
-        acc = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x_ptr(p, m, k); },
-                                       [&](int k, int n) { return p.W[0] + (int64_t)k * Wd + n; });
+        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4(p, m, k); },
+                                     [&](int n, int k) { return ld4(p.W[0] + (int64_t)k * Wd + n); });
       else
-        acc = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return p.h[i - 1] + (int64_t)m * K + k; },
-                                       [&](int k, int n) { return p.W[i] + (int64_t)k * Wd + n; });
-      const int n = n0 + tile_col();
+        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return ld4(p.h[i - 1] + (int64_t)m * K + k); },
+                                     [&](int n, int k) { return ld4(p.W[i] + (int64_t)k * Wd + n); });
+      const int n = n0 + c;
       const float bias = p.b[i][n];
       const bool live_n = n < p.real[i + 1];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + tile_row(q);
-        const float v = (m < p.B && live_n) ? act_apply(p.act, acc[q] + bias) : 0.f;
-        p.h[i][(int64_t)m * Wd + n] = v;
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + out_row(j);
+        pub(&p.h[i][(int64_t)m * Wd + n], (m < p.B && live_n) ? act_apply(p.act, v.v[j] + bias) : 0.f);
       }
     }
     grid_sync(p, tn);
   }
-  // ---- output layer + masked MSE: y = M (h W_L + b_L); e = y - T; delta_L = e M; per-tile statistics
+  // ---- output layer + masked MSE: y = M (h W_L + b_L); e = y - T; delta_L = e M; per-tile statistics and
+  // the column sums of delta_L (b_L's gradient)
   {
     const int K = p.dim[L], nt = p.Np / TT;
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
-      // W_L is stored transposed ([Np][K]): B(k, n) = W_L[n][k], contiguous along k
-      const ocf_f16v acc = wg_tile<CT, false, false>(lds, m0, n0, K,
-                                                     [&](int m, int k) { return p.h[L - 1] + (int64_t)m * K + k; },
-                                                     [&](int k, int n) { return p.W[L] + (int64_t)n * K + k; });
-      const int n = n0 + tile_col();
+      // W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k], contiguous along k
+      const Tile v = wg_tile<CT, false, false>(lds, m0, n0, K,
+                                               [&](int m, int k) { return ld4(p.h[L - 1] + (int64_t)m * K + k); },
+                                               [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); });
+      const int n = n0 + c;
       const float bias = p.b[L][n];
-      float sse = 0.f, sae = 0.f, cnt = 0.f, rs[16], mkv[16], ttv[16];
+      float mkv[4], ttv[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {       // the mask / target loads first (clamped rows: always in bounds)
-        const int m = m0 + tile_row(q);
+      for (int j = 0; j < 4; ++j) {        // the mask / target loads first (clamped: always in bounds)
+        const int m = m0 + out_row(j);
         const int64_t o = p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
-        mkv[q] = p.om[o];
-        ttv[q] = p.tg[o];
+        mkv[j] = p.om[o];
+        ttv[j] = p.tg[o];
       }
+      Tile dl;
+      float sse = 0.f, sae = 0.f, cnt = 0.f, rs[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + tile_row(q);
-        float dl = 0.f, se = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + out_row(j);
+        float d = 0.f, se = 0.f;
         if (m < p.B && n < p.N) {
-          const float mk = mkv[q], tt = ttv[q];
-          const float y = mk * (acc[q] + bias);
-          const float e = y - tt;
+          const float y = mkv[j] * (v.v[j] + bias);
+          const float e = y - ttv[j];
           se = e * e;
           sse += se;
           sae += fabsf(e);
-          cnt += (tt + y != 0.f) ? 1.f : 0.f;
-          dl = e * mk;
+          cnt += (ttv[j] + y != 0.f) ? 1.f : 0.f;
+          d = e * mkv[j];
         }
-        p.d[L][(int64_t)m * p.Np + n] = dl;
-        rs[q] = se;
+        pub(&p.d[L][(int64_t)m * p.Np + n], d);
+        dl.v[j] = d;
+        rs[j] = se;
       }
-      // row sums over the wave's 32 columns (the 32 lanes of each half-wave), in a fixed butterfly order
+      // row sums over the tile's 32 columns (the 32 lanes of each half-wave), in a fixed butterfly order
       for (int o = 16; o > 0; o >>= 1)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) rs[q] += __shfl_xor(rs[q], o, 64);
-      const int ct = n0 / 32 + (wave & 1);        // the wave's 32-column block
+        for (int j = 0; j < 4; ++j) rs[j] += __shfl_xor(rs[j], o, 64);
       if ((lane & 31) == 0)
 #pragma unroll
-        for (int q = 0; q < 16; ++q) p.rowp[(int64_t)ct * p.Bp + m0 + tile_row(q)] = rs[q];
+        for (int j = 0; j < 4; ++j) pub(&p.rowp[(int64_t)(n0 / TT) * p.Bp + m0 + out_row(j)], rs[j]);
       for (int o = 32; o > 0; o >>= 1) {
         sse += __shfl_xor(sse, o, 64);
         sae += __shfl_xor(sae, o, 64);
@@ -340,10 +401,11 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
       if (lane == 0) {
         const int64_t slot = (int64_t)t * WAVES + wave;
-        p.totp[slot * 3 + 0] = sse;
-        p.totp[slot * 3 + 1] = sae;
-        p.totp[slot * 3 + 2] = cnt;
+        pub(&p.totp[slot * 3 + 0], sse);
+        pub(&p.totp[slot * 3 + 1], sae);
+        pub(&p.totp[slot * 3 + 2], cnt);
       }
+      tile_colsum<CT>(lds, dl, p.colp[L] + (int64_t)(m0 / TT) * p.Np + n0);
     }
     grid_sync(p, tn);
   }
@@ -354,9 +416,9 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       const int R = i + 1 == L ? p.dim[L + 1] : p.dim[i + 1], C = i + 1 == L ? p.dim[L] : p.dim[i + 2];
       update_from<CT, KIND>(p, i + 1, p.g[i + 1], (int64_t)R * C, gtid, gthreads);
     }
-    if (i == L && blockIdx.x == 0 && wave == 0) {
+    if (i == L && blockIdx.x == gridDim.x - 1 && wave == 0) {
       // the step's statistics from the per-wave partials, in order
-      const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / 32;
+      const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / TT;
       float a[3] = {0.f, 0.f, 0.f};
       for (int t = lane; t < slots; t += 64)
         for (int k = 0; k < 3; ++k) a[k] += p.totp[(int64_t)t * 3 + k];
@@ -370,14 +432,14 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
       for (int b = lane; b < p.Bp; b += 64) {
         float r = 0.f;
-        for (int c = 0; c < ncb; ++c) r += p.rowp[(int64_t)c * p.Bp + b];
+        for (int cb = 0; cb < ncb; ++cb) r += p.rowp[(int64_t)cb * p.Bp + b];
         p.stats[4 + b] = r;
       }
     }
     bias_update<KIND>(p, i, gtid, gthreads);
     const int Wi = p.dim[i + 1];                 // layer i's output width (padded)
     const int Ki = p.dim[i];                     // its input width
-    // delta of layer i - 1's output: (delta_i W_i^T) * act'(h_{i-1})
+    // delta of layer i - 1's output: (delta_i W_i^T) * act'(h_{i-1}), with its column sums
     const int nd = i > 0 ? (Bt * (Ki / TT)) : 0;
     // dW_i: [input][output] (layer L: [output][input]) tiles, K = the batch rows
     const int gr = i == L ? Wi : Ki, gc = i == L ? Ki : Wi;
@@ -385,48 +447,50 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     for (int t = blockIdx.x; t < nd + ng; t += gridDim.x) {
       if (t < nd) {
         const int ct = Ki / TT, m0 = (t / ct) * TT, n0 = (t % ct) * TT;
-        ocf_f16v acc;
-        if (i == L)      // B(k = output unit, n = input unit) = W_L[k][n], contiguous along n
-          acc = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return p.d[i] + (int64_t)m * Wi + k; },
-                                         [&](int k, int n) { return p.W[L] + (int64_t)k * Ki + n; });
-        else             // B(k = output unit, n = input unit) = W_i[n][k], contiguous along k
-          acc = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return p.d[i] + (int64_t)m * Wi + k; },
-                                          [&](int k, int n) { return p.W[i] + (int64_t)n * Wi + k; });
-        const int n = n0 + tile_col();
-        float hv[16];
+        Tile v;
+        if (i == L)      // B(n = input unit, k = output unit) = W_L[k][n], contiguous along n
+          v = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return ld4(p.d[i] + (int64_t)m * Wi + k); },
+                                       [&](int n, int k) { return ld4(p.W[L] + (int64_t)k * Ki + n); });
+        else             // B(n = input unit, k = output unit) = W_i[n][k], contiguous along k
+          v = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return ld4(p.d[i] + (int64_t)m * Wi + k); },
+                                        [&](int n, int k) { return ld4(p.W[i] + (int64_t)n * Wi + k); });
+        const int n = n0 + c;
+        float hv[4];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) hv[q] = p.h[i - 1][(int64_t)(m0 + tile_row(q)) * Ki + n];
+        for (int j = 0; j < 4; ++j) hv[j] = p.h[i - 1][(int64_t)(m0 + out_row(j)) * Ki + n];
+        Tile dv;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int m = m0 + tile_row(q);
-          p.d[i - 1][(int64_t)m * Ki + n] = (m < p.B && n < p.real[i]) ? acc[q] * act_grad(p.act, hv[q]) : 0.f;
+        for (int j = 0; j < 4; ++j) {
+          const int m = m0 + out_row(j);
+          dv.v[j] = (m < p.B && n < p.real[i]) ? v.v[j] * act_grad(p.act, hv[j]) : 0.f;
+          pub(&p.d[i - 1][(int64_t)m * Ki + n], dv.v[j]);
         }
+        tile_colsum<CT>(lds, dv, p.colp[i - 1] + (int64_t)(m0 / TT) * Ki + n0);
         continue;
       }
       const int u = t - nd, ct = gc / TT, m0 = (u / ct) * TT, n0 = (u % ct) * TT;
-      ocf_f16v acc;
+      Tile v;
       if (i == L)        // dW_L[n][j] = sum_b delta_L[b][n] h_{L-1}[b][j]
-        acc = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return p.d[L] + (int64_t)k * Wi + m; },
-                                      [&](int k, int n) { return p.h[L - 1] + (int64_t)k * Ki + n; });
+        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ld4(p.d[L] + (int64_t)k * Wi + m); },
+                                    [&](int n, int k) { return ld4(p.h[L - 1] + (int64_t)k * Ki + n); });
       else if (i > 0)    // dW_i[k][j] = sum_b h_{i-1}[b][k] delta_i[b][j]
-        acc = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return p.h[i - 1] + (int64_t)k * Ki + m; },
-                                      [&](int k, int n) { return p.d[i] + (int64_t)k * Wi + n; });
+        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ld4(p.h[i - 1] + (int64_t)k * Ki + m); },
+                                    [&](int n, int k) { return ld4(p.d[i] + (int64_t)k * Wi + n); });
       else               // dW_0[k][j] = sum_b x[b][k] delta_0[b][j]
-        acc = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x_ptr(p, k, m); },
-                                      [&](int k, int n) { return p.d[0] + (int64_t)k * Wi + n; });
-      const int c = n0 + tile_col();
+        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4(p, k, m); },
+                                    [&](int n, int k) { return ld4(p.d[0] + (int64_t)k * Wi + n); });
       if (i == 0) {      // nothing reads W_0 any more: update it from the tile (padded elements have zero gradient)
-        float gv[16];
-        int rr[16];
+        float gv[4];
+        int rr[4];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          gv[q] = acc[q] * gs;
-          rr[q] = m0 + tile_row(q);
+        for (int j = 0; j < 4; ++j) {
+          gv[j] = v.v[j] * gs;
+          rr[j] = m0 + out_row(j);
         }
-        update_tile<CT, KIND>(p, 0, gv, rr, c);
+        update_tile<CT, KIND>(p, 0, gv, rr, n0 + c);
       } else {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) p.g[i][(int64_t)(m0 + tile_row(q)) * gc + c] = acc[q] * gs;
+        for (int j = 0; j < 4; ++j) pub(&p.g[i][(int64_t)(m0 + out_row(j)) * gc + n0 + c], v.v[j] * gs);
       }
     }
     if (i > 0) grid_sync(p, tn);
@@ -435,7 +499,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
 }
 
 struct Layout {
-  size_t h[MAXL], d[MAXL + 1], g[MAXL], rowp, totp, total;
+  size_t h[MAXL], d[MAXL + 1], g[MAXL], colp[MAXL + 1], rowp, totp, total;
 };
 Layout layout(const OcfMlpStepArgs& a, int* dim) {
   Layout w{};
@@ -449,8 +513,9 @@ Layout layout(const OcfMlpStepArgs& a, int* dim) {
   for (int i = 0; i < L; ++i) w.h[i] = take((size_t)a.Bp * dim[i + 1]);
   for (int i = 0; i <= L; ++i) w.d[i] = take((size_t)a.Bp * dim[i + 1]);
   for (int i = 1; i <= L; ++i) w.g[i] = take((size_t)dim[i] * dim[i + 1]);
-  w.rowp = take((size_t)(a.Np / 32) * a.Bp);
-  w.totp = take((size_t)(a.Bp / 64) * (a.Np / 64) * 4 * 3);
+  for (int i = 0; i <= L; ++i) w.colp[i] = take((size_t)(a.Bp / TT) * dim[i + 1]);
+  w.rowp = take((size_t)(a.Np / TT) * a.Bp);
+  w.totp = take((size_t)(a.Bp / TT) * (a.Np / TT) * WAVES * 3);
   w.total = off;
   return w;
 }
@@ -529,6 +594,7 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   for (int i = 0; i < p.L; ++i) p.h[i] = reinterpret_cast<float*>(ws + w.h[i]);
   for (int i = 0; i <= p.L; ++i) p.d[i] = reinterpret_cast<float*>(ws + w.d[i]);
   for (int i = 1; i <= p.L; ++i) p.g[i] = reinterpret_cast<float*>(ws + w.g[i]);
+  for (int i = 0; i <= p.L; ++i) p.colp[i] = reinterpret_cast<float*>(ws + w.colp[i]);
   p.rowp = reinterpret_cast<float*>(ws + w.rowp);
   p.totp = reinterpret_cast<float*>(ws + w.totp);
   for (int j = 0; j < 3; ++j) p.x[j] = a->x[j];
@@ -544,8 +610,16 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   p.err = async_error_word();
   p.max_polls = 1 << 22;
   p.trace = a->trace;
-  // every workgroup must be resident for the grid barriers: a few dozen on 256 CUs
-  int wgs = a->wgs > 0 ? a->wgs : 64;
+  // every workgroup must be resident for the grid barriers; by default one per tile of the busiest phase, at
+  // most 128 (the barriers' arrivals grow with the grid)
+  int tiles = 0;
+  {
+    const int bt = p.Bp / mlp::TT;
+    for (int i = 0; i <= p.L; ++i) tiles = std::max(tiles, bt * (p.dim[i + 1] / mlp::TT));
+    for (int i = p.L; i >= 0; --i)
+      tiles = std::max(tiles, (i > 0 ? bt * (p.dim[i] / mlp::TT) : 0) + (p.dim[i] / mlp::TT) * (p.dim[i + 1] / mlp::TT));
+  }
+  int wgs = a->wgs > 0 ? a->wgs : std::min(tiles, 128);
   int cus = 0, dev = 0;
   OCF_HIP(hipGetDevice(&dev));
   OCF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));

@@ -38,6 +38,6 @@ for s in range(a.steps):
     n = int(np.count_nonzero(t))
     rows.append(np.diff(t[:n]) / 100.0)          # us between marks
 d = np.mean(rows[3:], axis=0)
-print(json.dumps({"dtype": a.dtype, "wgs": a.wgs or 64, "us_between_marks": [round(x, 2) for x in d],
+print(json.dumps({"dtype": a.dtype, "wgs": a.wgs or "default", "us_between_marks": [round(x, 2) for x in d],
                   "total_us": round(float(d.sum()), 2),
                   "marks": "start, then per barrier: arrive, leave; last: end"}))
