@@ -4,16 +4,16 @@
 // with the fused optimizer, bias kernels, stats) is ~14 launches of 2-33 us on a model of 0.14 M
 // parameters (train_jester.py's 200 -> 256 -> 256 -> 100, batch 128): every launch is a handful of
 // workgroups waiting on latency, and the host spends longer issuing them than the GPU running them.
-// Here a grid of a few dozen workgroups stays resident and walks the step's phases, each a set of
-// 32 x 32 output tiles (one MFMA tile per wave, operands straight from the L2-resident weights and
-// activations), separated by grid barriers:
+// Here a grid of up to 128 workgroups stays resident and walks the step's phases, each a set of 32 x 32
+// output tiles (one per workgroup, the reduction dimension split over its four waves, MFMA from LDS;
+// operands from the L2 / MALL-resident weights and activations), separated by grid barriers:
 //   F_0 .. F_{L-1}  h_i = act(h_{i-1} W_i + b_i)                     (model.py:64-71)
-//   OUT             y = M * (h_{L-1} W_L + b_L), e = y - T, delta_L = e * M, the step's statistics
-//                   (model.py:81-86, train.py:49, 102-121)
-//   BACK_L          stats; db_L + its update; delta_{L-1} = (delta_L W_L^T) * act'; dW_L -> scratch
-//   BACK_i          W_{i+1} updated from its scratch gradient (nothing reads it any more); db_i + update;
+//   OUT             y = M * (h_{L-1} W_L + b_L), e = y - T, delta_L = e * M, the step's statistics, the
+//                   column sums of delta_L (model.py:81-86, train.py:49, 102-121)
+//   BACK_L          stats; b_L's update; delta_{L-1} = (delta_L W_L^T) * act' (+ column sums); dW_L -> scratch
+//   BACK_i          W_{i+1} updated from its scratch gradient (nothing reads it any more); b_i's update;
 //                   delta_{i-1}; dW_i -> scratch
-//   BACK_0          W_1 updated; db_0 + update; dW_0 tiles update W_0 directly
+//   BACK_0          W_1 updated; b_0's update; dW_0 tiles update W_0 directly
 // (Keras computes every gradient from the weights before the step, train.py:50-51: a layer's weights
 // change only after the phase that last reads them.)  Gradients are carried unscaled (e * M) and the
 // MSE's 2 / (B N) applied in fp32 at the update, as on the other paths.
@@ -61,42 +61,62 @@ __device__ __forceinline__ void mark(const P& p, int& n) {
   ++n;
 }
 
-// ---- hand-offs between phases.  Every value one workgroup writes for another (activations, deltas, scratch
-// gradients, column / row / tile partials) is stored write-through (sc1: a relaxed agent-scope store), so no
-// workgroup has to write its XCD's L2 back at a barrier; every storing wave drains its stores (vmcnt(0))
-// before the workgroup arrives, and every workgroup invalidates its L1 (agent acquire) when it leaves.
+// ---- hand-offs between phases (MI355X_MICROARCH.md § inter-workgroup visibility, the first row of its
+// table of sc1 hand-offs).  Every value one workgroup writes for another (activations, deltas, scratch
+// gradients, column / row / tile partials) is stored write-through (sc1: a relaxed agent-scope store) and
+// read with L1-bypassing sc1 loads (ldc / ldc4), so a barrier needs neither an L2 write-back on the producer
+// nor an L1 invalidate on the consumer: every storing wave drains its stores (vmcnt(0)), the workgroup
+// meets at a workgroup barrier, one lane adds to the arrival counter, and one lane polls that counter
+// (sc1 loads) until every workgroup has arrived.  Each handed-off word is written once per launch, before
+// any read of it; the launch starts with clean caches.
+constexpr int SC1 = 16;   // cache-policy bits of an L1-bypassing (sc1) access
 __device__ __forceinline__ void pub(float* q, float v) {
   __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs_of(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ float4 ldc4(const float* base, int64_t e) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_of(base), (uint32_t)(e * 4), 0, SC1);
+  float4 r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
+__device__ __forceinline__ float ldc(const float* base, int64_t e) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_of(base), (uint32_t)(e * 4), 0, SC1));
+}
 
-// grid barrier: arrive-count + generation (the last arrival clears the count and bumps the generation, so
-// the words are ready for the next barrier and the next launch).  Bounded: a workgroup that gives up (not all
-// workgroups resident) records the error word and continues.
-__device__ __forceinline__ void grid_sync(const P& p, int& tn) {
+// grid barrier number nb (1, 2, ...) of the launch: bar[0] counts arrivals monotonically within the launch
+// (barrier nb is passed when it reaches nb * grid); the last workgroup to leave the kernel resets it (exit()),
+// so it is zero for the next launch.  Bounded: a workgroup that gives up (not all workgroups resident)
+// records the error word and continues.
+__device__ __forceinline__ void grid_sync(const P& p, int& tn, int& nb) {
   mark(p, tn);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's write-through stores have landed
   __syncthreads();
+  ++nb;
   if (threadIdx.x == 0) {
-    const uint32_t gen = __hip_atomic_load(&p.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t arrived = __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
-    if (arrived == gridDim.x) {
-      __hip_atomic_store(&p.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&p.bar[1], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int it = 0;
-      while (__hip_atomic_load(&p.bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++it > p.max_polls) {
-          __hip_atomic_store(p.err, (uint32_t)OCF_ASYNC_MLP_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
+    const uint32_t target = (uint32_t)nb * gridDim.x;
+    __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int it = 0;
+    while (__hip_atomic_load(&p.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > p.max_polls) {
+        __hip_atomic_store(p.err, (uint32_t)OCF_ASYNC_MLP_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the L1 invalidate has completed
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
   __syncthreads();
   mark(p, tn);
+}
+__device__ __forceinline__ void grid_exit(const P& p, int nb) {
+  if (threadIdx.x == 0) {
+    const uint32_t all = (uint32_t)(nb + 1) * gridDim.x;
+    if (__hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == all)
+      __hip_atomic_store(&p.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---- one 32 x 32 tile of C = A B per workgroup, K split over the 4 waves (a wave's quarter of K in chunks of
@@ -274,7 +294,7 @@ __device__ __forceinline__ void bias_update(const P& p, int i, int gtid, int gth
   for (int n = gtid; n < realw; n += gthreads) {
     float v[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) v[j] = j < nb ? p.colp[i][(int64_t)j * W + n] : 0.f;
+    for (int j = 0; j < 16; ++j) v[j] = j < nb ? ldc(p.colp[i], (int64_t)j * W + n) : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) s += v[j];
@@ -292,7 +312,7 @@ template <typename CT, int KIND>
 __device__ __forceinline__ void update_from(const P& p, int i, const float* g, int64_t n, int gtid, int gthreads) {
   const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
   for (int64_t e0 = (int64_t)gtid * 4; e0 < n; e0 += (int64_t)gthreads * 4) {
-    const float4 gv = *reinterpret_cast<const float4*>(g + e0);
+    const float4 gv = ldc4(g, e0);
     float4 w = *reinterpret_cast<const float4*>(p.W[i] + e0);
     float4 a = p.sW1[i] ? *reinterpret_cast<const float4*>(p.sW1[i] + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 bb = p.sW2[i] ? *reinterpret_cast<const float4*>(p.sW2[i] + e0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -322,7 +342,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
   const int L = p.L, Bt = p.Bp / TT;
   const float gs = p.op.gscale;
   const int c = out_col();
-  int tn = 0;
+  int tn = 0, nb = 0;
   mark(p, tn);
 
   // ---- forward: h_i = act(src W_i + b_i); padded rows / units are zero
@@ -335,7 +355,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4(p, m, k); },
                                      [&](int n, int k) { return ld4(p.W[0] + (int64_t)k * Wd + n); });
       else
-        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return ld4(p.h[i - 1] + (int64_t)m * K + k); },
+        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)m * K + k); },
                                      [&](int n, int k) { return ld4(p.W[i] + (int64_t)k * Wd + n); });
       const int n = n0 + c;
       const float bias = p.b[i][n];
@@ -346,7 +366,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         pub(&p.h[i][(int64_t)m * Wd + n], (m < p.B && live_n) ? act_apply(p.act, v.v[j] + bias) : 0.f);
       }
     }
-    grid_sync(p, tn);
+    grid_sync(p, tn, nb);
   }
   // ---- output layer + masked MSE: y = M (h W_L + b_L); e = y - T; delta_L = e M; per-tile statistics and
   // the column sums of delta_L (b_L's gradient)
@@ -356,7 +376,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
       // W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k], contiguous along k
       const Tile v = wg_tile<CT, false, false>(lds, m0, n0, K,
-                                               [&](int m, int k) { return ld4(p.h[L - 1] + (int64_t)m * K + k); },
+                                               [&](int m, int k) { return ldc4(p.h[L - 1], (int64_t)m * K + k); },
                                                [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); });
       const int n = n0 + c;
       const float bias = p.b[L][n];
@@ -407,7 +427,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
       tile_colsum<CT>(lds, dl, p.colp[L] + (int64_t)(m0 / TT) * p.Np + n0);
     }
-    grid_sync(p, tn);
+    grid_sync(p, tn, nb);
   }
   // ---- backward, layer by layer from the output
   for (int i = L; i >= 0; --i) {
@@ -421,7 +441,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / TT;
       float a[3] = {0.f, 0.f, 0.f};
       for (int t = lane; t < slots; t += 64)
-        for (int k = 0; k < 3; ++k) a[k] += p.totp[(int64_t)t * 3 + k];
+        for (int k = 0; k < 3; ++k) a[k] += ldc(p.totp, (int64_t)t * 3 + k);
       for (int k = 0; k < 3; ++k)
         for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
       if (lane == 0) {
@@ -432,7 +452,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
       for (int b = lane; b < p.Bp; b += 64) {
         float r = 0.f;
-        for (int cb = 0; cb < ncb; ++cb) r += p.rowp[(int64_t)cb * p.Bp + b];
+        for (int cb = 0; cb < ncb; ++cb) r += ldc(p.rowp, (int64_t)cb * p.Bp + b);
         p.stats[4 + b] = r;
       }
     }
@@ -449,15 +469,15 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         const int ct = Ki / TT, m0 = (t / ct) * TT, n0 = (t % ct) * TT;
         Tile v;
         if (i == L)      // B(n = input unit, k = output unit) = W_L[k][n], contiguous along n
-          v = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return ld4(p.d[i] + (int64_t)m * Wi + k); },
+          v = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
                                        [&](int n, int k) { return ld4(p.W[L] + (int64_t)k * Ki + n); });
         else             // B(n = input unit, k = output unit) = W_i[n][k], contiguous along k
-          v = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return ld4(p.d[i] + (int64_t)m * Wi + k); },
+          v = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
                                         [&](int n, int k) { return ld4(p.W[i] + (int64_t)n * Wi + k); });
         const int n = n0 + c;
         float hv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) hv[j] = p.h[i - 1][(int64_t)(m0 + out_row(j)) * Ki + n];
+        for (int j = 0; j < 4; ++j) hv[j] = ldc(p.h[i - 1], (int64_t)(m0 + out_row(j)) * Ki + n);
         Tile dv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -471,14 +491,14 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       const int u = t - nd, ct = gc / TT, m0 = (u / ct) * TT, n0 = (u % ct) * TT;
       Tile v;
       if (i == L)        // dW_L[n][j] = sum_b delta_L[b][n] h_{L-1}[b][j]
-        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ld4(p.d[L] + (int64_t)k * Wi + m); },
-                                    [&](int n, int k) { return ld4(p.h[L - 1] + (int64_t)k * Ki + n); });
+        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.d[L], (int64_t)k * Wi + m); },
+                                    [&](int n, int k) { return ldc4(p.h[L - 1], (int64_t)k * Ki + n); });
       else if (i > 0)    // dW_i[k][j] = sum_b h_{i-1}[b][k] delta_i[b][j]
-        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ld4(p.h[i - 1] + (int64_t)k * Ki + m); },
-                                    [&](int n, int k) { return ld4(p.d[i] + (int64_t)k * Wi + n); });
+        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)k * Ki + m); },
+                                    [&](int n, int k) { return ldc4(p.d[i], (int64_t)k * Wi + n); });
       else               // dW_0[k][j] = sum_b x[b][k] delta_0[b][j]
         v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4(p, k, m); },
-                                    [&](int n, int k) { return ld4(p.d[0] + (int64_t)k * Wi + n); });
+                                    [&](int n, int k) { return ldc4(p.d[0], (int64_t)k * Wi + n); });
       if (i == 0) {      // nothing reads W_0 any more: update it from the tile (padded elements have zero gradient)
         float gv[4];
         int rr[4];
@@ -493,8 +513,9 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         for (int j = 0; j < 4; ++j) pub(&p.g[i][(int64_t)(m0 + out_row(j)) * gc + n0 + c], v.v[j] * gs);
       }
     }
-    if (i > 0) grid_sync(p, tn);
+    if (i > 0) grid_sync(p, tn, nb);
   }
+  grid_exit(p, nb);
   mark(p, tn);
 }
 
