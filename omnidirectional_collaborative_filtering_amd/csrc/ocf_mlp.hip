@@ -261,30 +261,34 @@ __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c)
   return ((int64_t)(r >> 6) * (C >> 6) + (c >> 6)) * 4096 + (r & 63) * 64 + (c & 63);
 }
 
-// the update of a thread's 4 elements of weight i from their gradients (rows r[q], column c of a [R][C] weight):
-// every load first, then the updates and the stores
+// the update of a thread's 4 elements of weight i (rows r[q], column c of a [R][C] weight): the parameters and
+// slots are loaded before the tile's GEMM (load), the update applied from its gradients after it (apply)
 template <typename CT, int KIND>
-__device__ __forceinline__ void update_tile(const P& p, int i, const float* g, const int* r, int c) {
-  const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
+struct TileUpdate {
   float w[4], a[4], bb[4];
+  int64_t e[4];
+  __device__ __forceinline__ void load(const P& p, int i, const int* r, int c) {
+    const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t e = (int64_t)r[q] * C + c;
-    w[q] = p.W[i][e];
-    a[q] = p.sW1[i] ? p.sW1[i][e] : 0.f;
-    bb[q] = p.sW2[i] ? p.sW2[i][e] : 0.f;
+    for (int q = 0; q < 4; ++q) {
+      e[q] = (int64_t)r[q] * C + c;
+      w[q] = p.W[i][e[q]];
+      a[q] = p.sW1[i] ? p.sW1[i][e[q]] : 0.f;
+      bb[q] = p.sW2[i] ? p.sW2[i][e[q]] : 0.f;
+    }
   }
+  __device__ __forceinline__ void apply(const P& p, int i, const float* g, const int* r, int c) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t e = (int64_t)r[q] * C + c;
-    opt_update_k<KIND>(p.op, g[q], w[q], a[q], bb[q]);
-    p.W[i][e] = w[q];
-    if (p.sW1[i]) p.sW1[i][e] = a[q];
-    if (p.sW2[i]) p.sW2[i][e] = bb[q];
-    if constexpr (sizeof(CT) == 2)
-      if (p.sh[i]) reinterpret_cast<CT*>(p.sh[i])[shadow_index(p, i, r[q], c)] = CvtT<CT>::to(w[q]);
+    for (int q = 0; q < 4; ++q) {
+      opt_update_k<KIND>(p.op, g[q], w[q], a[q], bb[q]);
+      p.W[i][e[q]] = w[q];
+      if (p.sW1[i]) p.sW1[i][e[q]] = a[q];
+      if (p.sW2[i]) p.sW2[i][e[q]] = bb[q];
+      if constexpr (sizeof(CT) == 2)
+        if (p.sh[i]) reinterpret_cast<CT*>(p.sh[i])[shadow_index(p, i, r[q], c)] = CvtT<CT>::to(w[q]);
+    }
   }
-}
+};
 
 // bias i: db[n] = gscale * sum over the Bp / 32 row tiles of the column partials the producer of delta_i wrote
 // (tile order), then the update
@@ -374,20 +378,20 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     const int K = p.dim[L], nt = p.Np / TT;
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
-      // W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k], contiguous along k
-      const Tile v = wg_tile<CT, false, false>(lds, m0, n0, K,
-                                               [&](int m, int k) { return ldc4(p.h[L - 1], (int64_t)m * K + k); },
-                                               [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); });
       const int n = n0 + c;
       const float bias = p.b[L][n];
       float mkv[4], ttv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {        // the mask / target loads first (clamped: always in bounds)
+      for (int j = 0; j < 4; ++j) {        // the mask / target loads in flight during the GEMM (clamped)
         const int m = m0 + out_row(j);
         const int64_t o = p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
         mkv[j] = p.om[o];
         ttv[j] = p.tg[o];
       }
+      // W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k], contiguous along k
+      const Tile v = wg_tile<CT, false, false>(lds, m0, n0, K,
+                                               [&](int m, int k) { return ldc4(p.h[L - 1], (int64_t)m * K + k); },
+                                               [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); });
       Tile dl;
       float sse = 0.f, sae = 0.f, cnt = 0.f, rs[4];
 #pragma unroll
@@ -431,32 +435,6 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
   }
   // ---- backward, layer by layer from the output
   for (int i = L; i >= 0; --i) {
-    // the update of W_{i+1} from its scratch gradient: nothing reads W_{i+1} from here on
-    if (i + 1 <= L) {
-      const int R = i + 1 == L ? p.dim[L + 1] : p.dim[i + 1], C = i + 1 == L ? p.dim[L] : p.dim[i + 2];
-      update_from<CT, KIND>(p, i + 1, p.g[i + 1], (int64_t)R * C, gtid, gthreads);
-    }
-    if (i == L && blockIdx.x == gridDim.x - 1 && wave == 0) {
-      // the step's statistics from the per-wave partials, in order
-      const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / TT;
-      float a[3] = {0.f, 0.f, 0.f};
-      for (int t = lane; t < slots; t += 64)
-        for (int k = 0; k < 3; ++k) a[k] += ldc(p.totp, (int64_t)t * 3 + k);
-      for (int k = 0; k < 3; ++k)
-        for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
-      if (lane == 0) {
-        p.stats[0] = a[0];
-        p.stats[1] = a[1];
-        p.stats[2] = a[2];
-        p.stats[3] = 0.f;
-      }
-      for (int b = lane; b < p.Bp; b += 64) {
-        float r = 0.f;
-        for (int cb = 0; cb < ncb; ++cb) r += ldc(p.rowp, (int64_t)cb * p.Bp + b);
-        p.stats[4 + b] = r;
-      }
-    }
-    bias_update<KIND>(p, i, gtid, gthreads);
     const int Wi = p.dim[i + 1];                 // layer i's output width (padded)
     const int Ki = p.dim[i];                     // its input width
     // delta of layer i - 1's output: (delta_i W_i^T) * act'(h_{i-1}), with its column sums
@@ -464,9 +442,47 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     // dW_i: [input][output] (layer L: [output][input]) tiles, K = the batch rows
     const int gr = i == L ? Wi : Ki, gc = i == L ? Ki : Wi;
     const int ng = (gr / TT) * (gc / TT);
+    // the phase's side work, which no tile of the phase reads: the update of W_{i+1} from its scratch gradient
+    // (nothing reads W_{i+1} from here on), the step's statistics (i = L), b_i's update.  Done by the
+    // workgroups without a tile when there are enough of them, else by every workgroup after its tiles.
+    auto side = [&](int sid, int sthreads, bool last) {
+      if (i + 1 <= L) {
+        const int R = i + 1 == L ? p.dim[L + 1] : p.dim[i + 1], C = i + 1 == L ? p.dim[L] : p.dim[i + 2];
+        update_from<CT, KIND>(p, i + 1, p.g[i + 1], (int64_t)R * C, sid, sthreads);
+      }
+      if (i == L && last && wave == 0) {
+        // the step's statistics from the per-wave partials, in order
+        const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / TT;
+        float a[3] = {0.f, 0.f, 0.f};
+        for (int t = lane; t < slots; t += 64)
+          for (int k = 0; k < 3; ++k) a[k] += ldc(p.totp, (int64_t)t * 3 + k);
+        for (int k = 0; k < 3; ++k)
+          for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+        if (lane == 0) {
+          p.stats[0] = a[0];
+          p.stats[1] = a[1];
+          p.stats[2] = a[2];
+          p.stats[3] = 0.f;
+        }
+        for (int b = lane; b < p.Bp; b += 64) {
+          float r = 0.f;
+          for (int cb = 0; cb < ncb; ++cb) r += ldc(p.rowp, (int64_t)cb * p.Bp + b);
+          p.stats[4 + b] = r;
+        }
+      }
+      bias_update<KIND>(p, i, sid, sthreads);
+    };
+    const int T = nd + ng, idle = (int)gridDim.x - T;
+    const bool side_idle = idle >= (int)gridDim.x / 4;
+    if (side_idle && (int)blockIdx.x >= T)
+      side(((int)blockIdx.x - T) * THREADS + threadIdx.x, idle * THREADS, blockIdx.x == gridDim.x - 1);
     for (int t = blockIdx.x; t < nd + ng; t += gridDim.x) {
       if (t < nd) {
         const int ct = Ki / TT, m0 = (t / ct) * TT, n0 = (t % ct) * TT;
+        const int n = n0 + c;
+        float hv[4];                    // in flight during the GEMM
+#pragma unroll
+        for (int j = 0; j < 4; ++j) hv[j] = ldc(p.h[i - 1], (int64_t)(m0 + out_row(j)) * Ki + n);
         Tile v;
         if (i == L)      // B(n = input unit, k = output unit) = W_L[k][n], contiguous along n
           v = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
@@ -474,10 +490,6 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         else             // B(n = input unit, k = output unit) = W_i[n][k], contiguous along k
           v = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
                                         [&](int n, int k) { return ld4(p.W[i] + (int64_t)n * Wi + k); });
-        const int n = n0 + c;
-        float hv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hv[j] = ldc(p.h[i - 1], (int64_t)(m0 + out_row(j)) * Ki + n);
         Tile dv;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -489,6 +501,11 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         continue;
       }
       const int u = t - nd, ct = gc / TT, m0 = (u / ct) * TT, n0 = (u % ct) * TT;
+      int rr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rr[j] = m0 + out_row(j);
+      TileUpdate<CT, KIND> up;
+      if (i == 0) up.load(p, 0, rr, n0 + c);   // W_0's parameters and slots in flight during the GEMM
       Tile v;
       if (i == L)        // dW_L[n][j] = sum_b delta_L[b][n] h_{L-1}[b][j]
         v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.d[L], (int64_t)k * Wi + m); },
@@ -501,18 +518,15 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
                                     [&](int n, int k) { return ldc4(p.d[0], (int64_t)k * Wi + n); });
       if (i == 0) {      // nothing reads W_0 any more: update it from the tile (padded elements have zero gradient)
         float gv[4];
-        int rr[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          gv[j] = v.v[j] * gs;
-          rr[j] = m0 + out_row(j);
-        }
-        update_tile<CT, KIND>(p, 0, gv, rr, n0 + c);
+        for (int j = 0; j < 4; ++j) gv[j] = v.v[j] * gs;
+        up.apply(p, 0, gv, rr, n0 + c);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) pub(&p.g[i][(int64_t)(m0 + out_row(j)) * gc + n0 + c], v.v[j] * gs);
       }
     }
+    if (!side_idle) side(gtid, gthreads, blockIdx.x == gridDim.x - 1);
     if (i > 0) grid_sync(p, tn, nb);
   }
   grid_exit(p, nb);

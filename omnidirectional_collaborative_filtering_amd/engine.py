@@ -101,6 +101,7 @@ class Engine:
         self._pending_pack = self._mlp_batch = self._mlp_args = None
         self.fused_mlp = True
         self.mlp_trace = None
+        self.mlp_wgs = 0                        # ocf_mlp_step's grid (0: the library's choice)
         self.act = _lib.ACT[activation]
         self.activation = activation
         self.dropout = dropout
@@ -702,6 +703,7 @@ class Engine:
         o = self.opt.step_params(2.0 / ((self.rows_real or self.B) * self.N_total), 0.0)
         a.opt = o
         a.trace = ptr(self.mlp_trace)          # (diagnostics: tools/mlp_trace.py)
+        a.wgs = self.mlp_wgs
         self._grow_stats(self.n_stats + 1)
         a.stats = self._stats_row(self.n_stats)
         with self.phase("mlp_step"):

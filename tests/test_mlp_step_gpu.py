@@ -28,18 +28,19 @@ def _opt(name):
             "adam": (lambda: O.Adam(lr=0.001), lambda: AdamOracle(lr=0.001))}[name]
 
 
-def _fit(layers, H, act, opt, cd, k, n, N, B, fused, vs=0.1):
+def _fit(layers, H, act, opt, cd, k, n, N, B, fused, vs=0.1, epochs=1, wgs=0):
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     x, om_, t = _data(n, N, k)
     m = omni_model(layers, H, N, B, dense_activation=act, use_causal_info=k >= 2, use_both_masks=k == 3,
                    compute_dtype=cd, seed=5)
     m.engine.fused_mlp = fused
+    m.engine.mlp_wgs = wgs
     model = m.model
     model.compile(_opt(opt)[0](), "mean_squared_error")
     w0 = model.get_weights()
     np.random.seed(42)
     ins = x[:2] + [om_] + x[2:]               # model.py:89-97's input order: data, mask, output mask, second mask
-    h = model.fit(ins, t, batch_size=B, validation_split=vs, epochs=1, shuffle=True)
+    h = model.fit(ins, t, batch_size=B, validation_split=vs, epochs=epochs, shuffle=True)
     ran = m.engine._mlp_args is not None
     return h.history, w0, model.get_weights(), ran, (x, om_, t)
 
@@ -110,3 +111,20 @@ def test_fused_step_matches_layerwise_path(gpu):
     assert abs(a[0]["val_loss"][0] - b[0]["val_loss"][0]) <= 1e-5 * b[0]["val_loss"][0]
     for x, y in zip(a[2], b[2]):
         assert np.abs(x - y).max() <= 2e-5, float(np.abs(x - y).max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wgs", [5, 128])
+def test_fused_step_grid_sizes_match_layerwise(gpu, wgs):
+    """the phases' hand-offs (write-through stores, L1-bypassing loads, the arrival counter) on a grid of 5
+    workgroups (each walks many tiles) and of 128 (most idle in some phases): three epochs of 24 steps with
+    Adam, 3 hidden layers, k = 3 equal the layer-wise path's in exact fp32 (a stale hand-off would not)"""
+    args = (3, 160, "sigmoid", "adam", "float32", 3, 3000, 100, 112)
+    a = _fit(*args, fused=True, epochs=3, wgs=wgs)
+    b = _fit(*args, fused=False, epochs=3)
+    assert a[3] and not b[3]
+    for e in range(3):
+        assert abs(a[0]["loss"][e] - b[0]["loss"][e]) <= 1e-5 * b[0]["loss"][e], e
+        assert abs(a[0]["val_loss"][e] - b[0]["val_loss"][e]) <= 1e-5 * b[0]["val_loss"][e], e
+    for x, y in zip(a[2], b[2]):
+        assert np.abs(x - y).max() <= 5e-5, float(np.abs(x - y).max())

@@ -24,14 +24,13 @@ m = om.model
 m.compile("rmsprop", "mean_squared_error")
 e = om.engine
 e.mlp_trace = torch.zeros(24, dtype=torch.int64, device="cuda")
+e.mlp_wgs = a.wgs
 xd = [torch.as_tensor(z).cuda() for z in (inputs, observed, out_m)]
 yd = torch.as_tensor(targets).cuda()
 idx = torch.arange(20000, device="cuda")
 rows = []
 for s in range(a.steps):
     m._load_rows(xd, yd, idx[s * 128:(s + 1) * 128])
-    if a.wgs and e._mlp_args is not None:
-        e._mlp_args.wgs = a.wgs
     e.train_step()
     torch.cuda.synchronize()
     t = e.mlp_trace.cpu().numpy().astype(np.float64)
