@@ -92,7 +92,10 @@ def parse():
                     help="weight-gradient row lists built per epoch by the generator (ocf_epoch_row_lists; the "
                          "timed region includes building them for the timed batches) instead of per step")
     ap.add_argument("--fused-mlp", type=int, default=1,
-                    help="--config jester: the whole step in one launch (ocf_mlp_step; 0: the layer-wise dense path)")
+                    help="small models (Jester, ML-100K, ML-1M): the whole step in one launch (ocf_mlp_step; 0: the "
+                         "layer-wise dense path / the row gathers)")
+    ap.add_argument("--fused-gen", type=int, default=0,
+                    help="generator batches of small models through ocf_mlp_step too (Engine.fused_gen; opt-in)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -478,6 +481,8 @@ def main():
     eng.split_dw_streams = bool(args.split_dw)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
     eng.epoch_row_lists = bool(args.epoch_lists)
+    eng.fused_mlp = bool(args.fused_mlp)
+    eng.fused_gen = bool(args.fused_gen)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
         eng.shadow_blocked = bool(args.shadow_blocked)
         eng._refresh_shadows()
@@ -518,7 +523,7 @@ def main():
     torch.cuda.synchronize()
     phases = eng.phase_times_ms(skip=1 if args.warmup > 1 else 0)
     cand = {k: v for k, v in phases.items()
-            if k in ("dW_in", "dW_out", "dW_pair", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm")}
+            if k in ("dW_in", "dW_out", "dW_pair", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm", "mlp_step")}
     dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
     if world > 1:
         torch.distributed.barrier()
@@ -526,7 +531,8 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     nnz = 0
-    epoch_lists = eng.epoch_row_lists and eng.sparse_dw and eng.use_sparse
+    fused_step = dom == "mlp_step"          # a small model: dense arrays + ocf_mlp_step, no row lists
+    epoch_lists = eng.epoch_row_lists and eng.sparse_dw and eng.use_sparse and not fused_step
     if epoch_lists:
         # the timed batches' row lists, built inside the timed region (one launch sequence, as at the
         # start of every training epoch)
@@ -604,6 +610,9 @@ def main():
         "dec_gemm_mse": P * w_b + Bg * H * 2 + Bg * Nl * 2,
         "dec_bwd_gemm": P * w_b + Bg * Nl * 2,
     }
+    # the fused small-model step: the whole step in one launch, against its dense-update bytes and its flops
+    # (forward, output layer, input-delta-free backward: 3 GEMMs of 2 B N H each way + the hidden delta)
+    alg["mlp_step"] = P * 2 * (opt_b + 4 + sh_b) + Bg * Nl * 4 * 3
     roof = None
     if dom is not None and dom_timed:
         if world > 1 and not fp and dom in ("dW_in", "dW_out"):
@@ -615,6 +624,15 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
                 "kernel_mean_us": round(ms * 1e3, 1), "kernel_samples": dom_timed["n"],
                 "alg_bytes_per_launch": int(alg[dom]), "live_row_frac": round(live, 4)}
+        if dom == "mlp_step":
+            fl = 10.0 * Bg * Nl * H
+            tf = fl / (ms * 1e-3) / 1e12
+            if tf / MFMA_F16_PEAK_TFS > ach / HBM_PEAK_GBS:
+                roof.update(bound="mfma", achieved=round(tf, 2), peak=MFMA_F16_PEAK_TFS, unit="TFLOP/s",
+                            frac=round(tf / MFMA_F16_PEAK_TFS, 4))
+            roof["alg_flops_per_launch"] = int(fl)
+            roof["note"] = ("the whole step in one persistent launch (ocf_mlp_step): dense GEMMs on the batch's "
+                            "data_gen arrays, fused masked MSE, optimizer updates")
         # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
         # the latest round's PMC summary that measured this kernel (r03_, r03b_, r03c_ ... sort in round order)
         pmcs = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")))

@@ -605,18 +605,19 @@ int ocf_backward(OcfCtx* ctx, const float* grad, int64_t ld_grad, int B, float g
  * whose weights fit in L2 (0.14 M parameters) the step is latency-bound: one launch instead of ~14.
  * The batch is gathered from device-resident arrays by row index (Model.fit's data path): input block j of
  * batch row b is x[j] + rows[b] * ld_x (N values), its output mask / targets out_mask / targets + rows[b] *
- * ld_t.  Rows b >= B are padding (zero).  Weights in the engine's padded layout: W[0] [k_blocks * Np][hidden_p[0]]
+ * ld_t.  Rows b >= B are padding (zero).  rows == NULL: dense batch arrays (ocf_scatter_batch's X / Mout / T
+ * outputs): x[j], out_mask, targets are [Bp][ld] with zero padding, ld >= Np, ld_x % 4 == 0.  Weights in the engine's padded layout: W[0] [k_blocks * Np][hidden_p[0]]
  * (block j's column n at row j * Np + n), W[i] [hidden_p[i-1]][hidden_p[i]], W[L] transposed [Np][hidden_p[L-1]];
  * b[i] the padded output width; optimizer slots alike (nullable per the optimizer); shadow[i] (nullable) the
- * compute-dtype copy of W[i] rewritten by the update (64 x 64-blocked with shadow_blocked).  No dropout, l2 = 0.
+ * compute-dtype copy of W[i] rewritten by the update (64 x 64-blocked with shadow_blocked).  l2 = 0.
  * stats: {sse, sae, count_nonzero(T + y), 0, row sse [Bp]} (the masked-MSE statistics).  work: scratch of
  * ocf_mlp_step_workspace bytes.  barrier: device uint32[2], zero before the first launch, left reusable.
  */
 typedef struct OcfMlpStepArgs {
   int n_hidden;                                   /* L, 1..OCF_MAX_HIDDEN */
-  int B, Bp;                                      /* batch rows; padded (multiple of 32, <= 512) */
-  int N, Np, k_blocks;                            /* output width / padded (multiple of 32); input blocks */
-  int hidden[OCF_MAX_HIDDEN], hidden_p[OCF_MAX_HIDDEN];   /* hidden widths, padded (multiples of 32) */
+  int B, Bp;                                      /* batch rows; padded (multiple of 64, <= 512) */
+  int N, Np, k_blocks;                            /* output width / padded (multiple of 64); input blocks */
+  int hidden[OCF_MAX_HIDDEN], hidden_p[OCF_MAX_HIDDEN];   /* hidden widths, padded (multiples of 64) */
   const float* x[3]; int64_t ld_x; const int64_t* rows;
   const float* out_mask; const float* targets; int64_t ld_t;
   float* W[OCF_MAX_HIDDEN + 1]; float* b[OCF_MAX_HIDDEN + 1];
@@ -632,6 +633,11 @@ typedef struct OcfMlpStepArgs {
                                                    * phase, at most 128; never more than the CU count) */
   uint64_t* trace;                                /* (nullable) device uint64[24]: workgroup 0's constant-rate
                                                    * clock (100 MHz) at the start and after each phase */
+  /* Dropout after every hidden layer (model.py:72-73; keep = 1 - dropout_probability, 1 = none): the mask of
+   * layer i's element (m, n) is floor(keep + U) with U the Philox uniform of (seed, stream + i, m * hidden_p[i]
+   * + n), as the layer-wise path draws it; mask[i] (u8 [Bp][hidden_p[i]], required when keep < 1) receives it. */
+  float keep; uint64_t seed, stream;
+  uint8_t* mask[OCF_MAX_HIDDEN];
 } OcfMlpStepArgs;
 int64_t ocf_mlp_step_workspace(const OcfMlpStepArgs* args);
 int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);

@@ -172,7 +172,13 @@ class OcfMlpStepArgs(ctypes.Structure):
                 ("out_mask", P), ("targets", P), ("ld_t", I64), ("W", P * _L), ("b", P * _L), ("sW1", P * _L),
                 ("sW2", P * _L), ("sb1", P * _L), ("sb2", P * _L), ("shadow", P * _L), ("shadow_blocked", I32),
                 ("act", I32), ("compute_dtype", I32), ("opt", OcfOptParams), ("stats", P), ("work", P),
-                ("work_bytes", I64), ("barrier", P), ("wgs", I32), ("trace", P)]
+                ("work_bytes", I64), ("barrier", P), ("wgs", I32), ("trace", P), ("keep", ctypes.c_float),
+                ("seed", ctypes.c_uint64), ("stream", ctypes.c_uint64), ("mask", P * 8)]
+
+    def __init__(self, *a, **kw):
+        super().__init__(*a, **kw)
+        if "keep" not in kw:
+            self.keep = 1.0
 
 
 ASYNC_MLP_BARRIER = 2          # ocf.h OCF_ASYNC_MLP_BARRIER

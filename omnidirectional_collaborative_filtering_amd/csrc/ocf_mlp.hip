@@ -48,7 +48,10 @@ struct P {
   float* h[MAXL];         // h[i]: [Bp][dim[i+1]] (i < L)
   float* d[MAXL + 1];     // d[i]: delta of layer i's output, [Bp][dim[i+1]] (i <= L)
   float* g[MAXL];         // g[i]: dW_i scratch (1 <= i <= L), W_i's layout
-  float* colp[MAXL + 1];  // colp[i]: [Bp / 32][dim[i+1]] column sums of delta_i per 32-row tile (bias gradients)
+  float* colp[MAXL + 1];  // colp[i]: [Bp / 32][dim[i+1]] column sums of delta_i per 32-row block (bias gradients)
+  float* am[MAXL];        // am[i], dm[i] (dropout only): layer i's activation before dropout, mask / keep
+  float* dm[MAXL];
+  float keep; uint64_t seed, stream; uint8_t* mask[MAXL];
   float* rowp;            // [Np / 32][Bp] per column-tile row sse
   float* totp;            // [tiles][waves][3] per output tile and wave sse / sae / count
   uint32_t* bar; uint32_t* err; int max_polls;
@@ -119,141 +122,175 @@ __device__ __forceinline__ void grid_exit(const P& p, int nb) {
   }
 }
 
-// ---- one 32 x 32 tile of C = A B per workgroup, K split over the 4 waves (a wave's quarter of K in chunks of
-// KC staged through the wave's own LDS region, then MFMA from LDS); the four partial tiles are summed in wave
-// order through LDS.  A phase of the Jester model has 16-96 such tiles, so every workgroup of the grid has
-// work and a wave walks one or two chunks instead of a workgroup walking the whole K.
-// a(r, k) / b(n, k) return 4 consecutive fp32 elements along the operand's contiguous direction (r .. r+3 when
-// A_RFAST / B_NFAST, else k .. k+3), rounded to CT when staged (as the MFMA operand staging of the other paths).
-// Every lane issues all of a chunk's loads before it writes any (the accessors are branch-free).
+// ---- one 32 x 32 tile of C = A B per workgroup, K split over the four waves: each wave stages its quarter of
+// K through its own LDS region in chunks of KC and the four partial tiles are summed in wave order through
+// LDS.  (Keeping the next chunk's loads in flight during the MFMAs raised the kernel to ~300 VGPRs and cost
+// Jester ~10 %: its waves walk one chunk.)  A phase of
+// the Jester model has 16-96 such tiles, so every workgroup of the grid has work and a wave walks one or two
+// chunks instead of a workgroup walking the whole K.  a(r, k) / b(n, k) return 4 consecutive fp32 elements
+// along the operand's contiguous direction (r .. r+3 when A_RFAST / B_NFAST, else k .. k+3), rounded to CT
+// when staged (as the MFMA operand staging of the other paths); every lane issues all of a chunk's loads
+// before it writes any (the accessors are branch-free).  (A 64 x 64 shape with one quadrant per wave was
+// measured for the wide GEMMs of ML-100K / ML-1M-sized models and removed: DESIGN.md §1.)
 constexpr int TT = 32;
-template <typename CT> struct Lds {
-  static constexpr int KC = sizeof(CT) == 2 ? 64 : 32;     // a wave's K chunk
+template <typename CT> struct Geo {
+  static constexpr int KC = sizeof(CT) == 2 ? 64 : 32;     // K chunk
   static constexpr int PAD = sizeof(CT) == 2 ? 8 : 4;
-  static constexpr int STRIDE = KC + PAD;                  // row stride 144 B (16-bit) / 144 B (fp32)
-  static constexpr int WAVE = 2 * TT * STRIDE;             // a wave's A + B chunk (elements)
-  static constexpr int STAGE_BYTES = WAVES * WAVE * (int)sizeof(CT);
-  static constexpr int RED_BYTES = WAVES * TT * (TT + 1) * 4;
-  static constexpr int BYTES = (STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES) + WAVES * TT * 4;
+  static constexpr int S = KC + PAD;                       // LDS row stride: 144 B
+  static constexpr int STAGE = WAVES * 2 * TT * S * (int)sizeof(CT);   // four waves' A + B
+  static constexpr int RED = WAVES * TT * (TT + 1) * 4;
+  static constexpr int CS_OFF = STAGE > RED ? STAGE : RED;
+  static constexpr int BYTES = CS_OFF + WAVES * TT * 4;
 };
 
-template <typename CT, bool FAST_R, typename F>
-__device__ __forceinline__ void stage(CT* dst, int r0, int k0, int kc, F&& f) {
-  constexpr int S = Lds<CT>::STRIDE, KC = Lds<CT>::KC, RUNS = TT * KC / 4 / 64;
-  const int lane = threadIdx.x & 63;
+// one operand's chunk: R rows x KC, loaded by NP participants (the lanes of a wave) as RUNS float4 each
+template <typename CT, bool FAST_R, int R, int NP>
+struct Chunk {
+  static constexpr int KC = Geo<CT>::KC, S = Geo<CT>::S, RUNS = R * KC / 4 / NP;
   float4 v[RUNS];
-#pragma unroll
-  for (int j = 0; j < RUNS; ++j) {
-    const int u = lane + 64 * j;
-    int r, k;
-    if (FAST_R) { r = 4 * (u % (TT / 4)); k = u / (TT / 4); }
+  __device__ __forceinline__ static void at(int u, int& r, int& k) {
+    if (FAST_R) { r = 4 * (u % (R / 4)); k = u / (R / 4); }
     else { r = u / (KC / 4); k = 4 * (u % (KC / 4)); }
-    v[j] = f(r0 + r, k0 + (k < kc ? k : 0));              // past the chunk's end: a valid address, unused
   }
+  template <typename F>
+  __device__ __forceinline__ void load(F& f, int r0, int k0, int kc, int pid) {
 #pragma unroll
-  for (int j = 0; j < RUNS; ++j) {
-    const int u = lane + 64 * j;
-    const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-    if (FAST_R) {
-      const int r = 4 * (u % (TT / 4)), k = u / (TT / 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dst[(r + q) * S + k] = CvtT<CT>::to(e[q]);
-    } else {
-      const int r = u / (KC / 4), k = 4 * (u % (KC / 4));
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dst[r * S + k + q] = CvtT<CT>::to(e[q]);
+    for (int j = 0; j < RUNS; ++j) {
+      int r, k;
+      at(pid + NP * j, r, k);
+      v[j] = f(r0 + r, k0 + (k < kc ? k : 0));            // past the chunk's end: a valid address, unused
     }
+  }
+  __device__ __forceinline__ void store(CT* dst, int pid) const {
+#pragma unroll
+    for (int j = 0; j < RUNS; ++j) {
+      int r, k;
+      at(pid + NP * j, r, k);
+      const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (FAST_R) dst[(r + q) * S + k] = CvtT<CT>::to(e[q]);
+        else dst[r * S + k + q] = CvtT<CT>::to(e[q]);
+      }
+    }
+  }
+};
+
+// acc += the 32 x 32 product of LDS rows sA[0..31] x sB[0..31] over kc (a multiple of 16)
+template <typename CT>
+__device__ __forceinline__ void mfma_chunk(ocf_f16v& acc, const CT* sA, const CT* sB, int kc) {
+  constexpr int S = Geo<CT>::S;
+  const int lane = threadIdx.x & 63, r = lane & 31, hf = lane >> 5;
+  if constexpr (sizeof(CT) == 2) {
+    using V = typename std::conditional<std::is_same<CT, _Float16>::value, ocf_h8, ocf_b8>::type;
+    for (int ks = 0; ks < kc; ks += 16) {
+      V fa, fb;
+      __builtin_memcpy(&fa, sA + r * S + ks + 8 * hf, 16);
+      __builtin_memcpy(&fb, sB + r * S + ks + 8 * hf, 16);
+      if constexpr (std::is_same<CT, _Float16>::value)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
+    }
+  } else {
+    for (int ks = 0; ks < kc; ks += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[r * S + ks + hf], sB[r * S + ks + hf], acc, 0, 0, 0);
   }
 }
 
-// the summed tile: thread t holds rows (t >> 5) + 8 j (j < 4) of column t & 31
-struct Tile {
-  float v[4];
+// a thread's share of a finished tile: NE rows m[] of one column n
+template <int NE> struct Frag {
+  int n;
+  int m[NE];
+  float v[NE];
 };
-__device__ __forceinline__ int out_row(int j) { return (threadIdx.x >> 5) + 8 * j; }
-__device__ __forceinline__ int out_col() { return threadIdx.x & 31; }
 
 template <typename CT, bool A_RFAST, bool B_NFAST, typename FA, typename FB>
-__device__ __forceinline__ Tile wg_tile(char* lds, int m0, int n0, int K, FA&& a, FB&& b) {
-  constexpr int S = Lds<CT>::STRIDE, KC = Lds<CT>::KC;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, hf = lane >> 5;
-  CT* sA = reinterpret_cast<CT*>(lds) + wave * Lds<CT>::WAVE;
+__device__ __forceinline__ Frag<4> tile_s(char* lds, int m0, int n0, int K, FA&& a, FB&& b) {
+  constexpr int S = Geo<CT>::S, KC = Geo<CT>::KC;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  CT* sA = reinterpret_cast<CT*>(lds) + wave * 2 * TT * S;
   CT* sB = sA + TT * S;
   const int kw = K / WAVES, kb = wave * kw;             // K % 64 == 0: kw is a multiple of 16
+  Chunk<CT, A_RFAST, TT, 64> ca;
+  Chunk<CT, B_NFAST, TT, 64> cb;
   ocf_f16v acc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   for (int k0 = 0; k0 < kw; k0 += KC) {
     const int kc = kw - k0 < KC ? kw - k0 : KC;
-    stage<CT, A_RFAST>(sA, m0, kb + k0, kc, a);
-    stage<CT, B_NFAST>(sB, n0, kb + k0, kc, b);
+    ca.load(a, m0, kb + k0, kc, lane);
+    cb.load(b, n0, kb + k0, kc, lane);
+    ca.store(sA, lane);
+    cb.store(sB, lane);
     __syncthreads();
-    if constexpr (sizeof(CT) == 2) {
-      using V = typename std::conditional<std::is_same<CT, _Float16>::value, ocf_h8, ocf_b8>::type;
-      for (int ks = 0; ks < kc; ks += 16) {
-        V fa, fb;
-        const int kk = ks + 8 * hf;
-        __builtin_memcpy(&fa, sA + r * S + kk, 16);
-        __builtin_memcpy(&fb, sB + r * S + kk, 16);
-        if constexpr (std::is_same<CT, _Float16>::value)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa, fb, acc, 0, 0, 0);
-        else
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
-      }
-    } else {
-      for (int ks = 0; ks < kc; ks += 2)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[r * S + ks + hf], sB[r * S + ks + hf], acc, 0, 0, 0);
-    }
+    mfma_chunk<CT>(acc, sA, sB, kc);
     __syncthreads();
   }
   // the four K quarters, summed in wave order (C layout of v_mfma_f32_32x32x*: register q holds row
-  // (q & 3) + 8 (q >> 2) + 4 hf, column r)
+  // (q & 3) + 8 (q >> 2) + 4 hf, column lane & 31)
   float* red = reinterpret_cast<float*>(lds);
+  const int r = lane & 31, hf = lane >> 5;
 #pragma unroll
   for (int q = 0; q < 16; ++q) red[(wave * TT + (q & 3) + 8 * (q >> 2) + 4 * hf) * (TT + 1) + r] = acc[q];
   __syncthreads();
-  Tile t;
+  Frag<4> f;
+  f.n = n0 + (threadIdx.x & 31);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int rr = out_row(j), cc = out_col();
+    const int rr = (threadIdx.x >> 5) + 8 * j, cc = threadIdx.x & 31;
     float s = red[rr * (TT + 1) + cc];
 #pragma unroll
     for (int w = 1; w < WAVES; ++w) s += red[(w * TT + rr) * (TT + 1) + cc];
-    t.v[j] = s;
+    f.m[j] = m0 + rr;
+    f.v[j] = s;
   }
   __syncthreads();
-  return t;
+  return f;
 }
 
-// the column sums of the summed tile over its 32 rows (a thread's rows, then the two half-waves, then the
-// waves in order), written to dst[0..31] by threads 0..31
+// the column sums of a fragment's tile over its 32 rows in a fixed order (a thread's rows, the two half-waves,
+// the four waves through LDS), written to colp[row block][column] (ld W)
 template <typename CT>
-__device__ __forceinline__ void tile_colsum(char* lds, const Tile& t, float* dst) {
-  float* cs = reinterpret_cast<float*>(lds + Lds<CT>::BYTES - WAVES * TT * 4);
-  float s = (t.v[0] + t.v[1]) + (t.v[2] + t.v[3]);
+__device__ __forceinline__ void frag_colsum(char* lds, const Frag<4>& f, int m0, float* colp, int W) {
+  float s = (f.v[0] + f.v[1]) + (f.v[2] + f.v[3]);
   s += __shfl_xor(s, 32, 64);
-  if ((threadIdx.x & 63) < 32) cs[(threadIdx.x >> 6) * TT + out_col()] = s;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* cs = reinterpret_cast<float*>(lds + Geo<CT>::CS_OFF);
+  if (lane < 32) cs[wave * TT + lane] = s;
   __syncthreads();
   if (threadIdx.x < TT) {
     float c = cs[threadIdx.x];
 #pragma unroll
     for (int w = 1; w < WAVES; ++w) c += cs[w * TT + threadIdx.x];
-    pub(&dst[threadIdx.x], c);
+    pub(&colp[(int64_t)(m0 / TT) * W + f.n], c);
   }
 }
 
 __device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast<const float4*>(q); }
 
 // ---- operand views
-// layer-0 input of batch row b, padded columns c .. c+3 (one block: Np % 4 == 0); zero past the batch and in
-// the block padding (element loads through selected addresses: no branches, the four loads go out together)
+// layer-0 input of batch row b, padded columns c .. c+3 (one block: Np % 4 == 0).  XD (dense batch arrays,
+// rows == NULL): [Bp][ld_x] with zero padding, one vector load; else row rows[b] of the caller's [n][ld_x] arrays,
+// zero past the batch and in the block padding (element loads through selected addresses: no branches)
+template <bool XD>
 __device__ __forceinline__ float4 x4(const P& p, int b, int c) {
   const int blk = c / p.Np, n = c - blk * p.Np;
-  const float* row = p.x[blk] + p.rows[b < p.B ? b : p.B - 1] * p.ld_x;
-  float e[4];
+  if constexpr (XD) {
+    return ld4(p.x[blk] + (int64_t)b * p.ld_x + n);
+  } else {
+    const float* row = p.x[blk] + p.rows[b < p.B ? b : p.B - 1] * p.ld_x;
+    float e[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) e[q] = *((b < p.B && n + q < p.N) ? row + n + q : g_zero);
-  return make_float4(e[0], e[1], e[2], e[3]);
+    for (int q = 0; q < 4; ++q) e[q] = *((b < p.B && n + q < p.N) ? row + n + q : g_zero);
+    return make_float4(e[0], e[1], e[2], e[3]);
+  }
+}
+// element offset of batch row m, column n of the output mask / targets
+template <bool XD>
+__device__ __forceinline__ int64_t t_off(const P& p, int m, int n) {
+  if constexpr (XD) return (int64_t)m * p.ld_t + n;
+  else return p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
 }
 __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c) {
   const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
@@ -261,37 +298,39 @@ __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c)
   return ((int64_t)(r >> 6) * (C >> 6) + (c >> 6)) * 4096 + (r & 63) * 64 + (c & 63);
 }
 
-// the update of a thread's 4 elements of weight i (rows r[q], column c of a [R][C] weight): the parameters and
+// the update of a thread's NE elements of weight i (rows r[q], column c of a [R][C] weight): the parameters and
 // slots are loaded before the tile's GEMM (load), the update applied from its gradients after it (apply)
-template <typename CT, int KIND>
+template <typename CT, int KIND, int NE>
 struct TileUpdate {
-  float w[4], a[4], bb[4];
-  int64_t e[4];
+  float w[NE], a[NE], bb[NE];
+  __device__ __forceinline__ int64_t at(const P& p, int i, int r, int c) const {
+    return (int64_t)r * (i == p.L ? p.dim[i] : p.dim[i + 1]) + c;
+  }
   __device__ __forceinline__ void load(const P& p, int i, const int* r, int c) {
-    const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      e[q] = (int64_t)r[q] * C + c;
-      w[q] = p.W[i][e[q]];
-      a[q] = p.sW1[i] ? p.sW1[i][e[q]] : 0.f;
-      bb[q] = p.sW2[i] ? p.sW2[i][e[q]] : 0.f;
+    for (int q = 0; q < NE; ++q) {
+      const int64_t e = at(p, i, r[q], c);
+      w[q] = p.W[i][e];
+      a[q] = p.sW1[i] ? p.sW1[i][e] : 0.f;
+      bb[q] = p.sW2[i] ? p.sW2[i][e] : 0.f;
     }
   }
   __device__ __forceinline__ void apply(const P& p, int i, const float* g, const int* r, int c) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NE; ++q) {
+      const int64_t e = at(p, i, r[q], c);
       opt_update_k<KIND>(p.op, g[q], w[q], a[q], bb[q]);
-      p.W[i][e[q]] = w[q];
-      if (p.sW1[i]) p.sW1[i][e[q]] = a[q];
-      if (p.sW2[i]) p.sW2[i][e[q]] = bb[q];
+      p.W[i][e] = w[q];
+      if (p.sW1[i]) p.sW1[i][e] = a[q];
+      if (p.sW2[i]) p.sW2[i][e] = bb[q];
       if constexpr (sizeof(CT) == 2)
         if (p.sh[i]) reinterpret_cast<CT*>(p.sh[i])[shadow_index(p, i, r[q], c)] = CvtT<CT>::to(w[q]);
     }
   }
 };
 
-// bias i: db[n] = gscale * sum over the Bp / 32 row tiles of the column partials the producer of delta_i wrote
-// (tile order), then the update
+// bias i: db[n] = gscale * sum over the Bp / 32 row blocks of the column partials the producer of delta_i wrote
+// (block order), then the update
 template <int KIND>
 __device__ __forceinline__ void bias_update(const P& p, int i, int gtid, int gthreads) {
   const int W = p.dim[i + 1], realw = p.real[i + 1], nb = p.Bp / TT;
@@ -338,65 +377,100 @@ __device__ __forceinline__ void update_from(const P& p, int i, const float* g, i
   }
 }
 
-template <typename CT, int KIND>
+// ---- phase epilogues, for either tile shape
+// hidden layer i's output: a = act(v + b), h = dropout(a) (model.py:64-73; the layer-wise path's Philox stream
+// and formula: mask = floor(keep + U(seed, stream + i, m * W + n)), h = a / keep * mask)
+template <int NE>
+__device__ __forceinline__ void epi_forward(const P& p, int i, const Frag<NE>& f) {
+  const int Wd = p.dim[i + 1], n = f.n;
+  const float bias = p.b[i][n];
+  const bool live_n = n < p.real[i + 1];
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    const int m = f.m[j];
+    const int64_t idx = (int64_t)m * Wd + n;
+    const float a = (m < p.B && live_n) ? act_apply(p.act, f.v[j] + bias) : 0.f;
+    float h = a;
+    if (p.keep < 1.f) {
+      const float mk = floorf(p.keep + philox_uniform(p.seed, p.stream + i, (uint64_t)idx));
+      h = (a / p.keep) * mk;
+      p.mask[i][idx] = (uint8_t)mk;                   // the caller's record (read after the launch)
+      pub(&p.am[i][idx], a);
+      pub(&p.dm[i][idx], mk / p.keep);
+    }
+    pub(&p.h[i][idx], h);
+  }
+}
+
+// delta of hidden layer i's output from v = (delta_{i+1} W_{i+1}^T): v * (mask / keep) * act'(a)
+template <int NE>
+__device__ __forceinline__ void epi_delta(const P& p, int i, const Frag<NE>& f, Frag<NE>& dv, const float* av,
+                                          const float* dmv) {
+  const int Wd = p.dim[i + 1], n = f.n;
+  dv.n = n;
+#pragma unroll
+  for (int j = 0; j < NE; ++j) {
+    const int m = f.m[j];
+    float d = 0.f;
+    if (m < p.B && n < p.real[i + 1]) {
+      d = f.v[j];
+      if (p.keep < 1.f) d = d * dmv[j];
+      d = d * act_grad(p.act, av[j]);
+    }
+    dv.m[j] = m;
+    dv.v[j] = d;
+    pub(&p.d[i][(int64_t)m * Wd + n], d);
+  }
+}
+
+template <typename CT, int KIND, bool XD>
 __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
-  __shared__ __attribute__((aligned(16))) char lds[Lds<CT>::BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[Geo<CT>::BYTES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int gtid = blockIdx.x * THREADS + threadIdx.x, gthreads = gridDim.x * THREADS;
   const int L = p.L, Bt = p.Bp / TT;
   const float gs = p.op.gscale;
-  const int c = out_col();
+  const int c = threadIdx.x & 31;               // a thread's column in every tile; rows (threadIdx.x >> 5) + 8 j
   int tn = 0, nb = 0;
   mark(p, tn);
 
-  // ---- forward: h_i = act(src W_i + b_i); padded rows / units are zero
+  // ---- forward: h_i = dropout(act(src W_i + b_i)); padded rows / units are zero
   for (int i = 0; i < L; ++i) {
     const int K = p.dim[i], Wd = p.dim[i + 1], nt = Wd / TT;
+    auto Bw = [&](int n, int k) { return ld4(p.W[i] + (int64_t)k * Wd + n); };
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
-      Tile v;
-      if (i == 0)
-        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4(p, m, k); },
-                                     [&](int n, int k) { return ld4(p.W[0] + (int64_t)k * Wd + n); });
+      if (i == 0)      // (one accessor per call: a select inside it would split the chunk's loads)
+        epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4<XD>(p, m, k); }, Bw));
       else
-        v = wg_tile<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)m * K + k); },
-                                     [&](int n, int k) { return ld4(p.W[i] + (int64_t)k * Wd + n); });
-      const int n = n0 + c;
-      const float bias = p.b[i][n];
-      const bool live_n = n < p.real[i + 1];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = m0 + out_row(j);
-        pub(&p.h[i][(int64_t)m * Wd + n], (m < p.B && live_n) ? act_apply(p.act, v.v[j] + bias) : 0.f);
-      }
+        epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K,
+                                                  [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)m * K + k); }, Bw));
     }
     grid_sync(p, tn, nb);
   }
   // ---- output layer + masked MSE: y = M (h W_L + b_L); e = y - T; delta_L = e M; per-tile statistics and
-  // the column sums of delta_L (b_L's gradient)
+  // the column sums of delta_L (b_L's gradient).  W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k].
   {
     const int K = p.dim[L], nt = p.Np / TT;
+    auto A = [&](int m, int k) { return ldc4(p.h[L - 1], (int64_t)m * K + k); };
+    auto Bw = [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); };
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
-      const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
-      const int n = n0 + c;
+      const int m0 = (t / nt) * TT, n0 = (t % nt) * TT, n = n0 + c;
       const float bias = p.b[L][n];
       float mkv[4], ttv[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {        // the mask / target loads in flight during the GEMM (clamped)
-        const int m = m0 + out_row(j);
-        const int64_t o = p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
+      for (int j = 0; j < 4; ++j) {        // the mask / target loads fly during the GEMM
+        const int64_t o = t_off<XD>(p, m0 + (threadIdx.x >> 5) + 8 * j, n);
         mkv[j] = p.om[o];
         ttv[j] = p.tg[o];
       }
-      // W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k], contiguous along k
-      const Tile v = wg_tile<CT, false, false>(lds, m0, n0, K,
-                                               [&](int m, int k) { return ldc4(p.h[L - 1], (int64_t)m * K + k); },
-                                               [&](int n, int k) { return ld4(p.W[L] + (int64_t)n * K + k); });
-      Tile dl;
+      const Frag<4> v = tile_s<CT, false, false>(lds, m0, n0, K, A, Bw);
+      Frag<4> dl;
+      dl.n = n;
       float sse = 0.f, sae = 0.f, cnt = 0.f, rs[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = m0 + out_row(j);
+        const int m = v.m[j];
         float d = 0.f, se = 0.f;
         if (m < p.B && n < p.N) {
           const float y = mkv[j] * (v.v[j] + bias);
@@ -408,6 +482,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
           d = e * mkv[j];
         }
         pub(&p.d[L][(int64_t)m * p.Np + n], d);
+        dl.m[j] = m;
         dl.v[j] = d;
         rs[j] = se;
       }
@@ -417,7 +492,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         for (int j = 0; j < 4; ++j) rs[j] += __shfl_xor(rs[j], o, 64);
       if ((lane & 31) == 0)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pub(&p.rowp[(int64_t)(n0 / TT) * p.Bp + m0 + out_row(j)], rs[j]);
+        for (int j = 0; j < 4; ++j) pub(&p.rowp[(int64_t)(n0 / TT) * p.Bp + v.m[j]], rs[j]);
       for (int o = 32; o > 0; o >>= 1) {
         sse += __shfl_xor(sse, o, 64);
         sae += __shfl_xor(sae, o, 64);
@@ -429,7 +504,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         pub(&p.totp[slot * 3 + 1], sae);
         pub(&p.totp[slot * 3 + 2], cnt);
       }
-      tile_colsum<CT>(lds, dl, p.colp[L] + (int64_t)(m0 / TT) * p.Np + n0);
+      frag_colsum<CT>(lds, dl, m0, p.colp[L], p.Np);
     }
     grid_sync(p, tn, nb);
   }
@@ -437,8 +512,8 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
   for (int i = L; i >= 0; --i) {
     const int Wi = p.dim[i + 1];                 // layer i's output width (padded)
     const int Ki = p.dim[i];                     // its input width
-    // delta of layer i - 1's output: (delta_i W_i^T) * act'(h_{i-1}), with its column sums
-    const int nd = i > 0 ? (Bt * (Ki / TT)) : 0;
+    // delta of layer i - 1's output: (delta_i W_i^T) * dropout' * act'(a_{i-1}), with its column sums
+    const int nd = i > 0 ? Bt * (Ki / TT) : 0;
     // dW_i: [input][output] (layer L: [output][input]) tiles, K = the batch rows
     const int gr = i == L ? Wi : Ki, gc = i == L ? Ki : Wi;
     const int ng = (gr / TT) * (gc / TT);
@@ -476,54 +551,53 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     const bool side_idle = idle >= (int)gridDim.x / 4;
     if (side_idle && (int)blockIdx.x >= T)
       side(((int)blockIdx.x - T) * THREADS + threadIdx.x, idle * THREADS, blockIdx.x == gridDim.x - 1);
-    for (int t = blockIdx.x; t < nd + ng; t += gridDim.x) {
+    for (int t = blockIdx.x; t < T; t += gridDim.x) {
       if (t < nd) {
-        const int ct = Ki / TT, m0 = (t / ct) * TT, n0 = (t % ct) * TT;
-        const int n = n0 + c;
-        float hv[4];                    // in flight during the GEMM
-#pragma unroll
-        for (int j = 0; j < 4; ++j) hv[j] = ldc(p.h[i - 1], (int64_t)(m0 + out_row(j)) * Ki + n);
-        Tile v;
-        if (i == L)      // B(n = input unit, k = output unit) = W_L[k][n], contiguous along n
-          v = wg_tile<CT, false, true>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
-                                       [&](int n, int k) { return ld4(p.W[L] + (int64_t)k * Ki + n); });
-        else             // B(n = input unit, k = output unit) = W_i[n][k], contiguous along k
-          v = wg_tile<CT, false, false>(lds, m0, n0, Wi, [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); },
-                                        [&](int n, int k) { return ld4(p.W[i] + (int64_t)n * Wi + k); });
-        Tile dv;
+        const int ct = Ki / TT, m0 = (t / ct) * TT, n0 = (t % ct) * TT, n = n0 + c;
+        // the activation (and dropout scale) of layer i - 1 in flight during the GEMM
+        float av[4], dmv[4];
+        const float* asrc = p.keep < 1.f ? p.am[i - 1] : p.h[i - 1];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int m = m0 + out_row(j);
-          dv.v[j] = (m < p.B && n < p.real[i]) ? v.v[j] * act_grad(p.act, hv[j]) : 0.f;
-          pub(&p.d[i - 1][(int64_t)m * Ki + n], dv.v[j]);
+          const int64_t o = (int64_t)(m0 + (threadIdx.x >> 5) + 8 * j) * Ki + n;
+          av[j] = ldc(asrc, o);
+          dmv[j] = p.keep < 1.f ? ldc(p.dm[i - 1], o) : 1.f;
         }
-        tile_colsum<CT>(lds, dv, p.colp[i - 1] + (int64_t)(m0 / TT) * Ki + n0);
+        auto Ad = [&](int m, int k) { return ldc4(p.d[i], (int64_t)m * Wi + k); };
+        Frag<4> v;
+        if (i == L)      // B(n = input unit, k = output unit) = W_L[k][n], contiguous along n
+          v = tile_s<CT, false, true>(lds, m0, n0, Wi, Ad, [&](int nn, int k) { return ld4(p.W[L] + (int64_t)k * Ki + nn); });
+        else             // B(n = input unit, k = output unit) = W_i[n][k], contiguous along k
+          v = tile_s<CT, false, false>(lds, m0, n0, Wi, Ad, [&](int nn, int k) { return ld4(p.W[i] + (int64_t)nn * Wi + k); });
+        Frag<4> dv;
+        epi_delta(p, i - 1, v, dv, av, dmv);
+        frag_colsum<CT>(lds, dv, m0, p.colp[i - 1], Ki);
         continue;
       }
-      const int u = t - nd, ct = gc / TT, m0 = (u / ct) * TT, n0 = (u % ct) * TT;
+      const int u = t - nd, ct = gc / TT, m0 = (u / ct) * TT, n0 = (u % ct) * TT, n = n0 + c;
       int rr[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rr[j] = m0 + out_row(j);
-      TileUpdate<CT, KIND> up;
-      if (i == 0) up.load(p, 0, rr, n0 + c);   // W_0's parameters and slots in flight during the GEMM
-      Tile v;
+      for (int j = 0; j < 4; ++j) rr[j] = m0 + (threadIdx.x >> 5) + 8 * j;
+      TileUpdate<CT, KIND, 4> up;
+      if (i == 0) up.load(p, 0, rr, n);             // W_0's parameters and slots in flight during the GEMM
+      Frag<4> v;
       if (i == L)        // dW_L[n][j] = sum_b delta_L[b][n] h_{L-1}[b][j]
-        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.d[L], (int64_t)k * Wi + m); },
-                                    [&](int n, int k) { return ldc4(p.h[L - 1], (int64_t)k * Ki + n); });
+        v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.d[L], (int64_t)k * Wi + m); },
+                                   [&](int nn, int k) { return ldc4(p.h[L - 1], (int64_t)k * Ki + nn); });
       else if (i > 0)    // dW_i[k][j] = sum_b h_{i-1}[b][k] delta_i[b][j]
-        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)k * Ki + m); },
-                                    [&](int n, int k) { return ldc4(p.d[i], (int64_t)k * Wi + n); });
+        v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)k * Ki + m); },
+                                   [&](int nn, int k) { return ldc4(p.d[i], (int64_t)k * Wi + nn); });
       else               // dW_0[k][j] = sum_b x[b][k] delta_0[b][j]
-        v = wg_tile<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4(p, k, m); },
-                                    [&](int n, int k) { return ldc4(p.d[0], (int64_t)k * Wi + n); });
-      if (i == 0) {      // nothing reads W_0 any more: update it from the tile (padded elements have zero gradient)
-        float gv[4];
+        v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4<XD>(p, k, m); },
+                                   [&](int nn, int k) { return ldc4(p.d[0], (int64_t)k * Wi + nn); });
+      float gv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) gv[j] = v.v[j] * gs;
-        up.apply(p, 0, gv, rr, n0 + c);
+      for (int j = 0; j < 4; ++j) gv[j] = v.v[j] * gs;
+      if (i == 0) {      // nothing reads W_0 any more: update it from the tile (padded elements: zero gradient)
+        up.apply(p, 0, gv, rr, n);
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pub(&p.g[i][(int64_t)(m0 + out_row(j)) * gc + n0 + c], v.v[j] * gs);
+        for (int j = 0; j < 4; ++j) pub(&p.g[i][(int64_t)rr[j] * gc + n], gv[j]);
       }
     }
     if (!side_idle) side(gtid, gthreads, blockIdx.x == gridDim.x - 1);
@@ -534,7 +608,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
 }
 
 struct Layout {
-  size_t h[MAXL], d[MAXL + 1], g[MAXL], colp[MAXL + 1], rowp, totp, total;
+  size_t h[MAXL], d[MAXL + 1], g[MAXL], colp[MAXL + 1], am[MAXL], dm[MAXL], rowp, totp, total;
 };
 Layout layout(const OcfMlpStepArgs& a, int* dim) {
   Layout w{};
@@ -549,6 +623,11 @@ Layout layout(const OcfMlpStepArgs& a, int* dim) {
   for (int i = 0; i <= L; ++i) w.d[i] = take((size_t)a.Bp * dim[i + 1]);
   for (int i = 1; i <= L; ++i) w.g[i] = take((size_t)dim[i] * dim[i + 1]);
   for (int i = 0; i <= L; ++i) w.colp[i] = take((size_t)(a.Bp / TT) * dim[i + 1]);
+  for (int i = 0; i < L; ++i) {
+    const size_t n = a.keep < 1.f ? (size_t)a.Bp * dim[i + 1] : 0;
+    w.am[i] = take(n);
+    w.dm[i] = take(n);
+  }
   w.rowp = take((size_t)(a.Np / TT) * a.Bp);
   w.totp = take((size_t)(a.Bp / TT) * (a.Np / TT) * WAVES * 3);
   w.total = off;
@@ -576,7 +655,13 @@ void check(const OcfMlpStepArgs& a) {
     OCF_CHECK(a.hidden_p[i] % 64 == 0 && a.hidden[i] >= 1 && a.hidden[i] <= a.hidden_p[i],
               "ocf_mlp_step: hidden widths padded to multiples of 64");
   for (int j = 0; j < a.k_blocks; ++j) OCF_CHECK(a.x[j] != nullptr, "ocf_mlp_step: null input block");
-  OCF_CHECK(a.rows && a.out_mask && a.targets && a.ld_x >= a.N && a.ld_t >= a.N, "ocf_mlp_step: batch arrays");
+  OCF_CHECK(a.out_mask && a.targets && a.ld_x >= a.N && a.ld_t >= a.N, "ocf_mlp_step: batch arrays");
+  if (!a.rows)
+    OCF_CHECK(a.ld_x >= a.Np && a.ld_x % 4 == 0 && a.ld_t >= a.Np,
+              "ocf_mlp_step: dense batch arrays (rows == NULL) need ld_x, ld_t >= Np, ld_x % 4 == 0");
+  OCF_CHECK(a.keep > 0.f && a.keep <= 1.f, "ocf_mlp_step: keep in (0, 1]");
+  if (a.keep < 1.f)
+    for (int i = 0; i < a.n_hidden; ++i) OCF_CHECK(a.mask[i] != nullptr, "ocf_mlp_step: dropout masks");
   for (int i = 0; i <= a.n_hidden; ++i) OCF_CHECK(a.W[i] && a.b[i], "ocf_mlp_step: null parameter");
   OCF_CHECK(a.opt.l2 == 0.f, "ocf_mlp_step: l2 must be 0 (the regulariser is not fused)");
   const bool slots = a.opt.kind == OCF_OPT_ADAGRAD || a.opt.kind == OCF_OPT_RMSPROP || a.opt.kind == OCF_OPT_ADAM;
@@ -587,15 +672,20 @@ void check(const OcfMlpStepArgs& a) {
   OCF_CHECK(a.stats && a.work && a.barrier, "ocf_mlp_step: stats / work / barrier");
 }
 
-template <typename CT>
-void launch(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
+template <typename CT, bool XD>
+void launch_x(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
   switch (a.opt.kind) {
-    case OCF_OPT_ADAGRAD: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAGRAD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    case OCF_OPT_RMSPROP: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_RMSPROP>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    case OCF_OPT_ADAM: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAM>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    default: hipLaunchKernelGGL((mlp_step_kernel<CT, 0>), dim3(wgs), dim3(THREADS), 0, s, p);
+    case OCF_OPT_ADAGRAD: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAGRAD, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    case OCF_OPT_RMSPROP: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_RMSPROP, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    case OCF_OPT_ADAM: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAM, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    default: hipLaunchKernelGGL((mlp_step_kernel<CT, 0, XD>), dim3(wgs), dim3(THREADS), 0, s, p);
   }
   OCF_HIP(hipGetLastError());
+}
+template <typename CT>
+void launch(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
+  if (a.rows) launch_x<CT, false>(a, p, wgs, s);
+  else launch_x<CT, true>(a, p, wgs, s);
 }
 
 }  // namespace mlp
@@ -630,6 +720,12 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   for (int i = 0; i <= p.L; ++i) p.d[i] = reinterpret_cast<float*>(ws + w.d[i]);
   for (int i = 1; i <= p.L; ++i) p.g[i] = reinterpret_cast<float*>(ws + w.g[i]);
   for (int i = 0; i <= p.L; ++i) p.colp[i] = reinterpret_cast<float*>(ws + w.colp[i]);
+  for (int i = 0; i < p.L; ++i) {
+    p.am[i] = reinterpret_cast<float*>(ws + w.am[i]);
+    p.dm[i] = reinterpret_cast<float*>(ws + w.dm[i]);
+    p.mask[i] = a->mask[i];
+  }
+  p.keep = a->keep; p.seed = a->seed; p.stream = a->stream;
   p.rowp = reinterpret_cast<float*>(ws + w.rowp);
   p.totp = reinterpret_cast<float*>(ws + w.totp);
   for (int j = 0; j < 3; ++j) p.x[j] = a->x[j];
@@ -645,8 +741,9 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   p.err = async_error_word();
   p.max_polls = 1 << 22;
   p.trace = a->trace;
-  // every workgroup must be resident for the grid barriers; by default one per tile of the busiest phase, at
-  // most 128 (the barriers' arrivals grow with the grid)
+  // every workgroup must be resident for the grid barriers; by default one per 32 x 32 tile of the busiest
+  // phase, at most 128 (the barriers' arrivals grow with the grid) -- or one per CU (at most 256) when a phase
+  // has more than 256 tiles (the wide output layers of the I-AutoRec models on the opt-in generator path)
   int tiles = 0;
   {
     const int bt = p.Bp / mlp::TT;
@@ -654,10 +751,10 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
     for (int i = p.L; i >= 0; --i)
       tiles = std::max(tiles, (i > 0 ? bt * (p.dim[i] / mlp::TT) : 0) + (p.dim[i] / mlp::TT) * (p.dim[i + 1] / mlp::TT));
   }
-  int wgs = a->wgs > 0 ? a->wgs : std::min(tiles, 128);
   int cus = 0, dev = 0;
   OCF_HIP(hipGetDevice(&dev));
   OCF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  int wgs = a->wgs > 0 ? a->wgs : (tiles > 256 ? std::min(cus, 256) : std::min(tiles, 128));
   OCF_CHECK(wgs <= cus, "ocf_mlp_step: wgs must not exceed the CU count (grid barriers)");
   hipStream_t s = (hipStream_t)stream;
   switch (a->compute_dtype) {

@@ -252,7 +252,11 @@ class Model(object):
         return float(st[:, 0].sum()), count
 
     def predict(self, x, batch_size=None, verbose=0):
-        """Returns y = output_mask * (h W_out + b_out) as a float32 CUDA tensor [B, N]."""
+        """Returns y = output_mask * (h W_out + b_out) as a float32 CUDA tensor [B, N].
+
+        Collective under data parallelism with ZeRO-1 (enable_data_parallel(mode="sharded")): the output
+        layer reads the fp32 masters, which each rank holds only 1/G of, so every rank must call predict
+        together (the masters are all-gathered first); a rank-0-only predict would wait forever."""
         e = self.engine
         blocks, out_mask = self._split_inputs(x)
         dummy_t = torch.zeros(e.B, e.N, device=e.dev)
@@ -339,6 +343,8 @@ class Model(object):
 
     # ------------------------------------------------------------------ weights / checkpoints
     def get_weights(self):
+        """Keras-layout weights.  Collective under data parallelism with ZeRO-1 (the sharded fp32 masters
+        are all-gathered first): call it on every rank, as predict and save."""
         return self.engine.get_weights()
 
     def set_weights(self, weights):

@@ -59,7 +59,7 @@ STRUCTS = {
     "OcfMlpStepArgs": (_lib.OcfMlpStepArgs, ["n_hidden", "Bp", "k_blocks", "hidden", "hidden_p", "x", "ld_x", "rows",
                                              "targets", "ld_t", "W", "b", "sW2", "sb2", "shadow", "shadow_blocked",
                                              "act", "compute_dtype", "opt", "stats", "work", "work_bytes", "barrier",
-                                             "wgs", "trace"]),
+                                             "wgs", "trace", "keep", "seed", "stream", "mask"]),
     "OcfBiasActArgs": (_lib.OcfBiasActArgs, ["slabs", "splits", "split_stride", "M", "N", "ld", "bias", "act", "keep",
                                              "seed", "stream", "mask_in", "mask_out", "a_out", "h_out", "h_dtype",
                                              "m_real", "n_real"]),
