@@ -1,8 +1,9 @@
 #!/bin/bash
 # MFMA utilisation evidence (rocprofv3 PMC, one pass per counter group, no other trace domains):
 # ML-20M step at B = 2,048 with dense weight-gradient operands (--sparse-dw 0: the generic MFMA tile
-# kernel) and the default B = 256 step; per-kernel SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES,
-# GRBM_GUI_ACTIVE plus a kernel trace for durations -> gpurun_out/<tag>/
+# kernel), the default B = 256 step, and the Jester step (one ocf_mlp_step launch); per-kernel
+# SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE plus a kernel trace for durations
+# -> gpurun_out/<tag>/ (reduce with tools/mfma_reduce.py)
 set -e -o pipefail
 TAG=${1:-mfma}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -10,8 +11,9 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd /tmp
 export TMPDIR=/tmp
-for cfg in "b2048d:--batch 2048 --sparse-dw 0" "b256:--batch 256"; do
+for cfg in "b2048d:--batch 2048 --sparse-dw 0" "b256:--batch 256" "jester:--config jester --dtype bfloat16"; do
   n=${cfg%%:*}; a=${cfg#*:}
+  mkdir -p $O/$n
   timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d $O/$n/pmc -o p -- python3 $R/bench.py --steps 6 --warmup 2 --cpu-baseline 0 --rmse 0 --fp32-steps 0 \
     --phase-timers 0 $a > $O/$n/pmc.log 2>&1
