@@ -40,6 +40,18 @@ def test_ml1m_bf16(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_ml1m_u_bf16(gpu):
+    """configs[1] as BASELINE words it: "256 users x ~3.7k items" -- the U-AutoRec orientation (6,040 user rows
+    x 3,706 item columns, bench.py --config ml1m_u), the benched dtype, against the oracle"""
+    data = _synth("ml1m_u")
+    assert data.num_cols == 3706 and 6000 < data.train.n_rows <= 6040
+    res = run_parity("bfloat16", "adagrad", 1, "sigmoid", steps=3, B=256, H=500, dropout=0.2, data=data,
+                     envelope=True, sparse_oracle=True, eval_batches=4)
+    assert_low_precision(res, 1e-2)
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_ml20m_bench_step(gpu):
     """bench.py's step (bench.py:176-205: rng='device' reader, f16, gathers, sparse dW, row skipping)"""
