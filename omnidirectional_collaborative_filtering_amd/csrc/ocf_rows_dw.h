@@ -30,6 +30,13 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_E0 = 2;   // entries per row loaded with the row's first loads (E0 = 1 / 3: equal / 3 % slower)
 constexpr int RS_ET = 4;   // entries loaded together beyond those (rows of long batches)
 constexpr int RS_ETL = 8;  // LONG variant: B rows of this many entries in flight per group
+// OCF_RS_GLDS 1: the next row's parameter / slot loads through LDS-DMA (global_load_lds_dwordx4 into the wave's
+// LDS slot, read back by the update) instead of into registers.  The stream-only probe gained 2.5 % with it
+// (tools/probes/opt_glds.hip); in the kernel the ML-20M pair launch moved 305.4 -> 304.0 us but the step and
+// ML-1M did not (profiles/r04_glds/), the kernel's VGPRs rose 75 -> 80: off, kept for the record.
+#ifndef OCF_RS_GLDS
+#define OCF_RS_GLDS 0
+#endif
 
 struct RowsDwArgs {
   float* p; float* s1; float* s2;
@@ -124,6 +131,11 @@ __device__ __forceinline__ void rowpipe_ranks(const RowsDwArgs& ra, const WsJobs
   if (nr == 0) return;
   const __amdgpu_buffer_rsrc_t rp = wt_rsrc(ra.p), r1 = wt_rsrc(ra.s1), r2 = wt_rsrc(ra.s2);
   const CT* Bg = reinterpret_cast<const CT*>(ra.B);
+  // LDS-DMA staging (16-B lanes only): the wave's slot holds one row's p | a (| b), NCH KB each
+  constexpr bool GL = OCF_RS_GLDS && CW == 4;
+  constexpr int SLOT = NCH * 64 * CW;                     // floats per array of a row
+  __shared__ __attribute__((aligned(16))) float gl_slot[GL ? RS_THREADS / 64 : 1][GL ? (ADAM ? 3 : 2) * SLOT : 1];
+  float* slot = gl_slot[GL ? (threadIdx.x >> 6) : 0];
   auto col = [&](int j) { return (lane + 64 * j) * CW; };
   auto off = [&](int m, int j) { return (uint32_t)(((int64_t)m * ra.ld + col(j)) * 4); };   // < 2 GiB: host check
   auto bpiece = [&](int k, int j) { return *reinterpret_cast<const H*>(Bg + (int64_t)k * ra.ldb + col(j)); };
@@ -132,12 +144,24 @@ __device__ __forceinline__ void rowpipe_ranks(const RowsDwArgs& ra, const WsJobs
     r.m = r.lv ? __builtin_amdgcn_readfirstlane(row_of(k0 + stride * i)) : 0;
   };
   auto ld_pa = [&](Row& r) {
+    if constexpr (GL) {
+      // the slot's previous row was read back by stE before this (its ds_reads have returned)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const uint32_t o = off(r.m, j);
-      r.p[j] = V::ld(rp, ra.p, o);
-      r.a[j] = V::ld(r1, ra.s1, o);
-      if constexpr (ADAM) r.b[j] = V::ld(r2, ra.s2, o);
+      for (int j = 0; j < NCH; ++j) {
+        const int64_t e = (int64_t)r.m * ra.ld + col(j);
+        __builtin_amdgcn_global_load_lds(ra.p + e, slot + j * 64 * CW, 16, 0, OCF_OPT_LD_POL);
+        __builtin_amdgcn_global_load_lds(ra.s1 + e, slot + SLOT + j * 64 * CW, 16, 0, OCF_OPT_LD_POL);
+        if constexpr (ADAM) __builtin_amdgcn_global_load_lds(ra.s2 + e, slot + 2 * SLOT + j * 64 * CW, 16, 0, OCF_OPT_LD_POL);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const uint32_t o = off(r.m, j);
+        r.p[j] = V::ld(rp, ra.p, o);
+        r.a[j] = V::ld(r1, ra.s1, o);
+        if constexpr (ADAM) r.b[j] = V::ld(r2, ra.s2, o);
+      }
     }
   };
   auto stB = [&](Row& r) {
@@ -190,6 +214,16 @@ __device__ __forceinline__ void rowpipe_ranks(const RowsDwArgs& ra, const WsJobs
   };
   auto stE = [&](Row& r) {
     if (!r.lv) return;
+    if constexpr (GL) {
+      // this row's LDS-DMA loads (issued by the previous stD, with its B pieces) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        r.p[j] = *reinterpret_cast<const F*>(slot + j * 64 * CW + lane * CW);
+        r.a[j] = *reinterpret_cast<const F*>(slot + SLOT + j * 64 * CW + lane * CW);
+        if constexpr (ADAM) r.b[j] = *reinterpret_cast<const F*>(slot + 2 * SLOT + j * 64 * CW + lane * CW);
+      }
+    }
     F g[NCH];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) g[j] = V::zero();
