@@ -525,23 +525,46 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         const int R = i + 1 == L ? p.dim[L + 1] : p.dim[i + 1], C = i + 1 == L ? p.dim[L] : p.dim[i + 2];
         update_from<CT, KIND>(p, i + 1, p.g[i + 1], (int64_t)R * C, sid, sthreads);
       }
-      if (i == L && last && wave == 0) {
-        // the step's statistics from the per-wave partials, in order
+      if (i == L && last) {
+        // the step's statistics from the per-wave partials, by the whole workgroup in a fixed order: each wave
+        // sums its stride of the slots (8 loads in flight), then the wave butterfly, then the waves through LDS
         const int slots = Bt * (p.Np / TT) * WAVES, ncb = p.Np / TT;
         float a[3] = {0.f, 0.f, 0.f};
-        for (int t = lane; t < slots; t += 64)
-          for (int k = 0; k < 3; ++k) a[k] += ldc(p.totp, (int64_t)t * 3 + k);
+        for (int t0 = threadIdx.x; t0 < slots; t0 += 8 * THREADS) {
+          float v[8][3];
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const int t = t0 + u * THREADS;
+              v[u][k] = t < slots ? ldc(p.totp, (int64_t)t * 3 + k) : 0.f;
+            }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) a[k] += v[u][k];
+        }
         for (int k = 0; k < 3; ++k)
           for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
-        if (lane == 0) {
-          p.stats[0] = a[0];
-          p.stats[1] = a[1];
-          p.stats[2] = a[2];
+        float* ws = reinterpret_cast<float*>(lds + Geo<CT>::CS_OFF);
+        __syncthreads();
+        if (lane == 0)
+          for (int k = 0; k < 3; ++k) ws[wave * 3 + k] = a[k];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          for (int k = 0; k < 3; ++k) p.stats[k] = ((ws[k] + ws[3 + k]) + ws[6 + k]) + ws[9 + k];
           p.stats[3] = 0.f;
         }
-        for (int b = lane; b < p.Bp; b += 64) {
+        // per-row sums over the 32-column blocks, one thread per row, 8 loads in flight
+        for (int b = threadIdx.x; b < p.Bp; b += THREADS) {
           float r = 0.f;
-          for (int cb = 0; cb < ncb; ++cb) r += ldc(p.rowp, (int64_t)cb * p.Bp + b);
+          for (int c0 = 0; c0 < ncb; c0 += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = c0 + u < ncb ? ldc(p.rowp, (int64_t)(c0 + u) * p.Bp + b) : 0.f;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r += v[u];
+          }
           p.stats[4 + b] = r;
         }
       }

@@ -389,10 +389,26 @@ extern "C" int ocf_scatter_batch(const ScatterArgs* args, void* stream) {
             "ocf_scatter_batch: col_cnt needs ecb, mode 0, B <= 4096 and N <= 2^19");
   OCF_CHECK(!(a.rtag_in || a.rtag_out) || (a.rtag >= 1 && a.rtag <= 255),
             "ocf_scatter_batch: row tags need 1 <= rtag <= 255");
-  // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks)
-  float* dense[5] = {a.X, a.Min, a.Mout, a.T, a.Mmiss};
-  for (float* d : dense)
-    if (d) OCF_HIP(hipMemsetAsync(d, 0, (size_t)a.B_pad * a.ld * 4, s));
+  // zero rows [0, B_pad) of every dense output (contiguous [B_pad][ld] blocks); outputs that sit back to back
+  // in memory are cleared by one memset (each memset is a launch of its own)
+  {
+    const size_t blk = (size_t)a.B_pad * a.ld * 4;
+    float* dense[5] = {a.X, a.Min, a.Mout, a.T, a.Mmiss};
+    char* run = nullptr;
+    size_t len = 0;
+    for (float* d : dense) {
+      if (!d) continue;
+      char* c = reinterpret_cast<char*>(d);
+      if (run && c == run + len) {
+        len += blk;
+        continue;
+      }
+      if (run) OCF_HIP(hipMemsetAsync(run, 0, len, s));
+      run = c;
+      len = blk;
+    }
+    if (run) OCF_HIP(hipMemsetAsync(run, 0, len, s));
+  }
   if (a.xin && !a.xin_clean)
     OCF_HIP(hipMemsetAsync(a.xin, 0, (size_t)a.B_pad * a.xin_ld * (a.xin_dtype == OCF_F32 ? 4 : 2), s));
   const int nblk1 = (int)((a.E1 + SC_THREADS - 1) / SC_THREADS);

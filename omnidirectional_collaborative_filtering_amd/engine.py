@@ -723,8 +723,9 @@ class Engine:
         Bp, Np = self.Bp, self.Np
         if self.gen_dense is None:
             self.gen_dense = torch.zeros(6, Bp, Np, device=self.dev, dtype=torch.float32)
-        d = self.gen_dense
-        a.X, a.Min, a.Mout, a.T = ptr(d[0]), ptr(d[1]) if a.feed == 1 else None, ptr(d[2]), ptr(d[3])
+        d = self.gen_dense              # [X, M_out, T, M_in, M_miss, zeros]: the always-written blocks adjacent
+        a.X, a.Mout, a.T = ptr(d[0]), ptr(d[1]), ptr(d[2])  # (the scatter clears adjacent outputs in one memset)
+        a.Min = ptr(d[3]) if a.feed == 1 else None
         a.Mmiss = ptr(d[4]) if (a.feed == 2 or a.both) else None
         a.ld = Np
         a.xin = None
@@ -735,15 +736,15 @@ class Engine:
             call("ocf_scatter_batch", a, cur_stream())
         blocks = [d[0]]
         if self.k >= 2:
-            blocks.append({1: d[1], 2: d[4]}.get(int(a.feed), d[5]))
+            blocks.append({1: d[3], 2: d[4]}.get(int(a.feed), d[5]))
         if self.k >= 3:
             blocks.append(d[4])
         p = [ptr(t) for t in blocks] + [None] * (3 - len(blocks))
         self.rows_real = None
         self._pending_pack = (p, Np, None)          # packed into xin only if the layer-wise path runs after all
-        self._mlp_batch = (p, Np, None, ptr(d[2]), ptr(d[3]))
+        self._mlp_batch = (p, Np, None, ptr(d[1]), ptr(d[2]))
         self._fg_scatter, self._fg_pending, self._fg_batch = a, self._pending_pack, self._mlp_batch
-        self.tseg = dict(dn_t=ptr(d[3]), dn_m=ptr(d[2]), ld_dn=Np, dn_rows=None, n_real=self.N)
+        self.tseg = dict(dn_t=ptr(d[2]), dn_m=ptr(d[1]), ld_dn=Np, dn_rows=None, n_real=self.N)
         self._dense_keep = (d,)
         self.tb = self.gt = self._enc_fused = None
         self._rtag_live = False

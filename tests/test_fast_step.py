@@ -231,5 +231,6 @@ def test_small_model_generator_step_is_one_fused_launch(monkeypatch):
         sa, ma = calls[0][1][0], calls[1][1][0]
         assert sa.X and sa.Mout and sa.T and not sa.xin and not sa.xval1      # the data_gen arrays only
         assert ma.rows is None and ma.x[0] == sa.X and ma.out_mask == sa.Mout and ma.targets == sa.T
+        assert sa.Mout - sa.X == sa.T - sa.Mout == eng.Bp * eng.Np * 4     # one memset clears all three
         assert ma.ld_x == eng.Np and abs(ma.keep - 0.8) < 1e-7 and ma.stream == step * 16
         assert ma.mask[0] == eng.mask[0].data_ptr()
