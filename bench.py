@@ -517,18 +517,26 @@ def main():
 
     # warm-up (untimed): every phase bracketed by HIP events -> per-phase breakdown and the dominant
     # kernel.  The timed region then brackets only that kernel, so the timers cost ~2 events/step.
+    # the first W - 2 warm-up steps with every phase timed (the general path), the last two with only the dominant
+    # kernel's timers: the one-call step records and verifies its template there, not in the timed region
+    w_all = max(1, args.warmup - 2) if args.warmup >= 3 else args.warmup
     eng.enable_timers(bool(args.phase_timers))
-    for i in range(args.warmup):
+    for i in range(w_all):
         step(i)
     torch.cuda.synchronize()
-    phases = eng.phase_times_ms(skip=1 if args.warmup > 1 else 0)
+    phases = eng.phase_times_ms(skip=1 if w_all > 1 else 0)
     cand = {k: v for k, v in phases.items()
             if k in ("dW_in", "dW_out", "dW_pair", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm", "mlp_step")}
     dom = max(cand, key=lambda k: cand[k]["total_ms"]) if cand else None
+    eng.enable_timers(dom is not None, only=[dom] if dom else None)
+    for i in range(w_all, args.warmup):
+        eng.timer_only = {"-"}
+        step(i)
     if world > 1:
         torch.distributed.barrier()
     eng.enable_timers(dom is not None, only=[dom] if dom else None)
     torch.cuda.synchronize()
+    paths0 = dict(eng.step_paths)
     t_start = time.perf_counter()
     nnz = 0
     fused_step = dom == "mlp_step"          # a small model: dense arrays + ocf_mlp_step, no row lists
@@ -551,6 +559,8 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t_start
     host_ms = (t_issued - t_start) / args.steps * 1e3    # host time to issue one step (diagnostic)
+    step_paths = {k: (v - paths0.get(k, 0) if isinstance(v, int) else v)          # one-call vs recorded general
+                  for k, v in eng.step_paths.items()}                            # steps (and why)
     dom_timed = eng.phase_times_ms().get(dom) if dom else None
     eng.timers = None
     row_skip_used = eng._rtag_live          # (the eval batches below reset it)
@@ -676,9 +686,10 @@ def main():
                                                         / (ms_step * 1e-3), 4)},
         "phases_ms": {k: round(v["mean_ms"], 4) for k, v in phases.items()},
         "phases_from": "warm-up steps 2..%d, every phase bracketed by HIP events (timed region: only %s, "
-                       "every %d-th step)" % (args.warmup, dom, TIMER_EVERY),
+                       "every %d-th step)" % (w_all, dom, TIMER_EVERY),
         "setup_s": round(setup_s, 1),
         "host_issue_ms_per_step": round(host_ms, 4),
+        "timed_step_paths": step_paths,
         "row_lists": ("per epoch: ocf_epoch_row_lists for the %d timed batches inside the timed region"
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
                      if epoch_lists else "per step (ocf_row_lists)" if eng.sparse_dw else "n/a",

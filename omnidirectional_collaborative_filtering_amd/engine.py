@@ -106,6 +106,7 @@ class Engine:
         # gathers at ML-100K / ML-1M sizes)
         self.fused_gen = False
         self._fg_args = None                    # (key, scatter arguments) of the fused generator step
+        self.step_paths = {"one_call": 0, "general": 0}   # fast_train_step's choices (diagnostics)
         self.gen_dense = None                   # their dense X / M_in / M_out / T / M_miss / zeros [Bp][Np]
         self.act = _lib.ACT[activation]
         self.activation = activation
@@ -469,7 +470,9 @@ class Engine:
     def _grow_stats(self, n):
         if n <= self.stats_cap:
             return
-        cap = max(n, 2 * self.stats_cap)
+        # at least STATS_MIN_ROWS: every growth re-records the one-call step's template (two general steps),
+        # and a doubling from a handful of rows did that three times in the first 40 steps
+        cap = max(n, 2 * self.stats_cap, self.STATS_MIN_ROWS)
         new = torch.zeros(cap, 4 + self.Bp, device=self.dev, dtype=torch.float32)
         # l2 penalty per step: [cap][2] = (column-sharded kernels, replicated kernels)
         pen = torch.zeros(cap, 2, device=self.dev, dtype=torch.float32)
@@ -479,6 +482,8 @@ class Engine:
         self.stats_hist = new
         self.pen_hist = pen
         self.stats_cap = cap
+
+    STATS_MIN_ROWS = 1024
 
     def _l2_penalty(self):
         """Keras adds l2 * sum(W^2) of every kernel with a W_regularizer (all of them,
@@ -1375,6 +1380,15 @@ class Engine:
 
     _gen_tokens = 0
 
+    def _count_general(self, pl, key):
+        """diagnostics: why a step took the recorded general path"""
+        self.step_paths["general"] += 1
+        why = ("no template" if pl is None else "unverified" if not pl.get("ready") else
+               "key" if pl["key"] != key else "capacity")
+        self.step_paths[why] = self.step_paths.get(why, 0) + 1
+        if why == "key" and self.step_paths.get("key_diff") is None:
+            self.step_paths["key_diff"] = [i for i, (x, y) in enumerate(zip(pl["key"], key)) if x != y]
+
     def fast_train_step(self, gen, bi):
         """Model._train_one's step on generator batch bi through ocf_train_step_rows; False when this step
         must take the general path (then nothing was done)."""
@@ -1395,7 +1409,9 @@ class Engine:
             f = gen.step_fields(bi, self.Np)
             if f is not None and self._fits(pl, f):
                 self._issue(pl, f)
+                self.step_paths["one_call"] += 1
                 return True
+        self._count_general(pl, key)
         # the general path, recorded
         self._grow_stats(self.n_stats + 1)
         per = self._per_step()
@@ -1590,7 +1606,9 @@ class Engine:
             f = gen.step_fields(bi, self.Np)
             if f is not None and self._rank_fits(pl, f):
                 self._rank_issue(pl, f)
+                self.step_paths["one_call"] += 1
                 return True
+        self._count_general(pl, key)
         self._grow_stats(self.n_stats + 1)
         calls = self._recorded_step(gen, bi)
         key = self._rank_key(gen)
