@@ -29,7 +29,10 @@ namespace ocf {
 constexpr int RS_THREADS = 256;
 constexpr int RS_E0 = 2;   // entries per row loaded with the row's first loads (E0 = 1 / 3: equal / 3 % slower)
 constexpr int RS_ET = 4;   // entries loaded together beyond those (rows of long batches)
-constexpr int RS_ETL = 8;  // LONG variant: B rows of this many entries in flight per group
+#ifndef OCF_RS_ETL
+#define OCF_RS_ETL 4
+#endif
+constexpr int RS_ETL = OCF_RS_ETL;  // LONG variant: B rows of this many entries in flight per group
 // OCF_RS_GLDS 1: the next row's parameter / slot loads through LDS-DMA (global_load_lds_dwordx4 into the wave's
 // LDS slot, read back by the update) instead of into registers.  The stream-only probe gained 2.5 % with it
 // (tools/probes/opt_glds.hip); in the kernel the ML-20M pair launch moved 305.4 -> 304.0 us but the step and
