@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--rows-small-waves", type=int, default=-1,
                     help="row-stream dW kernel: 32 workgroups per 128-row tile when 12 would give fewer waves than "
                          "this (-1: library default)")
+    ap.add_argument("--rows-dual", type=int, default=-1,
+                    help="small weights: both updates in one dual-row launch (1, library default) or two (0)")
+    ap.add_argument("--reduce-in-decoder", type=int, default=-1,
+                    help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
+                         "engine default (small weights)")
     ap.add_argument("--fold-jobs", type=int, default=1,
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
@@ -478,6 +483,8 @@ def main():
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
+    if args.reduce_in_decoder >= 0:
+        eng.reduce_in_decoder = bool(args.reduce_in_decoder)
     eng.split_dw_streams = bool(args.split_dw)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
     eng.epoch_row_lists = bool(args.epoch_lists)
@@ -491,6 +498,8 @@ def main():
         _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)
     if args.rows_long >= 0:
         _lib.call("ocf_set_tuning", b"rows_long", int(args.rows_long), None)
+    if args.rows_dual >= 0:
+        _lib.call("ocf_set_tuning", b"rows_dual", int(args.rows_dual), None)
     if args.rows_small_waves >= 0:
         _lib.call("ocf_set_tuning", b"rows_small_waves", int(args.rows_small_waves), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)

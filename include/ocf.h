@@ -161,6 +161,13 @@ typedef struct OcfGatherArgs {
   /* decoder, optional: a device word the launch sets to zero (a caller's flag cleared for free; the
    * engine no longer needs it: ocf_gemm_pair's counter never needs clearing) */
   uint64_t* zero_word;
+  /* decoder, optional (jr and row_arrive both set): the hidden delta's row reduction (ocf_rows_reduce with
+   * OCF_REDUCE_GRAD_ACT on *jr: the same sums and arithmetic, the chunk stats summed into the stats rows) done
+   * in this launch by the last chunk of each batch row to finish.  The chunks store their partials and stats
+   * write-through and count themselves in row_arrive[b] (device uint32 [Bp], zero when first passed: the
+   * last chunk of a row resets it); rows without chunks (padding, no targets) get the zero delta.  jr->part
+   * and jr->chunk_stats must be this launch's part and chunk_stats, jr->H its H. */
+  const struct OcfRowsReduceArgs* jr; uint32_t* row_arrive;
 } OcfGatherArgs;
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);
@@ -300,8 +307,11 @@ int ocf_gemm(const OcfGemmArgs* args, void* stream);
  * and job inputs that reduction writes: train.py:50-51 for both kernels).  When both take the row-stream
  * kernel with the same instance they run as ONE launch: b's workgroups wait, in the kernel, for a's
  * row-reduction workgroups (agent-scope release / acquire on sync[0]), so the two row streams run back to
- * back without a kernel boundary.  sync (NULL = two launches): the hand-off counter below.  Results are
- * identical to the two ocf_gemm calls.
+ * back without a kernel boundary.  On small weights (fewer than ~170 row tiles) whose two updates share
+ * their row lists (sp_rowptr / sp_rowent / row_live equal: the generator's train batches) the launch is
+ * the dual-row form instead: one wave walks column m's entry chain once and updates row m of both
+ * matrices (ocf_set_tuning "rows_dual" 0: two launches).  sync (NULL = two launches): the hand-off
+ * counter below.  Results are identical to the two ocf_gemm calls.
  *
  * The counter only grows, so nothing is reset between launches: word is a device uint64 that is zero
  * when first passed (one hipMemset after allocating it) and that only the library writes afterwards;
@@ -342,6 +352,8 @@ typedef struct OcfRowStepArgs {
   OcfGatherArgs dec;
   OcfGemmArgs dw_out;
   OcfGemmArgs dw_in;
+  /* the decoder's row reduction: jr_on 1 = as jobs of dw_out (its jr), 2 = in the decoder launch (dec.jr;
+   * dec.row_arrive set), 0 = none (dw_out.jr / dec.jr are ignored: the library points them at jr) */
   OcfRowsReduceArgs jr; int jr_on;
   /* (nullable) hipEvent_t recorded on `stream` before / after each launch: encoder, decoder, dW_out, dW_in
    * (the per-kernel timing bench.py reports; recorded only where set) */

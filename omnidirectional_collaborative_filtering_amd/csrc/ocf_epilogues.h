@@ -93,17 +93,21 @@ struct BiasActParams {
 };
 
 // a = act(v + bias), h = dropout(a); stores a / mask / h where the pointers are set; returns h
-__device__ __forceinline__ float bias_act_value(const BiasActParams& p, int m, int n, float v) {
+// (a_o / mk_o, nullable: the activation and the mask value, for a caller that reuses them)
+__device__ __forceinline__ float bias_act_value(const BiasActParams& p, int m, int n, float v, float* a_o = nullptr,
+                                                uint8_t* mk_o = nullptr) {
   int64_t idx = (int64_t)m * p.ld + n;
   bool live = m < p.m_real && n < p.n_real;
   float a = live ? act_apply(p.act, v + p.bias[n]) : 0.f;
   float h = a;
+  if (a_o) *a_o = a;
   if (p.keep < 1.f) {
     uint8_t mk;
     if (p.mask_in) mk = p.mask_in[idx];
     else mk = (uint8_t)floorf(p.keep + philox_uniform(p.seed, p.stream, (uint64_t)idx));
     h = (a / p.keep) * (float)mk;
     if (p.mask_out) p.mask_out[idx] = mk;
+    if (mk_o) *mk_o = mk;
   }
   if (p.a_out) p.a_out[idx] = a;
   if (p.h_out) {

@@ -258,6 +258,12 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   } else if (k == "rows_long") {
     if (previous) *previous = g_rows_long;
     g_rows_long = value < 0 ? -1 : (value ? 1 : 0);
+  } else if (k == "rows_dual") {          // ocf_gemm_pair on small weights: dual-row launch (1) or two (0)
+    if (previous) *previous = g_rows_dual;
+    g_rows_dual = value ? 1 : 0;
+  } else if (k == "rows_dual_count") {    // read (previous) and reset the dual-row launch count
+    if (previous) *previous = g_rows_dual_count;
+    g_rows_dual_count = 0;
   } else if (k == "rows_small_waves") {
     if (previous) *previous = g_rows_small_waves;
     g_rows_small_waves = value;
@@ -354,10 +360,12 @@ extern "C" int ocf_train_step_rows(const OcfRowStepArgs* a, void* stream) {
   OCF_CHECK(ocf_gather_encoder(&a->enc, stream) == 0, ocf_last_error());
   ev(1);
   ev(2);
-  OCF_CHECK(ocf_gather_decoder(&a->dec, stream) == 0, ocf_last_error());
+  OcfGatherArgs d = a->dec;
+  d.jr = a->jr_on == 2 ? &a->jr : nullptr;      // the row reduction in the decoder (d.row_arrive) ...
+  OCF_CHECK(ocf_gather_decoder(&d, stream) == 0, ocf_last_error());
   ev(3);
   OcfGemmArgs o = a->dw_out;
-  o.jr = a->jr_on ? &a->jr : nullptr;
+  o.jr = a->jr_on == 1 ? &a->jr : nullptr;      // ... or as jobs of the dW_out launch
   if (a->pair_sync) {          // both updates in one launch (ocf_gemm_pair): events 4 / 7 bracket it
     ev(4);
     OCF_CHECK(ocf_gemm_pair(&o, &a->dw_in, a->pair_sync, stream) == 0, ocf_last_error());

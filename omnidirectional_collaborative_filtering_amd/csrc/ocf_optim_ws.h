@@ -207,29 +207,30 @@ struct WsJobs {
 
   __host__ __device__ __forceinline__ int count() const {
     int n = jr_on ? jr.Bp : 0;
-    n += jb_part ? (jb_n + 63) / 64 : 0;
+    n += jb_part ? (jb_n + 15) / 16 : 0;
     if (js_sp) n += 1 + (js_rs ? js_M : 0);
     return n;
   }
-  // bias_opt_partials_kernel's four partial groups (k = grp mod 4) summed by one lane, in order
+  // bias_opt_partials_kernel's four partial groups (k = grp mod 4), 16 columns per job: lane 16 q + c sums
+  // group q of column c in row order (16 loads in flight: 4 rounds over 256 partial rows instead of 16 with
+  // one lane per column), then lane c adds the four as the kernel does, (p0 + p1) + (p2 + p3)
   template <int KIND>
   __device__ __forceinline__ void bias_block(int blk, int lane) const {
-    const int i = blk * 64 + lane;
-    if (i >= jb_n) return;
-    // 16 loads in flight per batch (group k & 3 of row k), added per group in row order (the sums are
-    // those of any batch size that is a multiple of 4; 16 keeps the jobs' register footprint small)
+    const int q = lane >> 4, i = blk * 16 + (lane & 15);
+    const bool ok = i < jb_n;
     constexpr int NB = 16;
-    float p[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < jb_parts; k0 += NB) {
+    float p = 0.f;
+    for (int k0 = q; k0 < jb_parts; k0 += 4 * NB) {
       float x[NB];
 #pragma unroll
-      for (int j = 0; j < NB; ++j) x[j] = k0 + j < jb_parts ? jb_part[(int64_t)(k0 + j) * jb_ld + i] : 0.f;
+      for (int j = 0; j < NB; ++j) x[j] = ok && k0 + 4 * j < jb_parts ? jb_part[(int64_t)(k0 + 4 * j) * jb_ld + i] : 0.f;
 #pragma unroll
       for (int j = 0; j < NB; ++j)
-        if (k0 + j < jb_parts) p[j & 3] += x[j];
+        if (k0 + 4 * j < jb_parts) p += x[j];
     }
-    const float p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3];
-    const float g = (p0 + p1) + (p2 + p3);
+    const float p1 = __shfl_down(p, 16, 64), p2 = __shfl_down(p, 32, 64), p3 = __shfl_down(p, 48, 64);
+    if (q != 0 || !ok) return;
+    const float g = (p + p1) + (p2 + p3);
     float w = jb_p[i], a = jb_s1 ? jb_s1[i] : 0.f, b = jb_s2 ? jb_s2[i] : 0.f;
     opt_update_k<KIND>(jb_op, g, w, a, b);
     jb_p[i] = w;
@@ -323,7 +324,7 @@ struct WsJobs {
       }
       j -= jr.Bp;
     }
-    const int nbj = jb_part ? (jb_n + 63) / 64 : 0;
+    const int nbj = jb_part ? (jb_n + 15) / 16 : 0;
     if (j < nbj) bias_block<KIND>(j, lane);
     else if (j == nbj) stats_totals(lane);
     else stats_row(j - nbj - 1, lane);

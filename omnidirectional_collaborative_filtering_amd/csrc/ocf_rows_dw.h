@@ -467,4 +467,198 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
   rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(rb, jb, bx - ps.n_a);
 }
 
+// ---- the dual-row launch (ocf_gemm_pair on small weights): both layers' updates row by row in ONE chain.
+// On the generator's train batches the two weight matrices' rows are the same columns with the same entry
+// lists (the row lists are shared: dW_out[m] = sum of delta_e h[k], dW_in[m] = sum of x_e dh[k] over the
+// entries (e, k) of column m), so a wave walks column m's index chain (row pointer -> entries -> values)
+// once and streams both rows' parameters, slots and B rows.  At about one weight row per wave (ML-1M:
+// 6,040 rows, ML-100K: 943) the two separate launches were each one such chain (18-22 us); here the chain
+// is paid once.  The decoder's row reduction (the dh rows, the hidden-bias partial rows, the stats rows)
+// is either done by the decoder launch (OcfGatherArgs jr: the engine's choice on small weights; nothing
+// here waits) or rides in the first workgroups as in the pair kernel and publishes through the same
+// monotonic counter; then the hidden-bias / stats jobs that read its outputs take the next workgroups and
+// wait for it, and every row workgroup waits for it once, after its first row's index chain and parameter
+// loads are in flight (they need no dh) and before its first dh row load (measured: slower than the two
+// launches, ML-1M 49.5 vs 42.5 us -- the wait puts the reduction back on every row's path).  The per-element sums run in entry order as in
+// rowpipe_ranks (the same fp32 results: the bit-identity tests compare both launches).
+template <typename CT, int KIND, int CW, int NCH>
+struct RdRow {
+  using F = typename RsVec<CW>::F;
+  int m, lo, n;
+  int2 ev;                // the row's first 64 entries (lane i = entry i)
+  float vo, vi;           // their output deltas / input values
+  F po[NCH], ao[NCH], bo[KIND == OCF_OPT_ADAM ? NCH : 1];
+  F pi[NCH], ai[NCH], bi[KIND == OCF_OPT_ADAM ? NCH : 1];
+  WsJobs::BiasPre bias;
+};
+
+template <typename CT, int KIND, int CW, int NCH, int PARTS>
+__global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro, WsJobs jo, RowsDwArgs ri, WsJobs ji,
+                                                                   RsPair ps) {
+  using V = RsVec<CW>;
+  using F = typename V::F;
+  using H = RsH<CT, CW>;
+  constexpr bool ADAM = KIND == OCF_OPT_ADAM;
+  using Row = RdRow<CT, KIND, CW, NCH>;
+  const int bx = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // producers: the output side's jobs (the row reduction), published with the pair kernel's release
+  const int nprod = (jo.count() + 3) / 4;
+  if (bx < nprod) {
+    const int j = bx * 4 + wave;
+    if (j < jo.count()) jo.run<KIND>(j, lane);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0 && ps.n_prod) __hip_atomic_fetch_add(ps.word, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // consumers of the reduction's outputs: the hidden-bias update and the stats jobs
+  const int ncons = (ji.count() + 3) / 4;
+  if (bx < nprod + ncons) {
+    if (ps.n_prod && !pair_wait(ps)) return;
+    const int j = (bx - nprod) * 4 + wave;
+    if (j < ji.count()) ji.run<KIND>(j, lane);
+    return;
+  }
+  const int wb = bx - nprod - ncons;
+  const int t = wb / PARTS, part = wb % PARTS;
+  if (t >= ro.M / 128) return;          // (uniform per workgroup: no wait reached)
+  const int m0 = t * 128;
+  const uint8_t* rec = ro.live ? ro.live + (int64_t)t * OCF_LIVE_REC : nullptr;
+  const int L = rec ? *reinterpret_cast<const int*>(rec) : (ro.M - m0 < 128 ? ro.M - m0 : 128);
+  auto row_of = [&](int k) { return m0 + (rec ? (int)rec[16 + (k & 7) * 16 + (k >> 3)] : k); };
+  if (ro.colsum && rec && part == 0) {      // rows without entries: zero output-bias gradient
+    __shared__ uint8_t live_fl[128];
+    if (tid < 128) live_fl[tid] = 0;
+    __syncthreads();
+    if (tid < L) live_fl[row_of(tid) - m0] = 1;
+    __syncthreads();
+    if (tid < 128 && !live_fl[tid]) ro.colsum[m0 + tid] = 0.f;
+  }
+  const int kb = part * L / PARTS, ke = (part + 1) * L / PARTS;
+  const int nr = __builtin_amdgcn_readfirstlane(ke - kb - wave > 0 ? (ke - kb - wave + 3) / 4 : 0);
+  const __amdgpu_buffer_rsrc_t rpo = wt_rsrc(ro.p), r1o = wt_rsrc(ro.s1), r2o = wt_rsrc(ro.s2);
+  const __amdgpu_buffer_rsrc_t rpi = wt_rsrc(ri.p), r1i = wt_rsrc(ri.s1), r2i = wt_rsrc(ri.s2);
+  const CT* Bo = reinterpret_cast<const CT*>(ro.B);
+  const CT* Bi = reinterpret_cast<const CT*>(ri.B);
+  auto col = [&](int j) { return (lane + 64 * j) * CW; };
+  auto off = [&](int m, int j) { return (uint32_t)(((int64_t)m * ro.ld + col(j)) * 4); };
+  auto piece = [&](const CT* Bg, int64_t ldb, int k, int j) {
+    return *reinterpret_cast<const H*>(Bg + (int64_t)k * ldb + col(j));
+  };
+  auto rdl = [&](int x, int i) { return __builtin_amdgcn_readlane(x, i); };
+  // the row's index chain and parameter loads (nothing here reads the reduction's outputs)
+  auto start = [&](Row& r, int i) {
+    r.m = __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * i));
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const uint32_t o = off(r.m, j);
+      r.po[j] = V::ld(rpo, ro.p, o);
+      r.ao[j] = V::ld(r1o, ro.s1, o);
+      r.pi[j] = V::ld(rpi, ri.p, o);
+      r.ai[j] = V::ld(r1i, ri.s1, o);
+      if constexpr (ADAM) {
+        r.bo[j] = V::ld(r2o, ro.s2, o);
+        r.bi[j] = V::ld(r2i, ri.s2, o);
+      }
+    }
+    r.lo = __builtin_amdgcn_readfirstlane(ro.rowptr[r.m]);
+    r.n = __builtin_amdgcn_readfirstlane(ro.rowptr[r.m + 1]) - r.lo;
+    r.ev = lane < r.n ? ro.rowent[r.lo + lane] : make_int2(0, 0);
+    r.vo = lane < r.n ? ro.vals[r.ev.x] : 0.f;
+    r.vi = lane < r.n ? ri.vals[r.ev.x] : 0.f;
+    if (ro.colsum && jo.cb_p) r.bias = jo.colsum_pre(r.m);
+  };
+  auto acc = [&](F& g, float v, H h) {
+    CT x[CW];
+    __builtin_memcpy(x, &h, sizeof(h));
+    float* gf = reinterpret_cast<float*>(&g);
+#pragma unroll
+    for (int i = 0; i < CW; ++i) gf[i] += v * CvtT<CT>::from(x[i]);
+  };
+  auto update = [&](const RowsDwArgs& ra, __amdgpu_buffer_rsrc_t rp, __amdgpu_buffer_rsrc_t r1,
+                    __amdgpu_buffer_rsrc_t r2, int m, F (&p)[NCH], F (&a)[NCH], F* b, const F (&g)[NCH]) {
+    const OcfOptParams o = ra.op;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      F pj = p[j], aj = a[j], bj = V::zero();
+      if constexpr (ADAM) bj = b[j];
+      float* pf = reinterpret_cast<float*>(&pj);
+      float* af = reinterpret_cast<float*>(&aj);
+      float* bf = reinterpret_cast<float*>(&bj);
+      const float* gf = reinterpret_cast<const float*>(&g[j]);
+#pragma unroll
+      for (int i = 0; i < CW; ++i) opt_update_k<KIND>(o, gf[i] * o.gscale, pf[i], af[i], bf[i]);
+      const uint32_t ob = off(m, j);
+      V::st(rp, ra.p, ob, pj);
+      V::st(r1, ra.s1, ob, aj);
+      if constexpr (ADAM) V::st(r2, ra.s2, ob, bj);
+      if (ra.shadow) {
+        CT hh[CW];
+#pragma unroll
+        for (int i = 0; i < CW; ++i) hh[i] = CvtT<CT>::to(pf[i]);
+        H w;
+        __builtin_memcpy(&w, hh, sizeof(w));
+        *reinterpret_cast<H*>(reinterpret_cast<char*>(ra.shadow) + ((int64_t)m * ra.ld + col(j)) * sizeof(CT)) = w;
+      }
+    }
+  };
+  Row r;
+  if (nr > 0) start(r, 0);
+  if (ps.n_prod && !pair_wait(ps)) return;   // every wave of the workgroup, once (none: the decoder reduced)
+  for (int i = 0; i < nr; ++i) {
+    F go[NCH], gi[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) go[j] = gi[j] = V::zero();
+    float cs = 0.f;
+    int2 ev = r.ev;
+    float vo = r.vo, vi = r.vi;
+    // entries in groups of RS_ETL, every B row of a group (both layers) in flight together
+    for (int e0 = 0; e0 < r.n; e0 += RS_ETL) {
+      if ((e0 & 63) < RS_ETL && e0 >= 64) {     // crossed into the next 64 entries (rows over 64 entries)
+        const int c0 = e0 & ~63;
+        ev = c0 + lane < r.n ? ro.rowent[r.lo + c0 + lane] : make_int2(0, 0);
+        vo = c0 + lane < r.n ? ro.vals[ev.x] : 0.f;
+        vi = c0 + lane < r.n ? ri.vals[ev.x] : 0.f;
+      }
+      H ho[RS_ETL][NCH], hi[RS_ETL][NCH];
+#pragma unroll
+      for (int e = 0; e < RS_ETL; ++e) {
+        const int q = e0 + e;
+        if (q < r.n && (q & ~63) == (e0 & ~63)) {
+          const int k = rdl(ev.y, q & 63);
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            ho[e][j] = piece(Bo, ro.ldb, k, j);
+            hi[e][j] = piece(Bi, ri.ldb, k, j);
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < RS_ETL; ++e) {
+        const int q = e0 + e;
+        if (q < r.n && (q & ~63) == (e0 & ~63)) {
+          const float a = __int_as_float(rdl(__float_as_int(vo), q & 63));
+          const float b = __int_as_float(rdl(__float_as_int(vi), q & 63));
+#pragma unroll
+          for (int j = 0; j < NCH; ++j) {
+            acc(go[j], a, ho[e][j]);
+            acc(gi[j], b, hi[e][j]);
+          }
+          cs += a;
+        }
+      }
+      // a group straddling a 64-entry boundary: continue from the boundary
+      if (((e0 + RS_ETL) & ~63) != (e0 & ~63) && ((e0 + RS_ETL) & 63) != 0) e0 = ((e0 + RS_ETL) & ~63) - RS_ETL;
+    }
+    update(ro, rpo, r1o, r2o, r.m, r.po, r.ao, r.bo, go);
+    update(ri, rpi, r1i, r2i, r.m, r.pi, r.ai, r.bi, gi);
+    if (ro.colsum && lane == 0) {
+      const float v = cs * ro.colsum_scale;
+      ro.colsum[r.m] = v;
+      if (jo.cb_p) jo.colsum_bias<KIND>(r.m, v, r.bias);
+    }
+    if (i + 1 < nr) start(r, i + 1);
+  }
+}
+
 }  // namespace ocf

@@ -66,6 +66,28 @@ struct RowsPair {
   }
 };
 
+struct RowsDual {
+  const RowsLaunch& A;
+  const RowsLaunch& B;
+  RsPair ps;
+  int grid;
+  hipStream_t s;
+  template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
+    if constexpr (PARTS == 32)      // small weights only (one instance per optimizer and width)
+      hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, PARTS>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
+                         A.jb, B.ra, B.jb, ps);
+  }
+};
+
+// the dual-row launch (ocf_rows_dw.h optim_rowdual_kernel): both updates of a small weight pair walk the
+// shared row lists once.  Needs the same lists, live records and row geometry on both sides, the row
+// reduction (if any) as the output side's only job and none on the input side.
+inline bool rows_dual_ok(const OcfGemmArgs& a, const OcfGemmArgs& b, const RowsLaunch& A, const RowsLaunch& B) {
+  return a.sp_rowptr == b.sp_rowptr && a.sp_rowent == b.sp_rowent && a.row_live == b.row_live && !b.sp_colsum &&
+         A.ra.M == B.ra.M && A.ra.ld == B.ra.ld && A.N == B.N && !B.jb.jr_on &&
+         !(A.jb.jr_on && (A.jb.jb_part || A.jb.js_sp));
+}
+
 template <typename CT>
 bool launch_rows(const OcfGemmArgs& g, const EpiOptim::Params& ep, hipStream_t s) {
   RowsLaunch L;
@@ -81,10 +103,12 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
   RowsLaunch A, B;
   if (!rows_setup(a, optim_params(a), A) || !rows_setup(b, optim_params(b), B)) return false;
   if (A.kind != B.kind || A.N != B.N || A.parts != B.parts || A.lng != B.lng || A.small != B.small) return false;
-  // small weights (about one row per wave) keep two launches: there the in-kernel wait (the producers'
-  // L2 write-back, the consumers' polling) cost more than the boundary it replaces (ML-1M 36.9 vs 36.8 us,
-  // ML-100K 25.8 vs 21.7; ML-20M 303 vs 307: tools/step_parts_probe.py)
-  if (A.small) return false;
+  // small weights (about one row per wave): the pair form's in-kernel wait (the producers' L2 write-back, the
+  // consumers' polling) cost more than the boundary it replaces (ML-1M 36.9 vs 36.8 us, ML-100K 25.8 vs 21.7;
+  // ML-20M 303 vs 307: tools/step_parts_probe.py) -- there the dual-row launch walks each row's chain once for
+  // both layers instead (g_rows_dual, "rows_dual"), or two launches
+  const bool dual = A.small && g_rows_dual && rows_dual_ok(a, b, A, B);
+  if (A.small && !dual) return false;
   RsPair ps;
   ps.word = reinterpret_cast<unsigned long long*>(sync.word);
   ps.n_a = A.grid;
@@ -92,7 +116,17 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
   ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
   ps.err = async_error_word();
   ps.max_polls = g_pair_wait_polls;
-  rows_dispatch<CT>(A, RowsPair{A, B, ps, s});
+  if (dual) {
+    ps.n_a = 0;
+    const int nprod = (A.jb.count() + 3) / 4;
+    ps.n_prod = A.jb.jr_on ? nprod : 0;
+    ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
+    const int grid = nprod + (B.jb.count() + 3) / 4 + A.ra.M / 128 * 32;
+    rows_dispatch<CT>(A, RowsDual{A, B, ps, grid, s});
+    ++g_rows_dual_count;
+  } else {
+    rows_dispatch<CT>(A, RowsPair{A, B, ps, s});
+  }
   OCF_HIP(hipGetLastError());
   sync.count = ps.want;
   return true;

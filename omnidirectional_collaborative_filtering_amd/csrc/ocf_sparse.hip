@@ -95,9 +95,22 @@ __device__ __forceinline__ void load_act_piece(const void* h, int64_t ld, int b,
 }
 
 // fixed-order reduction of the groups' per-lane vectors into part[chunk][H]
+// sc1 (write-through / L1-bypassing) buffer accesses of values another workgroup of the same launch reads
+// (MI355X_MICROARCH.md, inter-workgroup visibility: the hand-off table's first row)
+constexpr int RG_SC1 = 16;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1(float* base, int64_t e, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rg_rsrc(base), (uint32_t)(e * 4), 0, RG_SC1);
+}
+__device__ __forceinline__ float ld_sc1(const float* base, int64_t e) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg_rsrc(base), (uint32_t)(e * 4), 0, RG_SC1));
+}
+
 template <int G, int V, int E, int PPL>
 __device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red, float* part, int c, int H, int grp,
-                                              int l) {
+                                              int l, bool wt = false) {
   constexpr int NG = RG_THREADS / G;
 #pragma unroll
   for (int i = 0; i < PPL; ++i)
@@ -111,7 +124,74 @@ __device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red,
       s0 += red[g * H + x];
       if (g + 1 < NG) s1 += red[(g + 1) * H + x];
     }
-    part[(int64_t)c * H + x] = s0 + s1;
+    if (wt) st_sc1(part, (int64_t)c * H + x, s0 + s1);
+    else part[(int64_t)c * H + x] = s0 + s1;
+  }
+}
+
+// The decoder's folded row reduction (OcfGatherArgs jr / row_arrive): after its partial and stats stores
+// (write-through) have landed, each chunk workgroup counts itself in row_arrive[b]; the one that completes
+// the count sums the row's chunk partials in chunk order (sc1 loads) and applies rows_reduce_kernel's
+// OCF_REDUCE_GRAD_ACT arithmetic (grad_act_value) and its stats rows.  a / mk: the row's activation and
+// dropout mask from this workgroup's own hidden epilogue (stash), else read from jr.a_in / jr.mask_in
+// (written by an earlier launch).
+__device__ __forceinline__ void dec_row_tail(const OcfGatherArgs& a, const OcfRowsReduceArgs& r, int b,
+                                             const float* a_sh, const uint8_t* mk_sh, bool stash) {
+  __shared__ int last_sh;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's write-through stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t nch = (uint32_t)(r.row_cptr[b + 1] - r.row_cptr[b]);
+    const uint32_t old = __hip_atomic_fetch_add(&a.row_arrive[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old + 1 == nch;
+    if (last) __hip_atomic_store(&a.row_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_sh = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last_sh) return;
+  const int c0 = r.row_cptr[b], c1 = r.row_cptr[b + 1];
+  const int64_t rb = (int64_t)b * r.H;
+  for (int x = threadIdx.x; x < r.H; x += RG_THREADS) {
+    float v = 0.f;
+    for (int c = c0; c < c1; c += 4) {          // 4 chunks' loads in flight, added in chunk order
+      float q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q[k] = c + k < c1 ? ld_sc1(r.part, (int64_t)(c + k) * r.H + x) : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < c1) v += q[k];
+    }
+    float d = 0.f;
+    if (b < r.B && x < r.n_real) {              // grad_act_value
+      const float av = stash ? a_sh[x] : r.a_in[rb + x];
+      d = v;
+      if (r.keep < 1.f && r.mask_in) d = d * ((float)(stash ? mk_sh[x] : r.mask_in[rb + x]) / r.keep);
+      d = d * act_grad(r.act, av);
+    }
+    store_ct(r.h_out, r.h_dtype, rb + x, d);
+    if (r.db_part) r.db_part[rb + x] = d * r.gscale;
+  }
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+    if (threadIdx.x < 3)
+      for (int c = c0; c < c1; ++c) v += ld_sc1(r.chunk_stats, (int64_t)c * 4 + threadIdx.x);
+    r.stats_part[(int64_t)b * 4 + threadIdx.x] = v;
+    if (threadIdx.x == 0 && r.row_sse) r.row_sse[b] = v;
+  }
+}
+
+// rows no chunk arrives at (padding rows b >= B, rows without targets): the reduction's outputs for an
+// empty row (zero delta, bias-gradient row and stats), by one thread per row (rare)
+__device__ __forceinline__ void dec_zero_rows(const OcfRowsReduceArgs& r) {
+  for (int b = threadIdx.x; b < r.Bp; b += RG_THREADS) {
+    if (b < r.B && r.row_cptr[b + 1] > r.row_cptr[b]) continue;
+    const int64_t rb = (int64_t)b * r.H;
+    for (int x = 0; x < r.H; ++x) {
+      store_ct(r.h_out, r.h_dtype, rb + x, 0.f);
+      if (r.db_part) r.db_part[rb + x] = 0.f;
+    }
+    for (int k = 0; k < 4; ++k) r.stats_part[(int64_t)b * 4 + k] = 0.f;
+    if (r.row_sse) r.row_sse[b] = 0.f;
   }
 }
 
@@ -172,7 +252,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
 }
 
 template <typename WT, typename HT, int G, int PPL>
-__global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a) {
+__global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a, OcfRowsReduceArgs jr) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
@@ -188,6 +268,10 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   const float m = a.aux;
   if (a.zero_word && c == 0 && threadIdx.x == 0)
     __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool fold = a.row_arrive != nullptr;
+  if (fold && c == 0) dec_zero_rows(jr);
+  __shared__ float a_sh[RG_MAX_H];             // (fold) the row's activation / dropout mask from the epilogue
+  __shared__ uint8_t mk_sh[RG_MAX_H];
   float hv[V];
   // entry indices one iteration ahead; the bias of each entry's column loads with its weight row.  The
   // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->
@@ -228,7 +312,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
         for (int k = 0; k < 4; ++k)
           if (c + k < e1) v += q[k];
       }
-      red[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, v));
+      red[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, v, fold ? &a_sh[x] : nullptr, fold ? &mk_sh[x] : nullptr));
     }
     __syncthreads();
 #pragma unroll
@@ -313,12 +397,14 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
     st[grp][1] = sae;
     st[grp][2] = cnt;
   }
-  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l);
+  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l, fold);
   if (threadIdx.x < 3) {
     float v = 0.f;
     for (int g = 0; g < NG; ++g) v += st[g][threadIdx.x];
-    a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
+    if (fold) st_sc1(a.chunk_stats, (int64_t)c * 4 + threadIdx.x, v);
+    else a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
   }
+  if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr);
 }
 
 // per batch row: fixed-order sum of its chunk partials, then the layer epilogue
@@ -402,7 +488,9 @@ template <typename WT> struct Enc {
 template <typename WT, typename HT> struct Dec {
   template <int G, int P> struct L {
     static void go(const OcfGatherArgs& a, hipStream_t s) {
-      hipLaunchKernelGGL((gather_decoder_kernel<WT, HT, G, P>), dim3(a.n_chunks), dim3(RG_THREADS), 0, s, a);
+      OcfRowsReduceArgs r{};
+      if (a.jr && a.row_arrive) r = *a.jr;
+      hipLaunchKernelGGL((gather_decoder_kernel<WT, HT, G, P>), dim3(a.n_chunks), dim3(RG_THREADS), 0, s, a, r);
     }
   };
 };
@@ -447,7 +535,18 @@ extern "C" int ocf_gather_decoder(const OcfGatherArgs* args, void* stream) {
   OCF_CHECK(a.h_dtype == a.w_dtype, "ocf_gather_decoder: h and W must share the compute dtype");
   OCF_CHECK(!a.enc_part || (a.enc_cptr && a.bias_h && (a.keep >= 1.f || a.mask_out) && a.a_out),
             "ocf_gather_decoder: enc_part needs enc_cptr, bias_h, a_out and (with dropout) mask_out");
-  if (a.n_chunks == 0) return 0;
+  OCF_CHECK(!a.jr == !a.row_arrive, "ocf_gather_decoder: jr and row_arrive go together");
+  if (a.jr) {
+    const OcfRowsReduceArgs& r = *a.jr;
+    OCF_CHECK(r.mode == OCF_REDUCE_GRAD_ACT && r.part == a.part && r.chunk_stats == a.chunk_stats && r.H == a.H &&
+                  r.row_cptr && r.h_out && r.a_in && r.stats_part && r.B <= r.Bp && (r.keep >= 1.f || r.mask_in),
+              "ocf_gather_decoder: jr must be OCF_REDUCE_GRAD_ACT over this launch's part / chunk_stats (same H) "
+              "with row_cptr, h_out, a_in, stats_part and (with dropout) mask_in");
+  }
+  if (a.n_chunks == 0) {
+    OCF_CHECK(!a.jr, "ocf_gather_decoder: a folded row reduction needs at least one chunk");
+    return 0;
+  }
   hipStream_t s = (hipStream_t)stream;
   int G, ppl;
   if (a.w_dtype == OCF_F32) { shape_or_throw<float>(a, G, ppl); by_shape<Dec<float, float>::L>(G, ppl, a, s); }

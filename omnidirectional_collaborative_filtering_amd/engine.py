@@ -350,6 +350,12 @@ class Engine:
         # fused single-GPU step: the decoder's δh row reduction as jobs of the dW_out launch
         self.fold_reduce = True
         self._reduce_job = None
+        # ... or done in the decoder launch itself by the last chunk of each batch row (OcfGatherArgs jr /
+        # row_arrive: a per-row arrival counter the launch leaves at zero): None = on small weights, where
+        # ocf_gemm_pair's dual-row form then runs both updates without waiting for it; True / False forced
+        self.reduce_in_decoder = None
+        self._dec_reduced = False
+        self.row_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
         # ... and dW_out + dW_in as one launch (ocf_gemm_pair: a device word the launches count up, never
         # cleared, and its host-side running count)
         self.pair_dw = True
@@ -943,7 +949,6 @@ class Engine:
         elif with_grad:               # dense delta for the output-layer weight-gradient GEMM
             self.d_out.zero_()
             g.d_out, g.d_dtype, g.ld_d = ptr(self.d_out), self.cdt, self.Np
-        call("ocf_gather_decoder", g, cur_stream())
         if with_grad and self.comm is None:
             r = self._reduce_args(tab, part, HpL, _lib.REDUCE_GRAD_ACT)
             r.a_in = ptr(self.a[L - 1])
@@ -955,8 +960,20 @@ class Engine:
             r.out = ptr(self.dhpre if (with_grad and self.comm is not None) else self.dh_raw)
         r.chunk_stats, r.stats_part, r.row_sse = ptr(cst), ptr(self.stats_rows), ptr(self.row_sse_rows)
         self._reduce_job = None
-        if (with_grad and self.comm is None and self._fused_step and self.fold_reduce and self._folds()
-                and self.trainable[0]):
+        self._dec_reduced = False
+        fold = (with_grad and self.comm is None and self._fused_step and self.fold_reduce and self._folds()
+                and self.trainable[0])
+        in_dec = self.reduce_in_decoder
+        if in_dec is None:            # small weights: the dual-row dW launch (ocf_gemm_pair, ocf_rows_impl.h)
+            in_dec = self.Np // TILE * 48 < 8192
+        if fold and in_dec and tab["n_chunks"] > 0:
+            g.jr, g.row_arrive = ctypes.addressof(r), ptr(self.row_arrive)
+            self._last_jr = r             # (kept alive: the recorded step's decoder arguments point at it)
+            self._dec_reduced = True
+        call("ocf_gather_decoder", g, cur_stream())
+        if g.jr:
+            pass                          # done by the decoder's last chunk of each row
+        elif fold:
             self._reduce_job = r          # rides in the dW_out launch (OcfGemmArgs jr), see _backward_gather
             self._last_jr = r             # (kept alive: the recorded step's dW_out arguments point at it)
         else:
@@ -1172,6 +1189,8 @@ class Engine:
             late = jobs_out
             if self._reduce_job is not None:
                 jobs_out.update(jr=ctypes.addressof(self._reduce_job))
+                late = jobs_in
+            elif self._dec_reduced:         # (the decoder reduced: the same job layout, nothing to wait for)
                 late = jobs_in
             if self.trainable[0]:
                 sb = self.slots[0][1]
@@ -1473,7 +1492,11 @@ class Engine:
         if g_out.jr:
             ctypes.memmove(ctypes.addressof(st.jr), g_out.jr, ctypes.sizeof(st.jr))
             st.jr_on = 1
+        elif dec.jr:
+            ctypes.memmove(ctypes.addressof(st.jr), dec.jr, ctypes.sizeof(st.jr))
+            st.jr_on = 2
         st.dw_out.jr = None
+        st.dec.jr = None
         st.pair_sync = sync
         pl = dict(key=key, st=st, cap_enc=self._gbuf["part_enc"].numel() // self.Hp[0],
                   cap_dec=min(self._gbuf["part_dec"].numel() // self.Hp[-1], self._gbuf["chunk_stats"].numel() // 4),
@@ -1526,10 +1549,11 @@ class Engine:
             return False
         b = lambda x: ctypes.string_at(ctypes.addressof(x), ctypes.sizeof(x))
         o = type(g_out).from_buffer_copy(g_out)
-        jr_ok = (not g_out.jr and not st.jr_on) or (
-            g_out.jr and st.jr_on and ctypes.string_at(g_out.jr, ctypes.sizeof(st.jr)) == b(st.jr))
-        o.jr = None
-        return jr_ok and b(enc) == b(st.enc) and b(dec) == b(st.dec) and b(o) == b(st.dw_out) and b(g_in) == b(st.dw_in)
+        d = type(dec).from_buffer_copy(dec)
+        on, src = (1, g_out.jr) if g_out.jr else ((2, dec.jr) if dec.jr else (0, None))
+        jr_ok = on == st.jr_on and (not on or ctypes.string_at(src, ctypes.sizeof(st.jr)) == b(st.jr))
+        o.jr = d.jr = None
+        return jr_ok and b(enc) == b(st.enc) and b(d) == b(st.dec) and b(o) == b(st.dw_out) and b(g_in) == b(st.dw_in)
 
     # phase -> (event slot before, after) in OcfRowStepArgs.ev; dW_pair with ocf_gemm_pair
     _EV_SLOTS = {"enc_gemm": (0, 1), "dec_gemm_mse": (2, 3), "dW_out": (4, 5), "dW_in": (6, 7), "dW_pair": (4, 7)}

@@ -2,6 +2,8 @@
 bit-identical to the general path (four library calls per step) -- weights, optimizer slots, the 16-bit
 shadows and the logged history -- over two epochs with dropout, the reference's reciprocal split (NumPy's
 MT19937 draws on the device) and Adagrad / Adam; and the one-call step really ran."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -54,6 +56,7 @@ def test_fast_step_bit_identical(gpu, cd, opt, sparsity):
 
 def _run_pair(pair, cd, opt, shape):
     import torch
+    from omnidirectional_collaborative_filtering_amd import _lib
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.model import omni_model
@@ -70,12 +73,18 @@ def _run_pair(pair, cd, opt, shape):
     eng = om.engine
     eng.pair_dw = pair
     gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
-    h = m.fit_generator(gen, min(6, gen.num_batches - 1), epochs=1, verbose=0).history
+    _lib.call("ocf_set_tuning", b"rows_dual_count", 0, None)
+    n = min(6, gen.num_batches - 1)
+    h = m.fit_generator(gen, n, epochs=1, verbose=0).history
     torch.cuda.synchronize()
-    # the pair launches' producer count (never cleared; the host keeps its running twin): the pair ran on
-    # weights of more than 170 row tiles (smaller ones keep two launches), every launch on the same word
-    ran = eng.pair_state.count > 0
-    assert ran == (pair and eng.Np // 128 > 170)
+    dual = ctypes.c_int(-1)
+    _lib.call("ocf_set_tuning", b"rows_dual_count", 0, ctypes.byref(dual))
+    # one launch per step: on weights of more than 170 row tiles the pair form, which advances the producers'
+    # count (never cleared; the host keeps its running twin; every launch on the same word); on smaller ones
+    # the dual-row form (the decoder did the row reduction: nothing to count)
+    large = eng.Np // 128 > 170
+    assert (eng.pair_state.count > 0) == (pair and large)
+    assert dual.value == (n if pair and not large else 0)
     assert eng.pair_sync[0].item() == eng.pair_state.count and eng.pair_state.count % ((eng.Bp + 3) // 4) == 0
     st = [t.cpu().numpy().copy() for sw, sb in eng.slots for t in sw + sb if t is not None]
     sh = [t.float().cpu().numpy() for t in eng.Wsh if t is not None]

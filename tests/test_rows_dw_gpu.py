@@ -371,31 +371,36 @@ def test_rows_job_only_workgroups_stay_in_bounds(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cd", ["float16", "float32"])
-def test_engine_fold_reduce_bit_identical(gpu, cd):
+@pytest.mark.parametrize("cd,B", [("float16", 128), ("float32", 128), ("bfloat16", 100)])
+def test_engine_fold_reduce_bit_identical(gpu, cd, B):
     """The decoder's δh row reduction as jobs of the dW_out launch (Engine.fold_reduce; the hidden-bias and
-    stats jobs then ride in dW_in) against its own ocf_rows_reduce launch: identical losses, weights, slots,
-    shadows and per-step stats."""
+    stats jobs then ride in dW_in), or in the decoder launch by each row's last chunk (reduce_in_decoder:
+    write-through partials and a per-row arrival counter; B = 100 leaves 28 padding rows for its zero-row
+    pass), against its own ocf_rows_reduce launch: identical losses, weights, slots, shadows and per-step
+    stats; the arrival counters are back at zero after every launch."""
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     out = []
-    for fold in (False, True):
-        rd, gen = _gen_for(900, 4000, 60000, 128, 0.5, seed=8)
-        om = om_ = omni_model(1, 200, 4000, 128, dense_activation="sigmoid", use_causal_info=False,
+    for fold, in_dec in ((False, False), (True, False), (True, True)):
+        rd, gen = _gen_for(900, 4000, 60000, B, 0.5, seed=8)
+        om = om_ = omni_model(1, 200, 4000, B, dense_activation="sigmoid", use_causal_info=False,
                               dropout_probability=0.2, compute_dtype=cd, seed=4)
         eng = om.engine
         eng.fold_reduce = fold
+        eng.reduce_in_decoder = in_dec
         m = om.model
         m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
         h = m.fit_generator(gen, 5, epochs=1, verbose=0).history
         torch.cuda.synchronize()
+        assert eng._dec_reduced == in_dec and int(eng.row_arrive.abs().sum()) == 0
         out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
                     [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
                     [t.clone() for t in eng.Wsh if t is not None]))
         del om_
-    assert out[0][0] == out[1][0]
-    for a, b in zip(out[0][1], out[1][1]):
-        assert torch.equal(a, b)
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        for a, b in zip(out[0][1], o[1]):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.gpu
@@ -463,6 +468,55 @@ def test_rows_long_variant_bit_identical(gpu, cd, shape, opt):
             del om_
     finally:
         _lib.call("ocf_set_tuning", b"rows_long", -1, None)
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", ["adagrad", "rmsprop", "adam"])
+@pytest.mark.parametrize("cd,shape,skip", [
+    ("float16", (900, 4000, 40000, 128, 0.5), "always"),   # ~1.4 entries per weight row, live records
+    ("bfloat16", (3706, 6040, 1000209, 256, 0.0), True),    # ML-1M I-AutoRec: ~11 per row
+    ("float32", (1682, 943, 100000, 256, 0.0), True),       # ML-100K I-AutoRec: ~16 per row
+    ("float16", (5000, 1024, 1500000, 2048, 1.0), True),    # rows over 64 and over 1,024 entries
+])
+def test_rows_dual_bit_identical(gpu, cd, shape, skip, opt):
+    """ocf_gemm_pair's dual-row form on small weights (one chain per column for both layers' rows, the row
+    reduction riding in its first workgroups; ocf_set_tuning "rows_dual") against the two row-stream
+    launches: identical losses, weights, slots and shadows for every optimizer and compute dtype, and the
+    dual launch really ran (one per step)"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, B, skew = shape
+    mk = {"adagrad": lambda: O.Adagrad(lr=0.01, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=0.001),
+          "adam": lambda: O.Adam(lr=0.001)}[opt]
+    out = []
+    prev = ctypes.c_int(0)
+    n = 0
+    try:
+        for dual in (0, 1):
+            _lib.call("ocf_set_tuning", b"rows_dual", dual, ctypes.byref(prev))
+            _lib.call("ocf_set_tuning", b"rows_dual_count", 0, None)
+            rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=13)
+            om = om_ = omni_model(1, 500 if cd != "float32" else 200, cols, B, dense_activation="sigmoid",
+                                  use_causal_info=False, dropout_probability=0.2, compute_dtype=cd, seed=4)
+            eng = om.engine
+            eng.row_skip = skip
+            m = om.model
+            m.compile(mk(), "mean_squared_error", metrics=["mae"])
+            n = min(4, gen.num_batches)
+            h = m.fit_generator(gen, n, epochs=1, verbose=0).history
+            torch.cuda.synchronize()
+            cnt = ctypes.c_int(-1)
+            _lib.call("ocf_set_tuning", b"rows_dual_count", 0, ctypes.byref(cnt))
+            assert cnt.value == (n if dual else 0), (dual, cnt.value)
+            out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                        [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                        [t.clone() for t in eng.Wsh if t is not None]))
+            del om_
+    finally:
+        _lib.call("ocf_set_tuning", b"rows_dual", 1, None)
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
