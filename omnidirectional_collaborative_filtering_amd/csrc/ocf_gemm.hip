@@ -261,6 +261,10 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
   } else if (k == "rows_dual") {          // ocf_gemm_pair on small weights: dual-row launch (1) or two (0)
     if (previous) *previous = g_rows_dual;
     g_rows_dual = value ? 1 : 0;
+  } else if (k == "rows_dual_parts") {    // dual-row launch parts per tile: 0 by size, 16 or 32
+    if (previous) *previous = g_rows_dual_parts;
+    OCF_CHECK(value == 0 || value == 16 || value == 32, "ocf_set_tuning: rows_dual_parts 0, 16 or 32");
+    g_rows_dual_parts = value;
   } else if (k == "rows_dual_count") {    // read (previous) and reset the dual-row launch count
     if (previous) *previous = g_rows_dual_count;
     g_rows_dual_count = 0;

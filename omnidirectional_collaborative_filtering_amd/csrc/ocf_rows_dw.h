@@ -481,6 +481,16 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
 // loads are in flight (they need no dh) and before its first dh row load (measured: slower than the two
 // launches, ML-1M 49.5 vs 42.5 us -- the wait puts the reduction back on every row's path).  The per-element sums run in entry order as in
 // rowpipe_ranks (the same fp32 results: the bit-identity tests compare both launches).
+#ifndef OCF_RD_ETL
+#define OCF_RD_ETL 2
+#endif
+constexpr int RD_ETL = OCF_RD_ETL;   // dual-row launch: entries per group (both layers' B rows in flight)
+#ifndef OCF_RD_LATE_IN
+#define OCF_RD_LATE_IN 1
+#endif
+// 1: the input layer's parameter / slot loads issued after the entry groups (fewer VGPRs: the waves of a
+// small weight fit the chip in one round), 0: with the output layer's at the row's start
+constexpr int RD_LATE_IN = OCF_RD_LATE_IN;
 template <typename CT, int KIND, int CW, int NCH>
 struct RdRow {
   using F = typename RsVec<CW>::F;
@@ -547,20 +557,35 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   };
   auto rdl = [&](int x, int i) { return __builtin_amdgcn_readlane(x, i); };
   // the row's index chain and parameter loads (nothing here reads the reduction's outputs)
-  auto start = [&](Row& r, int i) {
-    r.m = __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * i));
+  auto ld_in = [&](Row& r) {
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const uint32_t o = off(r.m, j);
+      r.pi[j] = V::ld(rpi, ri.p, o);
+      r.ai[j] = V::ld(r1i, ri.s1, o);
+      if constexpr (ADAM) r.bi[j] = V::ld(r2i, ri.s2, o);
+    }
+  };
+  auto ld_out = [&](Row& r) {
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const uint32_t o = off(r.m, j);
       r.po[j] = V::ld(rpo, ro.p, o);
       r.ao[j] = V::ld(r1o, ro.s1, o);
-      r.pi[j] = V::ld(rpi, ri.p, o);
-      r.ai[j] = V::ld(r1i, ri.s1, o);
-      if constexpr (ADAM) {
-        r.bo[j] = V::ld(r2o, ro.s2, o);
-        r.bi[j] = V::ld(r2i, ri.s2, o);
-      }
+      if constexpr (ADAM) r.bo[j] = V::ld(r2o, ro.s2, o);
     }
+  };
+  auto start = [&](Row& r, int i) {
+    r.m = __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * i));
+    if constexpr (RD_LATE_IN < 2 || RD_LATE_IN == 3 && false)
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const uint32_t o = off(r.m, j);
+      r.po[j] = V::ld(rpo, ro.p, o);
+      r.ao[j] = V::ld(r1o, ro.s1, o);
+      if constexpr (ADAM) r.bo[j] = V::ld(r2o, ro.s2, o);
+    }
+    if constexpr (RD_LATE_IN < 1) ld_in(r);
     r.lo = __builtin_amdgcn_readfirstlane(ro.rowptr[r.m]);
     r.n = __builtin_amdgcn_readfirstlane(ro.rowptr[r.m + 1]) - r.lo;
     r.ev = lane < r.n ? ro.rowent[r.lo + lane] : make_int2(0, 0);
@@ -612,17 +637,17 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
     float cs = 0.f;
     int2 ev = r.ev;
     float vo = r.vo, vi = r.vi;
-    // entries in groups of RS_ETL, every B row of a group (both layers) in flight together
-    for (int e0 = 0; e0 < r.n; e0 += RS_ETL) {
-      if ((e0 & 63) < RS_ETL && e0 >= 64) {     // crossed into the next 64 entries (rows over 64 entries)
+    // entries in groups of RD_ETL, every B row of a group (both layers) in flight together
+    for (int e0 = 0; e0 < r.n; e0 += RD_ETL) {
+      if ((e0 & 63) < RD_ETL && e0 >= 64) {     // crossed into the next 64 entries (rows over 64 entries)
         const int c0 = e0 & ~63;
         ev = c0 + lane < r.n ? ro.rowent[r.lo + c0 + lane] : make_int2(0, 0);
         vo = c0 + lane < r.n ? ro.vals[ev.x] : 0.f;
         vi = c0 + lane < r.n ? ri.vals[ev.x] : 0.f;
       }
-      H ho[RS_ETL][NCH], hi[RS_ETL][NCH];
+      H ho[RD_ETL][NCH], hi[RD_ETL][NCH];
 #pragma unroll
-      for (int e = 0; e < RS_ETL; ++e) {
+      for (int e = 0; e < RD_ETL; ++e) {
         const int q = e0 + e;
         if (q < r.n && (q & ~63) == (e0 & ~63)) {
           const int k = rdl(ev.y, q & 63);
@@ -634,7 +659,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
         }
       }
 #pragma unroll
-      for (int e = 0; e < RS_ETL; ++e) {
+      for (int e = 0; e < RD_ETL; ++e) {
         const int q = e0 + e;
         if (q < r.n && (q & ~63) == (e0 & ~63)) {
           const float a = __int_as_float(rdl(__float_as_int(vo), q & 63));
@@ -648,10 +673,24 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
         }
       }
       // a group straddling a 64-entry boundary: continue from the boundary
-      if (((e0 + RS_ETL) & ~63) != (e0 & ~63) && ((e0 + RS_ETL) & 63) != 0) e0 = ((e0 + RS_ETL) & ~63) - RS_ETL;
+      if (((e0 + RD_ETL) & ~63) != (e0 & ~63) && ((e0 + RD_ETL) & 63) != 0) e0 = ((e0 + RD_ETL) & ~63) - RD_ETL;
+    }
+    if constexpr (RD_LATE_IN == 3) {      // one layer's state at a time
+      asm volatile("" ::: "memory");
+      ld_out(r);
+      update(ro, rpo, r1o, r2o, r.m, r.po, r.ao, r.bo, go);
+      asm volatile("" ::: "memory");
+      ld_in(r);
+      update(ri, rpi, r1i, r2i, r.m, r.pi, r.ai, r.bi, gi);
+    } else {
+    if constexpr (RD_LATE_IN >= 1) {
+      asm volatile("" ::: "memory");      // (keeps the compiler from hoisting these loads above the groups)
+      if constexpr (RD_LATE_IN >= 2) ld_out(r);
+      ld_in(r);
     }
     update(ro, rpo, r1o, r2o, r.m, r.po, r.ao, r.bo, go);
     update(ri, rpi, r1i, r2i, r.m, r.pi, r.ai, r.bi, gi);
+    }
     if (ro.colsum && lane == 0) {
       const float v = cs * ro.colsum_scale;
       ro.colsum[r.m] = v;

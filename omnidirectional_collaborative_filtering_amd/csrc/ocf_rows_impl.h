@@ -72,10 +72,16 @@ struct RowsDual {
   RsPair ps;
   int grid;
   hipStream_t s;
+  int parts;
   template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
-    if constexpr (PARTS == 32)      // small weights only (one instance per optimizer and width)
-      hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, PARTS>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
-                         A.jb, B.ra, B.jb, ps);
+    if constexpr (PARTS == 32) {    // small weights only (two instances per optimizer and width)
+      if (parts == 16)
+        hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, 16>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
+                           A.jb, B.ra, B.jb, ps);
+      else
+        hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, 32>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
+                           A.jb, B.ra, B.jb, ps);
+    }
   }
 };
 
@@ -121,8 +127,12 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
     const int nprod = (A.jb.count() + 3) / 4;
     ps.n_prod = A.jb.jr_on ? nprod : 0;
     ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
-    const int grid = nprod + (B.jb.count() + 3) / 4 + A.ra.M / 128 * 32;
-    rows_dispatch<CT>(A, RowsDual{A, B, ps, grid, s});
+    // parts per 128-row tile: 32 (about one row per wave) while the waves fit the chip's slots at the dual
+    // kernel's ~110-125 VGPRs (4 waves per SIMD: 4,096), else 16 (ML-1M's 48 tiles: 3,072 waves of ~2 rows
+    // instead of 6,144 in 1.5 rounds); g_rows_dual_parts forces one ("rows_dual_parts")
+    const int parts = g_rows_dual_parts ? g_rows_dual_parts : (A.ra.M / 128 * 32 * 4 > 4096 ? 16 : 32);
+    const int grid = nprod + (B.jb.count() + 3) / 4 + A.ra.M / 128 * parts;
+    rows_dispatch<CT>(A, RowsDual{A, B, ps, grid, s, parts});
     ++g_rows_dual_count;
   } else {
     rows_dispatch<CT>(A, RowsPair{A, B, ps, s});

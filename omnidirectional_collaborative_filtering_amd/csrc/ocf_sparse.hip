@@ -108,22 +108,27 @@ __device__ __forceinline__ float ld_sc1(const float* base, int64_t e) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg_rsrc(base), (uint32_t)(e * 4), 0, RG_SC1));
 }
 
+constexpr int RG_XPT = (RG_MAX_H + RG_THREADS - 1) / RG_THREADS;   // columns per thread in the row loops
+
 template <int G, int V, int E, int PPL>
 __device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red, float* part, int c, int H, int grp,
-                                              int l, bool wt = false) {
+                                              int l, bool wt = false, bool keep_only = false,
+                                              float* own = nullptr) {
   constexpr int NG = RG_THREADS / G;
 #pragma unroll
   for (int i = 0; i < PPL; ++i)
 #pragma unroll
     for (int k = 0; k < E; ++k) red[grp * H + (l + G * i) * E + k] = acc[i * E + k];
   __syncthreads();
-  for (int x = threadIdx.x; x < H; x += RG_THREADS) {
+  for (int x = threadIdx.x, i = 0; x < H; x += RG_THREADS, ++i) {
     float s0 = 0.f, s1 = 0.f;
 #pragma unroll
     for (int g = 0; g < NG; g += 2) {
       s0 += red[g * H + x];
       if (g + 1 < NG) s1 += red[(g + 1) * H + x];
     }
+    if (own) own[i] = s0 + s1;            // (this thread's columns x = tid + RG_THREADS i)
+    if (keep_only) continue;
     if (wt) st_sc1(part, (int64_t)c * H + x, s0 + s1);
     else part[(int64_t)c * H + x] = s0 + s1;
   }
@@ -135,24 +140,34 @@ __device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red,
 // OCF_REDUCE_GRAD_ACT arithmetic (grad_act_value) and its stats rows.  a / mk: the row's activation and
 // dropout mask from this workgroup's own hidden epilogue (stash), else read from jr.a_in / jr.mask_in
 // (written by an earlier launch).
+// solo: the row's only chunk is this workgroup's -- no stores to hand off, no counter: its own column sums
+// (own) and stats total (own_st, threads 0..2) are the row's, added to 0 as the chunk loop would.
 __device__ __forceinline__ void dec_row_tail(const OcfGatherArgs& a, const OcfRowsReduceArgs& r, int b,
-                                             const float* a_sh, const uint8_t* mk_sh, bool stash) {
+                                             const float* a_sh, const uint8_t* mk_sh, bool stash, bool solo,
+                                             const float* own, float own_st) {
   __shared__ int last_sh;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's write-through stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t nch = (uint32_t)(r.row_cptr[b + 1] - r.row_cptr[b]);
-    const uint32_t old = __hip_atomic_fetch_add(&a.row_arrive[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old + 1 == nch;
-    if (last) __hip_atomic_store(&a.row_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_sh = last ? 1 : 0;
+  if (!solo) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t nch = (uint32_t)(r.row_cptr[b + 1] - r.row_cptr[b]);
+      const uint32_t old = __hip_atomic_fetch_add(&a.row_arrive[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = old + 1 == nch;
+      if (last) __hip_atomic_store(&a.row_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_sh = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_sh) return;
   }
-  __syncthreads();
-  if (!last_sh) return;
-  const int c0 = r.row_cptr[b], c1 = r.row_cptr[b + 1];
+  const int c0 = r.row_cptr[b], c1 = solo ? c0 : r.row_cptr[b + 1];
   const int64_t rb = (int64_t)b * r.H;
-  for (int x = threadIdx.x; x < r.H; x += RG_THREADS) {
+  float sq[4];                                  // the first 4 chunks' stats, loaded with the partials
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    sq[k] = threadIdx.x < 3 && c0 + k < c1 ? ld_sc1(r.chunk_stats, (int64_t)(c0 + k) * 4 + threadIdx.x) : 0.f;
+  for (int x = threadIdx.x, i = 0; x < r.H; x += RG_THREADS, ++i) {
     float v = 0.f;
+    if (solo) v += own[i];
     for (int c = c0; c < c1; c += 4) {          // 4 chunks' loads in flight, added in chunk order
       float q[4];
 #pragma unroll
@@ -173,8 +188,13 @@ __device__ __forceinline__ void dec_row_tail(const OcfGatherArgs& a, const OcfRo
   }
   if (threadIdx.x < 4) {
     float v = 0.f;
-    if (threadIdx.x < 3)
-      for (int c = c0; c < c1; ++c) v += ld_sc1(r.chunk_stats, (int64_t)c * 4 + threadIdx.x);
+    if (threadIdx.x < 3) {
+      if (solo) v += own_st;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c0 + k < c1) v += sq[k];
+      for (int c = c0 + 4; c < c1; ++c) v += ld_sc1(r.chunk_stats, (int64_t)c * 4 + threadIdx.x);
+    }
     r.stats_part[(int64_t)b * 4 + threadIdx.x] = v;
     if (threadIdx.x == 0 && r.row_sse) r.row_sse[b] = v;
   }
@@ -397,14 +417,23 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
     st[grp][1] = sae;
     st[grp][2] = cnt;
   }
-  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l, fold);
+  // (fold) a row of one chunk keeps its sums in registers: nothing to hand off
+  const bool solo = fold && jr.row_cptr[b + 1] - jr.row_cptr[b] == 1;
+  float own[RG_XPT];
+  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l, fold, solo, own);
+  float own_st = 0.f;
   if (threadIdx.x < 3) {
     float v = 0.f;
     for (int g = 0; g < NG; ++g) v += st[g][threadIdx.x];
-    if (fold) st_sc1(a.chunk_stats, (int64_t)c * 4 + threadIdx.x, v);
-    else a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
+    own_st = v;
+    if (solo) {
+    } else if (fold) {
+      st_sc1(a.chunk_stats, (int64_t)c * 4 + threadIdx.x, v);
+    } else {
+      a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
+    }
   }
-  if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr);
+  if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr, solo, own, own_st);
 }
 
 // per batch row: fixed-order sum of its chunk partials, then the layer epilogue

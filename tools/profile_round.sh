@@ -14,7 +14,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$O/tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/tests.log" 2>&1
   tail -3 "$O/tests.log"
 fi
 timeout -k 10 400 python bench.py "$@" > "$O/bench.log" 2>&1
