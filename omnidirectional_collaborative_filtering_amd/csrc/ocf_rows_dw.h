@@ -630,7 +630,13 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   Row r;
   if (nr > 0) start(r, 0);
   if (ps.n_prod && !pair_wait(ps)) return;   // every wave of the workgroup, once (none: the decoder reduced)
+  // PARTS 16 (waves of ~2 rows, fewer than the chip's slots): the next row's chain and parameter loads are
+  // issued before this row's entry groups (register room: 3 waves per SIMD still hold every wave)
+  constexpr bool PF = PARTS == 16;
+  Row rn;
   for (int i = 0; i < nr; ++i) {
+    if constexpr (PF)
+      if (i + 1 < nr) start(rn, i + 1);
     F go[NCH], gi[NCH];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) go[j] = gi[j] = V::zero();
@@ -696,7 +702,11 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
       ro.colsum[r.m] = v;
       if (jo.cb_p) jo.colsum_bias<KIND>(r.m, v, r.bias);
     }
-    if (i + 1 < nr) start(r, i + 1);
+    if constexpr (PF) {
+      r = rn;
+    } else {
+      if (i + 1 < nr) start(r, i + 1);
+    }
   }
 }
 
