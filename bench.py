@@ -82,7 +82,11 @@ def parse():
     ap.add_argument("--rows-dual", type=int, default=-1,
                     help="small weights: both updates in one dual-row launch (1, library default) or two (0)")
     ap.add_argument("--rows-dual-parts", type=int, default=-1,
-                    help="dual-row launch: workgroups per 128-row tile (0: library's choice by size, 16, 32)")
+                    help="dual-row launch: workgroups per 128-row tile (0: library's choice by size, else 1..64)")
+    ap.add_argument("--rows-dual-pf", type=int, default=-2,
+                    help="dual-row launch: the next row's chain issued ahead (-1 library's choice, 0, 1)")
+    ap.add_argument("--rows-dual-large", type=int, default=-1,
+                    help="the dual-row launch on large weights too (1; with --reduce-in-decoder 1) or the pair launch (0)")
     ap.add_argument("--reduce-in-decoder", type=int, default=-1,
                     help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
                          "engine default (small weights)")
@@ -504,6 +508,10 @@ def main():
         _lib.call("ocf_set_tuning", b"rows_dual", int(args.rows_dual), None)
     if args.rows_dual_parts >= 0:
         _lib.call("ocf_set_tuning", b"rows_dual_parts", int(args.rows_dual_parts), None)
+    if args.rows_dual_pf >= -1:
+        _lib.call("ocf_set_tuning", b"rows_dual_pf", int(args.rows_dual_pf), None)
+    if args.rows_dual_large >= 0:
+        _lib.call("ocf_set_tuning", b"rows_dual_large", int(args.rows_dual_large), None)
     if args.rows_small_waves >= 0:
         _lib.call("ocf_set_tuning", b"rows_small_waves", int(args.rows_small_waves), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)

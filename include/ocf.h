@@ -663,6 +663,11 @@ int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);
  * previous (nullable) receives the old value. */
 int ocf_set_tuning(const char* key, int value, int* previous);
 
+/* ocf_check_async -- reports (status 1, ocf_last_error) and clears a pending asynchronous kernel error
+ * (OCF_ASYNC_*) without launching anything: hosts call it after their last step's results are read back
+ * (Engine.take_stats at every epoch end), so a fault in the last launches of a run cannot go unseen. */
+int ocf_check_async(void);
+
 int ocf_version(void);
 const char* ocf_last_error(void);
 

@@ -256,6 +256,7 @@ SIGNATURES = {
     "ocf_masked_mse": (I32, [P, P, P, I64, I32, I32, P, I64, P, P]),
     "ocf_backward": (I32, [P, P, I64, I32, F32, P, P, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
+    "ocf_check_async": (I32, []),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

@@ -53,6 +53,15 @@ void check_async_errors() {
   if (code) throw std::runtime_error(std::string("error from an earlier launch: ") + async_error_text(code));
 }
 
+}  // namespace ocf
+
+extern "C" int ocf_check_async(void) {
+  OCF_TRY_BEGIN
+  OCF_TRY_END
+}
+
+namespace ocf {
+
 // Split-K reductions: grid (N/64, M/4); 256 threads = 64 columns x 4 rows, one output element per
 // thread, slabs summed in a fixed order (4 independent partial sums for memory-level parallelism).
 __device__ __forceinline__ float sum_slabs(const float* s, int splits, int64_t sstride) {

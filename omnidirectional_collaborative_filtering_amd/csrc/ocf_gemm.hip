@@ -263,8 +263,14 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     g_rows_dual = value ? 1 : 0;
   } else if (k == "rows_dual_parts") {    // dual-row launch parts per tile: 0 by size, 16 or 32
     if (previous) *previous = g_rows_dual_parts;
-    OCF_CHECK(value == 0 || value == 16 || value == 32, "ocf_set_tuning: rows_dual_parts 0, 16 or 32");
+    OCF_CHECK(value >= 0 && value <= 64, "ocf_set_tuning: rows_dual_parts 0 (by size) or 1..64");
     g_rows_dual_parts = value;
+  } else if (k == "rows_dual_pf") {       // dual-row launch: next row issued ahead (-1 by parts, 0, 1)
+    if (previous) *previous = g_rows_dual_pf;
+    g_rows_dual_pf = value < 0 ? -1 : value ? 1 : 0;
+  } else if (k == "rows_dual_large") {    // the dual-row launch on large weights too (1) or the pair launch (0)
+    if (previous) *previous = g_rows_dual_large;
+    g_rows_dual_large = value ? 1 : 0;
   } else if (k == "rows_dual_count") {    // read (previous) and reset the dual-row launch count
     if (previous) *previous = g_rows_dual_count;
     g_rows_dual_count = 0;
@@ -278,6 +284,10 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     if (previous) *previous = g_pair_wait_polls;
     OCF_CHECK(value > 0, "ocf_set_tuning: pair_wait_polls > 0");
     g_pair_wait_polls = value;
+  } else if (k == "mlp_max_polls") {      // ocf_mlp_step's bounded barrier wait (tests: < 0 injects a give-up)
+    if (previous) *previous = g_mlp_max_polls;
+    OCF_CHECK(value != 0, "ocf_set_tuning: mlp_max_polls != 0");
+    g_mlp_max_polls = value;
   } else if (k == "optim_ws_max_k") {
     if (previous) *previous = g_optim_ws_max_k;
     g_optim_ws_max_k = value;

@@ -14,6 +14,7 @@ void set_error(const std::string& msg);
 // pinned, host-coherent word; every entry point reports a pending one (once) before doing anything.
 uint32_t* async_error_word();        // device-visible address of the word (allocated on first use)
 void check_async_errors();
+extern int g_mlp_max_polls;          // ocf_mlp_step's barrier wait (ocf_set_tuning "mlp_max_polls")
 }  // namespace ocf
 
 #define OCF_TRY_BEGIN try { ocf::check_async_errors();

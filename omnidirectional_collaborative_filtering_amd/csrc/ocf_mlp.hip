@@ -90,35 +90,59 @@ __device__ __forceinline__ float ldc(const float* base, int64_t e) {
 }
 
 // grid barrier number nb (1, 2, ...) of the launch: bar[0] counts arrivals monotonically within the launch
-// (barrier nb is passed when it reaches nb * grid); the last workgroup to leave the kernel resets it (exit()),
-// so it is zero for the next launch.  Bounded: a workgroup that gives up (not all workgroups resident)
-// records the error word and continues.
-__device__ __forceinline__ void grid_sync(const P& p, int& tn, int& nb) {
+// (barrier nb is passed when it reaches nb * grid); bar[1] counts the workgroups leaving the kernel and the
+// last one resets both words (grid_exit), so they are zero for the next launch.  Bounded and fail-safe: a
+// workgroup that gives up (not every workgroup resident) POISONS the barrier -- it sets bar[0]'s top bit with a
+// compare-and-swap on the count it last saw, so the poison lands only while the barrier is still incomplete --
+// and records OCF_ASYNC_MLP_BARRIER.  Every workgroup then finds the bit (its arrival's returned value or its
+// polls), and grid_sync returns false: the caller leaves the kernel without any further write.  Nobody passes
+// a poisoned barrier, so no weight, bias or slot is written after it; a residency failure shows at the first
+// barrier (once every workgroup has arrived there, all are resident), before the first parameter write, so
+// the step's parameters and slots stay untouched (tests/test_mlp_step_gpu.py::test_mlp_barrier_gives_up_safely).
+// max_polls < 0 is fault injection for that test: workgroup 0 never arrives at the first barrier and poisons it.
+constexpr uint32_t BAR_POISON = 0x80000000u;
+__device__ __forceinline__ bool grid_sync(const P& p, int& tn, int& nb) {
+  __shared__ int bar_ok;
   mark(p, tn);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's write-through stores have landed
   __syncthreads();
   ++nb;
   if (threadIdx.x == 0) {
     const uint32_t target = (uint32_t)nb * gridDim.x;
-    __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool inject = p.max_polls < 0 && blockIdx.x == 0 && nb == 1;
+    uint32_t v = inject ? __hip_atomic_load(&p.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : __hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     int it = 0;
-    while (__hip_atomic_load(&p.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++it > p.max_polls) {
-        __hip_atomic_store(p.err, (uint32_t)OCF_ASYNC_MLP_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+    bool ok;
+    for (;;) {
+      if (v & BAR_POISON) { ok = false; break; }
+      if (v >= target) { ok = true; break; }
+      if (inject || ++it > p.max_polls) {
+        // give up: poison unless the count moved since v was read (then v holds the new count: test it again)
+        if (__hip_atomic_compare_exchange_strong(&p.bar[0], &v, v | BAR_POISON, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(p.err, (uint32_t)OCF_ASYNC_MLP_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ok = false;
+          break;
+        }
+        continue;
       }
+      __builtin_amdgcn_s_sleep(1);
+      v = __hip_atomic_load(&p.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    bar_ok = ok ? 1 : 0;
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
   __syncthreads();
   mark(p, tn);
+  return bar_ok != 0;
 }
-__device__ __forceinline__ void grid_exit(const P& p, int nb) {
+__device__ __forceinline__ void grid_exit(const P& p) {
   if (threadIdx.x == 0) {
-    const uint32_t all = (uint32_t)(nb + 1) * gridDim.x;
-    if (__hip_atomic_fetch_add(&p.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 == all)
+    if (__hip_atomic_fetch_add(&p.bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == gridDim.x) {
       __hip_atomic_store(&p.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&p.bar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -446,7 +470,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K,
                                                   [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)m * K + k); }, Bw));
     }
-    grid_sync(p, tn, nb);
+    if (!grid_sync(p, tn, nb)) return grid_exit(p);
   }
   // ---- output layer + masked MSE: y = M (h W_L + b_L); e = y - T; delta_L = e M; per-tile statistics and
   // the column sums of delta_L (b_L's gradient).  W_L is stored transposed ([Np][K]): B(n, k) = W_L[n][k].
@@ -506,7 +530,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
       frag_colsum<CT>(lds, dl, m0, p.colp[L], p.Np);
     }
-    grid_sync(p, tn, nb);
+    if (!grid_sync(p, tn, nb)) return grid_exit(p);
   }
   // ---- backward, layer by layer from the output
   for (int i = L; i >= 0; --i) {
@@ -624,9 +648,9 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       }
     }
     if (!side_idle) side(gtid, gthreads, blockIdx.x == gridDim.x - 1);
-    if (i > 0) grid_sync(p, tn, nb);
+    if (i > 0 && !grid_sync(p, tn, nb)) return grid_exit(p);
   }
-  grid_exit(p, nb);
+  grid_exit(p);
   mark(p, tn);
 }
 
@@ -716,6 +740,10 @@ void launch(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
 
 using namespace ocf;
 
+namespace ocf {
+int g_mlp_max_polls = 1 << 22;   // ocf_mlp_step's bounded barrier wait (ocf_set_tuning "mlp_max_polls"; < 0: fault injection)
+}
+
 extern "C" int64_t ocf_mlp_step_workspace(const OcfMlpStepArgs* a) {
   try {
     OCF_CHECK(a != nullptr, "ocf_mlp_step_workspace: null arguments");
@@ -762,7 +790,7 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   p.stats = a->stats;
   p.bar = a->barrier;
   p.err = async_error_word();
-  p.max_polls = 1 << 22;
+  p.max_polls = g_mlp_max_polls;
   p.trace = a->trace;
   // every workgroup must be resident for the grid barriers; by default one per 32 x 32 tile of the busiest
   // phase, at most 128 (the barriers' arrivals grow with the grid) -- or one per CU (at most 256) when a phase
@@ -777,8 +805,12 @@ extern "C" int ocf_mlp_step(const OcfMlpStepArgs* a, void* stream) {
   int cus = 0, dev = 0;
   OCF_HIP(hipGetDevice(&dev));
   OCF_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  int wgs = a->wgs > 0 ? a->wgs : (tiles > 256 ? std::min(cus, 256) : std::min(tiles, 128));
-  OCF_CHECK(wgs <= cus, "ocf_mlp_step: wgs must not exceed the CU count (grid barriers)");
+  // (the default never exceeds the CU count: a partitioned device may have fewer CUs than tiles)
+  int wgs = tiles > 256 ? std::min(cus, 256) : std::min({tiles, 128, cus});
+  if (a->wgs > 0) {
+    OCF_CHECK(a->wgs <= cus, "ocf_mlp_step: wgs must not exceed the CU count (grid barriers)");
+    wgs = a->wgs;
+  }
   hipStream_t s = (hipStream_t)stream;
   switch (a->compute_dtype) {
     case OCF_F16: mlp::launch<_Float16>(*a, p, wgs, s); break;

@@ -6,7 +6,7 @@
 namespace ocf {
 // tuning switches (ocf_set_tuning)
 extern int g_optim_rows, g_rows_long, g_rows_small_waves, g_pair_wait_polls, g_rows_dual,
-    g_rows_dual_count, g_rows_dual_parts;
+    g_rows_dual_count, g_rows_dual_parts, g_rows_dual_large, g_rows_dual_pf;
 int cu_count();
 WsJobs ws_jobs(const OcfGemmArgs& g);
 // EPI_OPTIM through the row-stream kernel; false when the arguments need a tile kernel instead

@@ -13,7 +13,9 @@ int g_optim_rows = 1;   // row-list dW kernel when the caller passes row lists (
 int g_rows_long = -1;   // row-stream LONG variant: -1 by entries per row, 0 never, 1 always ("rows_long")
 int g_rows_small_waves = 8192;   // row-stream kernel: 32 parts per tile below this many waves at 12 ("rows_small_waves")
 int g_rows_dual = 1;   // ocf_gemm_pair on small weights: the dual-row launch ("rows_dual"; 0: two launches)
-int g_rows_dual_parts = 0;   // dual-row launch: workgroups per 128-row tile (0: by size; 16 or 32, "rows_dual_parts")
+int g_rows_dual_parts = 0;   // dual-row launch: workgroups per 128-row tile (0: by size, else 1..64, "rows_dual_parts")
+int g_rows_dual_pf = -1;   // dual-row launch: next row's chain issued ahead (-1: below 32 parts, 0 / 1: "rows_dual_pf")
+int g_rows_dual_large = 1;   // the dual-row launch on large weights too ("rows_dual_large"; 0: the pair launch there)
 int g_rows_dual_count = 0;   // dual-row launches since the last read ("rows_dual_count": tests see which form ran)
 int g_pair_wait_polls = 1 << 22;   // ocf_gemm_pair's bounded wait (ocf_set_tuning "pair_wait_polls"): seconds
 

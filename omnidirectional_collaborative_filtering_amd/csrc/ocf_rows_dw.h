@@ -420,6 +420,7 @@ struct RsPair {
   unsigned long long want;    // the count this launch's consumers wait for
   uint32_t* err;              // the library's asynchronous error word (host-coherent)
   int n_a, n_prod, max_polls;
+  int parts;                  // dual-row launch: workgroups per 128-row tile
 };
 
 // The wait: one plain load first (L2-cached: once a consumer of this XCD has seen the count complete, the
@@ -502,7 +503,7 @@ struct RdRow {
   WsJobs::BiasPre bias;
 };
 
-template <typename CT, int KIND, int CW, int NCH, int PARTS>
+template <typename CT, int KIND, int CW, int NCH, bool PF>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro, WsJobs jo, RowsDwArgs ri, WsJobs ji,
                                                                    RsPair ps) {
   using V = RsVec<CW>;
@@ -529,7 +530,10 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
     if (j < ji.count()) ji.run<KIND>(j, lane);
     return;
   }
+  // (workgroups go to the 8 XCDs round robin, so consecutive parts of a tile run on different XCDs; giving
+  // each XCD a contiguous range of tiles instead measured slower: 305-313 vs 291-298 us at ML-20M)
   const int wb = bx - nprod - ncons;
+  const int PARTS = ps.parts;
   const int t = wb / PARTS, part = wb % PARTS;
   if (t >= ro.M / 128) return;          // (uniform per workgroup: no wait reached)
   const int m0 = t * 128;
@@ -577,7 +581,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   };
   auto start = [&](Row& r, int i) {
     r.m = __builtin_amdgcn_readfirstlane(row_of(kb + wave + 4 * i));
-    if constexpr (RD_LATE_IN < 2 || RD_LATE_IN == 3 && false)
+    if constexpr (RD_LATE_IN < 2)
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const uint32_t o = off(r.m, j);
@@ -630,9 +634,8 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   Row r;
   if (nr > 0) start(r, 0);
   if (ps.n_prod && !pair_wait(ps)) return;   // every wave of the workgroup, once (none: the decoder reduced)
-  // PARTS 16 (waves of ~2 rows, fewer than the chip's slots): the next row's chain and parameter loads are
-  // issued before this row's entry groups (register room: 3 waves per SIMD still hold every wave)
-  constexpr bool PF = PARTS == 16;
+  // PF (parts < 32: waves of two or more rows): the next row's chain and parameter loads are issued before
+  // this row's entry groups (ML-1M at 16 parts: register room, 3 waves per SIMD still hold every wave)
   Row rn;
   for (int i = 0; i < nr; ++i) {
     if constexpr (PF)

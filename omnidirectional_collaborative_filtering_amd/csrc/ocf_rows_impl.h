@@ -2,6 +2,8 @@
 // per compute dtype in ocf_rows_f16.hip / ocf_rows_bf16.hip / ocf_rows_f32.hip (the kernel instances take
 // minutes to compile: one translation unit per dtype builds them in parallel).
 #pragma once
+#include <cmath>
+
 #include "ocf_internal.h"
 #include "ocf_rows.h"
 #include "ocf_rows_dw.h"
@@ -72,16 +74,16 @@ struct RowsDual {
   RsPair ps;
   int grid;
   hipStream_t s;
-  int parts;
+  // one instance per (optimizer, width, prefetch) whatever the single kernel's PARTS / LONG: the parts are a
+  // launch argument (ps.parts)
   template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG> void go() {
-    if constexpr (PARTS == 32) {    // small weights only (two instances per optimizer and width)
-      if (parts == 16)
-        hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, 16>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
-                           A.jb, B.ra, B.jb, ps);
-      else
-        hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, 32>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
-                           A.jb, B.ra, B.jb, ps);
-    }
+    // (the prefetch pays at ~2 rows per wave: ML-1M's 16 parts; at one row per wave it only costs registers)
+    if (g_rows_dual_pf > 0 || (g_rows_dual_pf < 0 && ps.parts <= 16))
+      hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, true>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
+                         A.jb, B.ra, B.jb, ps);
+    else
+      hipLaunchKernelGGL((optim_rowdual_kernel<CT, KIND, CW, NCH, false>), dim3(grid), dim3(RS_THREADS), 0, s, A.ra,
+                         A.jb, B.ra, B.jb, ps);
   }
 };
 
@@ -113,9 +115,9 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
   // consumers' polling) cost more than the boundary it replaces (ML-1M 36.9 vs 36.8 us, ML-100K 25.8 vs 21.7;
   // ML-20M 303 vs 307: tools/step_parts_probe.py) -- there the dual-row launch walks each row's chain once for
   // both layers instead (g_rows_dual, "rows_dual"), or two launches
-  const bool dual = A.small && g_rows_dual && rows_dual_ok(a, b, A, B);
+  const bool dual = (A.small || g_rows_dual_large) && g_rows_dual && rows_dual_ok(a, b, A, B);
   if (A.small && !dual) return false;
-  RsPair ps;
+  RsPair ps{};
   ps.word = reinterpret_cast<unsigned long long*>(sync.word);
   ps.n_a = A.grid;
   ps.n_prod = A.jb.jr_on ? (A.jb.jr.Bp + 3) / 4 : 0;   // the job-only workgroups holding the row reduction
@@ -127,12 +129,23 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
     const int nprod = (A.jb.count() + 3) / 4;
     ps.n_prod = A.jb.jr_on ? nprod : 0;
     ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
-    // parts per 128-row tile: 32 (about one row per wave) while the waves fit the chip's slots at the dual
-    // kernel's ~110-125 VGPRs (4 waves per SIMD: 4,096), else 16 (ML-1M's 48 tiles: 3,072 waves of ~2 rows
-    // instead of 6,144 in 1.5 rounds); g_rows_dual_parts forces one ("rows_dual_parts")
-    const int parts = g_rows_dual_parts ? g_rows_dual_parts : (A.ra.M / 128 * 32 * 4 > 4096 ? 16 : 32);
+    // parts per 128-row tile.  Small weights: 32 (about one row per wave) while the waves fit the chip's slots
+    // at the dual kernel's ~110-125 VGPRs (4 waves per SIMD: 4,096), else 16 (ML-1M's 48 tiles: 3,072 waves of
+    // ~2 rows instead of 6,144 in 1.5 rounds).  Large weights: about one live row per wave too -- the expected
+    // live rows per tile (128 (1 - exp(-entries / rows)) with live records, else 128) / 4 -- but never a multiple
+    // of 4: measured at ML-20M (pair launch, HIP events, same box, profiles/r05_dual_large/): parts 8 / 12 / 16 /
+    // 20 / 24 311 / 298 / 312 / 298 / 296 us, 13-15 294, 17-19 288-291, 21-23 278-282, 25-27 281-283, 30 / 34
+    // 287 / 289 (and the pair launch 311.6).  g_rows_dual_parts forces a count ("rows_dual_parts").
+    int parts = A.small ? (A.ra.M / 128 * 32 * 4 > 4096 ? 16 : 32) : 0;
+    if (!A.small) {
+      const double live = A.ra.live ? 1.0 - std::exp(-(double)a.sp_nent / (double)A.ra.M) : 1.0;
+      parts = std::min(63, std::max(5, (int)(128.0 * live / 4.0)));
+      if (parts % 4 == 0) --parts;
+    }
+    if (g_rows_dual_parts) parts = g_rows_dual_parts;
+    ps.parts = parts;
     const int grid = nprod + (B.jb.count() + 3) / 4 + A.ra.M / 128 * parts;
-    rows_dispatch<CT>(A, RowsDual{A, B, ps, grid, s, parts});
+    rows_dispatch<CT>(A, RowsDual{A, B, ps, grid, s});
     ++g_rows_dual_count;
   } else {
     rows_dispatch<CT>(A, RowsPair{A, B, ps, s});

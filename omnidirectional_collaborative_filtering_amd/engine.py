@@ -964,8 +964,13 @@ class Engine:
         fold = (with_grad and self.comm is None and self._fused_step and self.fold_reduce and self._folds()
                 and self.trainable[0])
         in_dec = self.reduce_in_decoder
-        if in_dec is None:            # small weights: the dual-row dW launch (ocf_gemm_pair, ocf_rows_impl.h)
-            in_dec = self.Np // TILE * 48 < 8192
+        if in_dec is None:
+            # one input block: ocf_gemm_pair's dual-row launch (ocf_rows_impl.h; both layers' rows share the row
+            # lists), which needs the reduction done; large weights with k >= 2 inputs: the pair launch, whose
+            # consumers then wait for nothing (ML-20M pair launch 311.6 -> 303.8 us, dual-row 299.8 us:
+            # profiles/r05_dual_large/); small weights with k >= 2: two launches with the reduction riding in
+            # the first (the measured round-4 form)
+            in_dec = self.k == 1 or self.Np // TILE * 48 >= 8192
         if fold and in_dec and tab["n_chunks"] > 0:
             g.jr, g.row_arrive = ctypes.addressof(r), ptr(self.row_arrive)
             self._last_jr = r             # (kept alive: the recorded step's decoder arguments point at it)
@@ -1775,6 +1780,9 @@ class Engine:
             self.comm(sh)
             pen = torch.stack([sh, pen[:, 1]], 1)
         out = st.cpu().numpy().astype(np.float64)
+        # a kernel fault recorded without stopping (a pair-launch wait or a fused-step barrier that gave up) in
+        # the steps just read back surfaces here, at every epoch end, not only at the next library call
+        _lib.call("ocf_check_async")
         # column 3 (0 from the loss epilogues) carries the step's l2 penalty
         out[:, 3] = pen.double().sum(1).cpu().numpy()
         self.pen_hist[: self.n_stats].zero_()

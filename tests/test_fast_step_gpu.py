@@ -54,7 +54,7 @@ def test_fast_step_bit_identical(gpu, cd, opt, sparsity):
         assert np.array_equal(a, b), float(np.abs(a - b).max())
 
 
-def _run_pair(pair, cd, opt, shape):
+def _run_pair(pair, cd, opt, shape, jobs=False):
     import torch
     from omnidirectional_collaborative_filtering_amd import _lib
     from omnidirectional_collaborative_filtering_amd import optimizers as O
@@ -72,19 +72,26 @@ def _run_pair(pair, cd, opt, shape):
     m.compile(mk(), "mean_squared_error", metrics=["mae"])
     eng = om.engine
     eng.pair_dw = pair
+    if jobs:      # the row reduction as the output layer's jobs (producers), the pair form on large weights
+        eng.reduce_in_decoder = False
+        _lib.call("ocf_set_tuning", b"rows_dual_large", 0, None)
     gen = rd.data_gen(B, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     _lib.call("ocf_set_tuning", b"rows_dual_count", 0, None)
     n = min(6, gen.num_batches - 1)
-    h = m.fit_generator(gen, n, epochs=1, verbose=0).history
-    torch.cuda.synchronize()
+    try:
+        h = m.fit_generator(gen, n, epochs=1, verbose=0).history
+        torch.cuda.synchronize()
+    finally:
+        _lib.call("ocf_set_tuning", b"rows_dual_large", 1, None)
     dual = ctypes.c_int(-1)
     _lib.call("ocf_set_tuning", b"rows_dual_count", 0, ctypes.byref(dual))
-    # one launch per step: on weights of more than 170 row tiles the pair form, which advances the producers'
-    # count (never cleared; the host keeps its running twin; every launch on the same word); on smaller ones
-    # the dual-row form (the decoder did the row reduction: nothing to count)
+    # one launch per step.  Default (the decoder did the row reduction): the dual-row form on every weight size,
+    # nothing to count.  With the reduction as producer jobs: the pair form on weights of more than 170 row
+    # tiles, the dual-row form with producers on smaller ones; both advance the producers' count (never cleared;
+    # the host keeps its running twin; every launch on the same word)
     large = eng.Np // 128 > 170
-    assert (eng.pair_state.count > 0) == (pair and large)
-    assert dual.value == (n if pair and not large else 0)
+    assert (eng.pair_state.count > 0) == (pair and jobs)
+    assert dual.value == (n if pair and not (jobs and large) else 0)
     assert eng.pair_sync[0].item() == eng.pair_state.count and eng.pair_state.count % ((eng.Bp + 3) // 4) == 0
     st = [t.cpu().numpy().copy() for sw, sb in eng.slots for t in sw + sb if t is not None]
     sh = [t.float().cpu().numpy() for t in eng.Wsh if t is not None]
@@ -98,11 +105,13 @@ def _run_pair(pair, cd, opt, shape):
     ("float32", "rmsprop", (1200, 30000, 150000, 128)),
     ("float16", "adam", (2000, 40000, 120000, 256)),
     ("bfloat16", "adagrad", (1500, 3000, 120000, 256))])  # small dense weight: two launches (no records)
-def test_pair_launch_bit_identical(gpu, cd, opt, shape):
-    """ocf_gemm_pair (dW_out + dW_in in one launch, dW_in's workgroups waiting in the kernel for the row
-    reduction) against the two ocf_gemm launches: identical history, weights, slots and shadows"""
-    a = _run_pair(True, cd, opt, shape)
-    b = _run_pair(False, cd, opt, shape)
+@pytest.mark.parametrize("jobs", [False, True])
+def test_pair_launch_bit_identical(gpu, cd, opt, shape, jobs):
+    """ocf_gemm_pair in one launch (the dual-row form; with the row reduction as the output layer's jobs the
+    pair form on large weights, dW_in's workgroups waiting in the kernel for it) against the two ocf_gemm
+    launches: identical history, weights, slots and shadows"""
+    a = _run_pair(True, cd, opt, shape, jobs)
+    b = _run_pair(False, cd, opt, shape, jobs)
     assert a[0] == b[0] and a[4] == b[4]
     for x, y in zip(a[1] + a[2] + a[3], b[1] + b[2] + b[3]):
         assert np.array_equal(x, y), float(np.abs(x - y).max())

@@ -128,3 +128,46 @@ def test_fused_step_grid_sizes_match_layerwise(gpu, wgs):
         assert abs(a[0]["val_loss"][e] - b[0]["val_loss"][e]) <= 1e-5 * b[0]["val_loss"][e], e
     for x, y in zip(a[2], b[2]):
         assert np.abs(x - y).max() <= 5e-5, float(np.abs(x - y).max())
+
+
+@pytest.mark.gpu
+def test_mlp_barrier_gives_up_safely(gpu):
+    """A grid barrier that gives up (injected: workgroup 0 never arrives at the first barrier, ocf_set_tuning
+    "mlp_max_polls" < 0) poisons the barrier: every workgroup leaves without writing, so the step's weights,
+    biases, slots and shadows are untouched; the next library call reports OCF_ASYNC_MLP_BARRIER once, the
+    barrier words are zero again, and the next step runs normally on them"""
+    import ctypes
+    import torch
+    from omnidirectional_collaborative_filtering_amd import _lib
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    x, om_, t = _data(300, 100, 2)
+    m = omni_model(2, 128, 100, 128, dense_activation="tanh", use_causal_info=True, compute_dtype="bfloat16", seed=5)
+    eng = m.engine
+    model = m.model
+    model.compile(_opt("rmsprop")[0](), "mean_squared_error")
+    model.fit(x[:2] + [om_], t, batch_size=128, epochs=1, shuffle=False)
+    assert eng._mlp_args is not None, "the fused small-model step (ocf_mlp_step) did not run"
+    torch.cuda.synchronize()
+
+    def state():
+        return [a.clone() for a in eng.W + eng.b + [s for sw, sb in eng.slots for s in sw + sb if s is not None]
+                + [w for w in eng.Wsh if w is not None]]
+    s0 = state()
+    lib = _lib.load()
+    prev = ctypes.c_int32()
+    _lib.call("ocf_set_tuning", b"mlp_max_polls", -1, ctypes.byref(prev))
+    try:
+        eng._mlp_step()
+        torch.cuda.synchronize()
+        # (before any other library call: every entry point reports a pending error)
+        assert lib.ocf_check_async() != 0 and b"ocf_mlp_step" in lib.ocf_last_error()
+        assert lib.ocf_check_async() == 0          # reported once
+    finally:
+        lib.ocf_set_tuning(b"mlp_max_polls", prev.value, None)
+    for a, b in zip(s0, state()):
+        assert torch.equal(a, b)
+    assert int(eng._mlp_bar.abs().sum()) == 0
+    eng._mlp_step()                                # the same barrier words work again
+    torch.cuda.synchronize()
+    _lib.call("ocf_check_async")                   # (raises if that step's barriers gave up)
+    assert not torch.equal(s0[0], eng.W[0]) and int(eng._mlp_bar.abs().sum()) == 0

@@ -520,3 +520,46 @@ def test_rows_dual_bit_identical(gpu, cd, shape, skip, opt):
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd,opt,skip", [("float16", "adagrad", True), ("bfloat16", "adam", False),
+                                         ("float32", "rmsprop", False)])
+def test_rows_dual_large_bit_identical(gpu, cd, opt, skip):
+    """The dual-row form on LARGE weights (235 row tiles: above the small-weight gate; ocf_set_tuning
+    "rows_dual_large", the row reduction in the decoder) against the pair launch and against two launches:
+    identical losses, weights, slots and shadows, and the dual launch really ran once per step"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    mk = {"adagrad": lambda: O.Adagrad(lr=0.01, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=0.001),
+          "adam": lambda: O.Adam(lr=0.001)}[opt]
+    out = []
+    try:
+        for large, in_dec in ((0, False), (0, True), (1, True)):
+            _lib.call("ocf_set_tuning", b"rows_dual_large", large, None)
+            _lib.call("ocf_set_tuning", b"rows_dual_count", 0, None)
+            rd, gen = _gen_for(2000, 30000, 300000, 256, 0.5, seed=21)
+            om = om_ = omni_model(1, 500 if cd != "float32" else 200, 30000, 256, dense_activation="sigmoid",
+                                  use_causal_info=False, dropout_probability=0.2, compute_dtype=cd, seed=4)
+            eng = om.engine
+            eng.row_skip = skip
+            eng.reduce_in_decoder = in_dec
+            m = om.model
+            m.compile(mk(), "mean_squared_error", metrics=["mae"])
+            n = min(4, gen.num_batches)
+            h = m.fit_generator(gen, n, epochs=1, verbose=0).history
+            torch.cuda.synchronize()
+            cnt = ctypes.c_int(-1)
+            _lib.call("ocf_set_tuning", b"rows_dual_count", 0, ctypes.byref(cnt))
+            assert cnt.value == (n if large else 0), (large, cnt.value)
+            assert eng._dec_reduced == in_dec
+            out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                        [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                        [t.clone() for t in eng.Wsh if t is not None]))
+            del om_
+    finally:
+        _lib.call("ocf_set_tuning", b"rows_dual_large", 1, None)
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        for a, b in zip(out[0][1], o[1]):
+            assert torch.equal(a, b)
