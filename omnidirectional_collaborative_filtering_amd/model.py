@@ -275,7 +275,9 @@ class Model(object):
         epoch, ceil(n / batch_size) batches -- the last one partial --, epoch logs weighted by batch size
         (BaseLogger) and the validation logs by sample over every held-out row (_test_loop).  With a Dropout
         layer the reference fixes noise_shape = [batch_size, H] (model.py:73), so a partial batch cannot run
-        there: with dropout only full batches are taken."""
+        there: with dropout only full TRAINING batches are taken.  Evaluation runs the layer through
+        in_train_phase (its noise never applies at test time), so the validation logs always cover every
+        held-out row, the trailing partial batch included."""
         e = self.engine
         bs = int(batch_size or e.B)
         if bs != e.B:
@@ -299,9 +301,9 @@ class Model(object):
         hist = History()
         callbacks = callbacks or []
 
-        def batches(m):
+        def batches(m, allow_partial):
             full, rest = divmod(m, bs)
-            return [(s * bs, bs) for s in range(full)] + ([(full * bs, rest)] if rest and partial else [])
+            return [(s * bs, bs) for s in range(full)] + ([(full * bs, rest)] if rest and allow_partial else [])
 
         def rows_of(ix, b):
             if b == bs:
@@ -313,12 +315,12 @@ class Model(object):
             if shuffle:
                 np.random.shuffle(idx)
             idx_d = torch.as_tensor(idx, dtype=torch.int64).to(dev)
-            tb = batches(split_at)
+            tb = batches(split_at, partial)
             for s0, b in tb:
                 self._load_rows(xd, yd, rows_of(idx_d[s0:s0 + b], b), b)
                 e.train_step()
             logs = self._logs_from_stats(e.take_stats(), [b for _, b in tb])
-            vb = batches(n - split_at)
+            vb = batches(n - split_at, True)
             if vb:
                 for s0, b in vb:
                     self._load_rows(xd, yd, rows_of(val_rows[s0:s0 + b], b), b)

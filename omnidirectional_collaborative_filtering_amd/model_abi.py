@@ -108,6 +108,7 @@ class ModelABI:
 
     # the five calls
     def forward(self, inputs, out_mask, B, training, masks_out=None):
+        """ocf_forward into the reused buffer self.pred (overwritten by the next call: clone to keep it)"""
         s = torch.cuda.current_stream().cuda_stream
         self.pred = self._out("pred", B, self.N)
         ins = (ctypes.c_void_p * self.k)(*[ptr(x) for x in inputs])
@@ -119,6 +120,7 @@ class ModelABI:
         return self.pred
 
     def masked_mse(self, pred, targets, out_mask, B):
+        """ocf_masked_mse into the reused buffers self.grad / self.stats (overwritten by the next call)"""
         s = torch.cuda.current_stream().cuda_stream
         # ocf_masked_mse takes one row stride for pred / targets / mask: [B][N] contiguous (data_gen's arrays are
         # views with a padded stride)
@@ -145,11 +147,14 @@ class ModelABI:
         self.opt.iterations += 1
 
     def train_on_batch(self, inputs, out_mask, targets, masks_out=None):
-        """train.py:157's per-batch step; returns the device stats (ocf_masked_mse layout)"""
+        """train.py:157's per-batch step; returns this step's device stats (ocf_masked_mse layout) as a fresh
+        tensor (4 + 3 B floats), so a caller may keep per-step stats on the device and read them later.
+        forward / masked_mse return the model's reused output buffers instead (pred, grad, stats: the next
+        call overwrites them)."""
         B = targets.shape[0]
         pred = self.forward(inputs, out_mask, B, True, masks_out)
         grad, stats = self.masked_mse(pred, targets, out_mask, B)
         self.backward(grad, B)
         self.opt_step()
         self.step += 1
-        return stats
+        return stats.clone()

@@ -65,6 +65,39 @@ def test_ml20m_bench_step(gpu):
     assert_low_precision(res, 2e-3)
 
 
+def _h512_hook(om):
+    e = om.engine
+    assert e.use_sparse and e.sparse_ok and e.Hp[0] == 512, "row gathers at H = Hp = 512 expected"
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cd", ["float32", "bfloat16"])
+def test_train_py_default_config(gpu, cd):
+    """the reference's own `python train.py` run (train.py:19-59): ML-1M I-AutoRec with num_hidden_units = 512
+    and batch_size = 128 (train.py:24,30,44), sigmoid, dropout 0.2, Adagrad lr 0.005 (train.py:40,50-52).  H =
+    512 is the row kernels' limit (no hidden padding: Hp = H, the gathers' LDS rows at their largest).  Exact
+    fp32 at 1e-5, bf16 inside the envelope"""
+    res = run_parity(cd, "adagrad", 1, "sigmoid", steps=4, B=128, H=512, dropout=0.2, lr=0.005, data=_synth("ml1m"),
+                     envelope=cd != "float32", sparse_oracle=True, eval_batches=4, model_hook=_h512_hook)
+    assert res.om.engine.sparse_dw
+    if cd == "float32":
+        assert_fp32(res)
+    else:
+        assert_low_precision(res, 1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_ml20m_h512_step(gpu):
+    """the ML-20M shape at train.py's H = 512 and B = 128 (f16, the default dual-row dW launch on large weights at
+    Hp = H = 512) against the oracle"""
+    res = run_parity("float16", "adagrad", 1, "sigmoid", steps=4, B=128, H=512, dropout=0.2, lr=0.005,
+                     data=_synth("ml20m"), envelope=True, sparse_oracle=True, eval_batches=4, model_hook=_h512_hook)
+    assert res.om.engine.sparse_dw and res.live_rows_used
+    assert_low_precision(res, 2e-3)
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_netflix_width_one_gpu(gpu):
