@@ -61,6 +61,9 @@ def parse():
                     help="N=1: also time one whole training epoch through fit_generator (train.py:157: floor(n/B)-1 "
                          "steps, the epoch plan and the reference RNG's draws included; reported as full_epoch)")
     ap.add_argument("--rmse", type=int, default=1)
+    ap.add_argument("--configs", type=int, default=1,
+                    help="N=1, default workload: also run the other BASELINE configs as short child benches "
+                         "(ml100k, ml1m, ml1m_u, jester, netflix) and report them in the line's 'configs' object")
     ap.add_argument("--emulate-shards", type=int, default=0,
                     help="diagnostic: run rank 0 of a G-way feature-parallel job alone (collectives skipped, "
                          "numerics of a partial model); not a bench line")
@@ -105,8 +108,6 @@ def parse():
     ap.add_argument("--fused-mlp", type=int, default=1,
                     help="small models (Jester, ML-100K, ML-1M): the whole step in one launch (ocf_mlp_step; 0: the "
                          "layer-wise dense path / the row gathers)")
-    ap.add_argument("--fused-gen", type=int, default=0,
-                    help="generator batches of small models through ocf_mlp_step too (Engine.fused_gen; opt-in)")
     ap.add_argument("--row-skip", type=int, default=1,
                     help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
                          "gradient, identity update; bit-identical)")
@@ -439,6 +440,47 @@ def jester_main(args):
     print(json.dumps(line), flush=True)
 
 
+# the other BASELINE configs, run as child processes after the headline (bench args, timeout s)
+SIDE_CONFIGS = [
+    ("ml100k", ["--config", "ml100k", "--dtype", "float32"], 240),
+    ("ml1m", ["--config", "ml1m", "--dtype", "bfloat16"], 240),
+    ("ml1m_u", ["--config", "ml1m_u", "--dtype", "bfloat16"], 240),
+    ("jester", ["--config", "jester", "--dtype", "bfloat16"], 240),
+    ("train_py_ml1m_h512_b128", ["--config", "ml1m", "--dtype", "float32", "--hidden", "512", "--batch", "128"], 240),
+    ("netflix", ["--config", "netflix", "--steps", "10"], 420),
+]
+
+
+def side_configs():
+    """short in-run lines of the other BASELINE configs (each a child bench.py: own process, own GPU memory;
+    CPU baseline, test RMSE, fp32 mode and full epoch off), reduced to ms/step, ratings/s and the roofline
+    fractions.  A config that fails is reported with its error, never retried."""
+    import subprocess
+    out = {}
+    for name, extra, tmo in SIDE_CONFIGS:
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline", "0", "--rmse", "0", "--fp32-steps", "0",
+               "--epoch", "0", "--configs", "0", "--warmup", "5"] + (["--steps", "20"] if "--steps" not in extra else []) \
+            + extra
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=tmo)
+            lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out[name] = {"error": "rc %d: %s" % (r.returncode, (r.stderr or r.stdout)[-300:])}
+                continue
+            d = json.loads(lines[-1])
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": "timeout after %d s" % tmo}
+            continue
+        roof, sr = d.get("roofline") or {}, d.get("step_roofline") or {}
+        out[name] = {"workload": d["config"]["workload"], "dtype": d["dtype"], "hidden": d["config"].get("hidden"),
+                     "batch": d["config"].get("batch_per_gpu"), "ms_per_step": d["ms_per_step"],
+                     "ratings_per_s": d["value"], "steps": d["steps"], "kernel": roof.get("kernel"),
+                     "kernel_mean_us": roof.get("kernel_mean_us"), "frac": roof.get("frac"),
+                     "step_roofline_frac": sr.get("frac_of_binding_roof"), "wall_s": round(time.time() - t0, 1)}
+    return out
+
+
 def main():
     args = parse()
     if args.config == "jester":
@@ -495,7 +537,6 @@ def main():
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
     eng.epoch_row_lists = bool(args.epoch_lists)
     eng.fused_mlp = bool(args.fused_mlp)
-    eng.fused_gen = bool(args.fused_gen)
     if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
         eng.shadow_blocked = bool(args.shadow_blocked)
         eng._refresh_shadows()
@@ -729,6 +770,10 @@ def main():
             line["cpu_baseline"] = cpu_baseline(data, rows_b, N, H, w0, lr, args.cpu_steps, args.config)
         except Exception as e:  # the baseline is reported, never the measured value
             line["cpu_baseline"] = {"error": repr(e)}
+    if world == 1 and args.configs and args.config == "ml20m" and not args.emulate_shards:
+        del om, m, eng, gen, rd
+        torch.cuda.empty_cache()
+        line["configs"] = side_configs()
     print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

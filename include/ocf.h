@@ -617,8 +617,7 @@ int ocf_backward(OcfCtx* ctx, const float* grad, int64_t ld_grad, int B, float g
  * whose weights fit in L2 (0.14 M parameters) the step is latency-bound: one launch instead of ~14.
  * The batch is gathered from device-resident arrays by row index (Model.fit's data path): input block j of
  * batch row b is x[j] + rows[b] * ld_x (N values), its output mask / targets out_mask / targets + rows[b] *
- * ld_t.  Rows b >= B are padding (zero).  rows == NULL: dense batch arrays (ocf_scatter_batch's X / Mout / T
- * outputs): x[j], out_mask, targets are [Bp][ld] with zero padding, ld >= Np, ld_x % 4 == 0.  Weights in the engine's padded layout: W[0] [k_blocks * Np][hidden_p[0]]
+ * ld_t.  Rows b >= B are padding (zero).  Weights in the engine's padded layout: W[0] [k_blocks * Np][hidden_p[0]]
  * (block j's column n at row j * Np + n), W[i] [hidden_p[i-1]][hidden_p[i]], W[L] transposed [Np][hidden_p[L-1]];
  * b[i] the padded output width; optimizer slots alike (nullable per the optimizer); shadow[i] (nullable) the
  * compute-dtype copy of W[i] rewritten by the update (64 x 64-blocked with shadow_blocked).  l2 = 0.

@@ -294,27 +294,20 @@ __device__ __forceinline__ void frag_colsum(char* lds, const Frag<4>& f, int m0,
 __device__ __forceinline__ float4 ld4(const float* q) { return *reinterpret_cast<const float4*>(q); }
 
 // ---- operand views
-// layer-0 input of batch row b, padded columns c .. c+3 (one block: Np % 4 == 0).  XD (dense batch arrays,
-// rows == NULL): [Bp][ld_x] with zero padding, one vector load; else row rows[b] of the caller's [n][ld_x] arrays,
-// zero past the batch and in the block padding (element loads through selected addresses: no branches)
-template <bool XD>
+// layer-0 input of batch row b, padded columns c .. c+3 (one block: Np % 4 == 0): row rows[b] of the caller's
+// [n][ld_x] arrays, zero past the batch and in the block padding (element loads through selected addresses: no
+// branches)
 __device__ __forceinline__ float4 x4(const P& p, int b, int c) {
   const int blk = c / p.Np, n = c - blk * p.Np;
-  if constexpr (XD) {
-    return ld4(p.x[blk] + (int64_t)b * p.ld_x + n);
-  } else {
-    const float* row = p.x[blk] + p.rows[b < p.B ? b : p.B - 1] * p.ld_x;
-    float e[4];
+  const float* row = p.x[blk] + p.rows[b < p.B ? b : p.B - 1] * p.ld_x;
+  float e[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) e[q] = *((b < p.B && n + q < p.N) ? row + n + q : g_zero);
-    return make_float4(e[0], e[1], e[2], e[3]);
-  }
+  for (int q = 0; q < 4; ++q) e[q] = *((b < p.B && n + q < p.N) ? row + n + q : g_zero);
+  return make_float4(e[0], e[1], e[2], e[3]);
 }
 // element offset of batch row m, column n of the output mask / targets
-template <bool XD>
 __device__ __forceinline__ int64_t t_off(const P& p, int m, int n) {
-  if constexpr (XD) return (int64_t)m * p.ld_t + n;
-  else return p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
+  return p.rows[m < p.B ? m : p.B - 1] * p.ld_t + (n < p.N ? n : 0);
 }
 __device__ __forceinline__ int64_t shadow_index(const P& p, int i, int r, int c) {
   const int C = i == p.L ? p.dim[i] : p.dim[i + 1];
@@ -447,7 +440,7 @@ __device__ __forceinline__ void epi_delta(const P& p, int i, const Frag<NE>& f, 
   }
 }
 
-template <typename CT, int KIND, bool XD>
+template <typename CT, int KIND>
 __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
   __shared__ __attribute__((aligned(16))) char lds[Geo<CT>::BYTES];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -465,7 +458,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
     for (int t = blockIdx.x; t < Bt * nt; t += gridDim.x) {
       const int m0 = (t / nt) * TT, n0 = (t % nt) * TT;
       if (i == 0)      // (one accessor per call: a select inside it would split the chunk's loads)
-        epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4<XD>(p, m, k); }, Bw));
+        epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K, [&](int m, int k) { return x4(p, m, k); }, Bw));
       else
         epi_forward(p, i, tile_s<CT, false, true>(lds, m0, n0, K,
                                                   [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)m * K + k); }, Bw));
@@ -484,7 +477,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
       float mkv[4], ttv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {        // the mask / target loads fly during the GEMM
-        const int64_t o = t_off<XD>(p, m0 + (threadIdx.x >> 5) + 8 * j, n);
+        const int64_t o = t_off(p, m0 + (threadIdx.x >> 5) + 8 * j, n);
         mkv[j] = p.om[o];
         ttv[j] = p.tg[o];
       }
@@ -635,7 +628,7 @@ __global__ void __launch_bounds__(THREADS) mlp_step_kernel(P p) {
         v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return ldc4(p.h[i - 1], (int64_t)k * Ki + m); },
                                    [&](int nn, int k) { return ldc4(p.d[i], (int64_t)k * Wi + nn); });
       else               // dW_0[k][j] = sum_b x[b][k] delta_0[b][j]
-        v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4<XD>(p, k, m); },
+        v = tile_s<CT, true, true>(lds, m0, n0, p.Bp, [&](int m, int k) { return x4(p, k, m); },
                                    [&](int nn, int k) { return ldc4(p.d[0], (int64_t)k * Wi + nn); });
       float gv[4];
 #pragma unroll
@@ -702,10 +695,7 @@ void check(const OcfMlpStepArgs& a) {
     OCF_CHECK(a.hidden_p[i] % 64 == 0 && a.hidden[i] >= 1 && a.hidden[i] <= a.hidden_p[i],
               "ocf_mlp_step: hidden widths padded to multiples of 64");
   for (int j = 0; j < a.k_blocks; ++j) OCF_CHECK(a.x[j] != nullptr, "ocf_mlp_step: null input block");
-  OCF_CHECK(a.out_mask && a.targets && a.ld_x >= a.N && a.ld_t >= a.N, "ocf_mlp_step: batch arrays");
-  if (!a.rows)
-    OCF_CHECK(a.ld_x >= a.Np && a.ld_x % 4 == 0 && a.ld_t >= a.Np,
-              "ocf_mlp_step: dense batch arrays (rows == NULL) need ld_x, ld_t >= Np, ld_x % 4 == 0");
+  OCF_CHECK(a.rows && a.out_mask && a.targets && a.ld_x >= a.N && a.ld_t >= a.N, "ocf_mlp_step: batch arrays");
   OCF_CHECK(a.keep > 0.f && a.keep <= 1.f, "ocf_mlp_step: keep in (0, 1]");
   if (a.keep < 1.f)
     for (int i = 0; i < a.n_hidden; ++i) OCF_CHECK(a.mask[i] != nullptr, "ocf_mlp_step: dropout masks");
@@ -719,20 +709,15 @@ void check(const OcfMlpStepArgs& a) {
   OCF_CHECK(a.stats && a.work && a.barrier, "ocf_mlp_step: stats / work / barrier");
 }
 
-template <typename CT, bool XD>
-void launch_x(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
-  switch (a.opt.kind) {
-    case OCF_OPT_ADAGRAD: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAGRAD, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    case OCF_OPT_RMSPROP: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_RMSPROP, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    case OCF_OPT_ADAM: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAM, XD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
-    default: hipLaunchKernelGGL((mlp_step_kernel<CT, 0, XD>), dim3(wgs), dim3(THREADS), 0, s, p);
-  }
-  OCF_HIP(hipGetLastError());
-}
 template <typename CT>
 void launch(const OcfMlpStepArgs& a, const P& p, int wgs, hipStream_t s) {
-  if (a.rows) launch_x<CT, false>(a, p, wgs, s);
-  else launch_x<CT, true>(a, p, wgs, s);
+  switch (a.opt.kind) {
+    case OCF_OPT_ADAGRAD: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAGRAD>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    case OCF_OPT_RMSPROP: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_RMSPROP>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    case OCF_OPT_ADAM: hipLaunchKernelGGL((mlp_step_kernel<CT, OCF_OPT_ADAM>), dim3(wgs), dim3(THREADS), 0, s, p); break;
+    default: hipLaunchKernelGGL((mlp_step_kernel<CT, 0>), dim3(wgs), dim3(THREADS), 0, s, p);
+  }
+  OCF_HIP(hipGetLastError());
 }
 
 }  // namespace mlp

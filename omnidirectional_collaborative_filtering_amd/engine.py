@@ -102,12 +102,7 @@ class Engine:
         self.fused_mlp = True
         self.mlp_trace = None
         self.mlp_wgs = 0                        # ocf_mlp_step's grid (0: the library's choice)
-        # generator batches of a small model through ocf_mlp_step too (opt-in: measured slower than the row
-        # gathers at ML-100K / ML-1M sizes)
-        self.fused_gen = False
-        self._fg_args = None                    # (key, scatter arguments) of the fused generator step
         self.step_paths = {"one_call": 0, "general": 0}   # fast_train_step's choices (diagnostics)
-        self.gen_dense = None                   # their dense X / M_in / M_out / T / M_miss / zeros [Bp][Np]
         self.act = _lib.ACT[activation]
         self.activation = activation
         self.dropout = dropout
@@ -535,9 +530,6 @@ class Engine:
             raise ValueError("target tile index has %d tiles, engine %d" % (targets["t_ntiles"], self.n_tiles))
         self.rows_real = None
         self._pending_pack = self._mlp_batch = None     # the scatter writes this batch's layer-0 input
-        if targets["flag"] == 1 and int(a.mode) == 0 and self._mlp_static_ok(gen=True):
-            self._load_batch_fused(a)
-            return
         if targets["E"] > self.tflag.numel():
             self.tflag = torch.zeros(max(targets["E"], 2 * self.tflag.numel()), device=self.dev, dtype=torch.uint8)
         a.tile_cnt = a.bk_ptr = a.bk_cur = a.bk_rc = a.bk_t = a.bk_m = None
@@ -683,83 +675,19 @@ class Engine:
     # ---------------------------------------------------------------- fused small-model step
     # A small dense model (train_jester.py: 0.14 M parameters, batch 128) on a row-gathered dense batch
     # (Model.fit) takes ONE persistent launch for the whole step (ocf.h ocf_mlp_step) instead of the
-    # layer-wise path's ~14 latency-bound launches.  No dropout, no l2, every layer trainable, one GPU.
-    # Generator batches (train.py's fit_generator) of the small I-AutoRec models (ML-100K, ML-1M: up to a few
-    # M parameters) can take it too (fused_gen, opt-in): ocf_scatter_batch writes the batch's dense X / M_out / T
-    # arrays (the data_gen arrays) and ocf_mlp_step runs the step with dense GEMMs instead of the row gathers.
-    # Exact (tests/test_train_gpu.py::*fused_generator*) but slower at those sizes: 32 x 32 tiles on a grid of
-    # at most 256 workgroups keep too few operand bytes in flight for K = 1,000-6,000 GEMMs.
+    # layer-wise path's ~14 latency-bound launches.  No l2, every layer trainable, one GPU.  (Generator batches
+    # of the small I-AutoRec models through it, on the dense data_gen arrays, were exact but slower than the
+    # row gathers -- ML-100K 0.089 vs 0.051 ms, ML-1M 0.39 vs 0.079 -- and were removed in round 5.)
     MLP_MAX_PARAMS = 4 << 20
-    MLP_GEN_MAX_PARAMS = 16 << 20
 
-    def _mlp_static_ok(self, gen=False):
-        return (self.fused_mlp and (self.fused_gen or not gen) and self.comm is None and self.dp_world == 1
+    def _mlp_static_ok(self):
+        return (self.fused_mlp and self.comm is None and self.dp_world == 1
                 and not self.l2 and all(self.trainable) and self.grad_hook is None and self.master_sync is None
                 and self.Bp <= 512 and self.opt is not None and self.opt.kind != _lib.OPT_SGD
-                and sum(w.numel() for w in self.W) <= (self.MLP_GEN_MAX_PARAMS if gen else self.MLP_MAX_PARAMS))
+                and sum(w.numel() for w in self.W) <= self.MLP_MAX_PARAMS)
 
     def _mlp_ok(self):
-        return (self._mlp_batch is not None and self._pending_pack is not None
-                and self._mlp_static_ok(gen=self._mlp_batch[2] is None))
-
-    def _fused_gen_step(self, gen, bi):
-        """fit_generator's step on batch bi of a small model: the scatter's arguments are built once per
-        generator (and epoch buffers) and only the batch's table pointers rewritten per step"""
-        key = (gen, gen.rows_dev, gen.boff_dev, gen.lboff1_dev, gen.keep_dev, gen.src1, self.gen_dense)
-        fa = self._fg_args
-        if fa is None or len(fa[0]) != len(key) or any(x is not y for x, y in zip(fa[0], key)):
-            self.load_batch(gen.scatter_args(bi, engine_args=self.scatter_args()), gen.targets(bi, self.N))
-            if self._mlp_batch is not None and self._mlp_batch[2] is None:
-                self._fg_args = ((gen, gen.rows_dev, gen.boff_dev, gen.lboff1_dev, gen.keep_dev, gen.src1,
-                                  self.gen_dense), self._fg_scatter)
-        else:
-            a, B = fa[1], gen.B
-            a.rows1 = gen.rows_dev.data_ptr() + 4 * bi * B
-            a.boff1 = gen.boff_dev.data_ptr() + 8 * bi * (B + 1)
-            a.lboff1 = gen.lboff1_dev.data_ptr() + 8 * bi * (B + 1)
-            a.E1 = int(gen.nnz1[bi])
-            a.keep1 = None if gen.keep_dev is None else gen.keep_dev.data_ptr() + int(gen.keep_off[bi])
-            if gen.r.rng == "device":
-                a.stream = 2 * (bi + 1)
-            self.rows_real = None
-            with self.phase("scatter"):
-                call("ocf_scatter_batch", a, cur_stream())
-            self._pending_pack = self._fg_pending
-            self._mlp_batch = self._fg_batch
-        self.train_step()
-
-    def _load_batch_fused(self, a):
-        """a train batch of a small model for ocf_mlp_step: the scatter writes the dense data_gen arrays
-        (X, the aux block, M_out, T) instead of the layer-0 input / gather tables"""
-        Bp, Np = self.Bp, self.Np
-        if self.gen_dense is None:
-            self.gen_dense = torch.zeros(6, Bp, Np, device=self.dev, dtype=torch.float32)
-        d = self.gen_dense              # [X, M_out, T, M_in, M_miss, zeros]: the always-written blocks adjacent
-        a.X, a.Mout, a.T = ptr(d[0]), ptr(d[1]), ptr(d[2])  # (the scatter clears adjacent outputs in one memset)
-        a.Min = ptr(d[3]) if a.feed == 1 else None
-        a.Mmiss = ptr(d[4]) if (a.feed == 2 or a.both) else None
-        a.ld = Np
-        a.xin = None
-        a.tile_cnt = a.bk_ptr = a.bk_cur = a.bk_rc = a.bk_t = a.bk_m = None
-        a.tflag1 = a.tflag2 = a.xval1 = a.col_cnt = a.ecb = a.rtag_in = a.rtag_out = a.tb_cnt = None
-        a.tb_nk = 0
-        with self.phase("scatter"):
-            call("ocf_scatter_batch", a, cur_stream())
-        blocks = [d[0]]
-        if self.k >= 2:
-            blocks.append({1: d[3], 2: d[4]}.get(int(a.feed), d[5]))
-        if self.k >= 3:
-            blocks.append(d[4])
-        p = [ptr(t) for t in blocks] + [None] * (3 - len(blocks))
-        self.rows_real = None
-        self._pending_pack = (p, Np, None)          # packed into xin only if the layer-wise path runs after all
-        self._mlp_batch = (p, Np, None, ptr(d[1]), ptr(d[2]))
-        self._fg_scatter, self._fg_pending, self._fg_batch = a, self._pending_pack, self._mlp_batch
-        self.tseg = dict(dn_t=ptr(d[2]), dn_m=ptr(d[1]), ld_dn=Np, dn_rows=None, n_real=self.N)
-        self._dense_keep = (d,)
-        self.tb = self.gt = self._enc_fused = None
-        self._rtag_live = False
-        self._live_ptrs = None
+        return self._mlp_batch is not None and self._pending_pack is not None and self._mlp_static_ok()
 
     def _mlp_step(self):
         a = self._mlp_args
@@ -1417,10 +1345,6 @@ class Engine:
         """Model._train_one's step on generator batch bi through ocf_train_step_rows; False when this step
         must take the general path (then nothing was done)."""
         self.rows_real = None         # a generator batch: always B rows
-        if self._mlp_static_ok(gen=True) and getattr(gen, "split", None) == "train":
-            # a small model: dense arrays + ocf_mlp_step (no gather tables, no row lists)
-            self._fused_gen_step(gen, bi)
-            return True
         if not self.fast_steps or (self.timers is not None and self.timer_only is None):
             return False
         if self.comm is not None:

@@ -48,7 +48,6 @@ def _model(opt, dropout, data):
     o = {"adagrad": lambda: O.Adagrad(lr=0.005, epsilon=1e-8), "adagrad_decay": lambda: O.Adagrad(lr=0.005, decay=0.01),
          "adam": lambda: O.Adam(lr=0.001), "rmsprop": lambda: O.RMSprop(lr=0.001)}[opt]()
     om.model.compile(o, "mean_squared_error")
-    om.engine.fused_gen = False         # the row-gather step (a model this small would take ocf_mlp_step)
     return om
 
 
@@ -116,7 +115,6 @@ def test_fast_step_declines_other_layouts(stubbed):
     frozen = omni_model(1, 64, data.num_cols, 32, dense_activation="sigmoid", use_causal_info=False, device=cpu)
     for om in (two, l2, frozen):
         om.model.compile(O.Adagrad(lr=0.005), "mean_squared_error")
-        om.engine.fused_gen = False
     frozen.engine.trainable[0] = False
     for om in (two, l2, frozen):
         gen = rd.data_gen(32, [1.0, 1.0], "train", True, None, -1)
@@ -193,44 +191,3 @@ def test_rank_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
                 assert eng.fast_train_step(gen, bi)
     assert checked >= 12 and fast >= 5, (checked, fast)
 
-
-def test_small_model_generator_step_is_one_fused_launch(monkeypatch):
-    """a small model's generator batch: the scatter writes the dense data_gen arrays and ocf_mlp_step runs
-    the step (no gather tables, no row lists, no dense GEMM sequence); its dropout fields follow forward()"""
-    _lib.load()
-    calls = []
-
-    def fake_call(name, *args):
-        calls.append((name, args))
-        return 0
-    monkeypatch.setattr(_lib, "call", fake_call)
-    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
-    from omnidirectional_collaborative_filtering_amd import data_reader as DR
-    from omnidirectional_collaborative_filtering_amd import engine as E
-    monkeypatch.setattr(E, "cur_stream", lambda: None)
-    monkeypatch.setattr(DR, "cur_stream", lambda: None)
-    monkeypatch.setattr(DR, "_rng_stream", lambda dev: None)
-    monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
-    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
-    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
-    r, c, v = synthetic_ratings(400, 300, 9000, half_stars=True, seed=3)
-    data = split_ratings(r, c, v, 400, 300, rng=np.random.RandomState(3), dup_free=True)
-    np.random.seed(5)
-    rd = data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split", rng="numpy",
-                     device=torch.device("cpu"))
-    om = _model("adagrad", 0.2, data)
-    eng = om.engine
-    eng.fused_gen = True
-    gen = rd.data_gen(32, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
-    for step in range(3):
-        calls.clear()
-        assert eng.fast_train_step(gen, gen.next_batch_index())
-        calls[:] = [c for c in calls if c[0] != "ocf_recip_keep"]     # (the epoch's NumPy draws, first step)
-        names = [n for n, _ in calls]
-        assert names == ["ocf_scatter_batch", "ocf_mlp_step"], names
-        sa, ma = calls[0][1][0], calls[1][1][0]
-        assert sa.X and sa.Mout and sa.T and not sa.xin and not sa.xval1      # the data_gen arrays only
-        assert ma.rows is None and ma.x[0] == sa.X and ma.out_mask == sa.Mout and ma.targets == sa.T
-        assert sa.Mout - sa.X == sa.T - sa.Mout == eng.Bp * eng.Np * 4     # one memset clears all three
-        assert ma.ld_x == eng.Np and abs(ma.keep - 0.8) < 1e-7 and ma.stream == step * 16
-        assert ma.mask[0] == eng.mask[0].data_ptr()

@@ -74,26 +74,3 @@ def test_fp32_l2_regulariser(gpu, gather):
     assert_fp32(res)
 
 
-# ---- the fused small-model step on generator batches (ocf_mlp_step, dense data_gen arrays) ------------------
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt_name,layers,act,dropout,causal", [
-    ("adagrad", 1, "sigmoid", None, False), ("adagrad", 1, "sigmoid", 0.2, False),
-    ("rmsprop", 2, "tanh", 0.2, True), ("adam", 2, "relu", None, False)])
-def test_fp32_parity_fused_generator_step(gpu, opt_name, layers, act, dropout, causal):
-    """train.py's generator batches through the one-launch step: the forward, dropout (the device's
-    Philox masks read back into the oracle), masked MSE, backward and every update meet the fp32 bar"""
-    res = run_parity("float32", opt_name, layers, act, dropout=dropout, H=100 if layers == 1 else 96,
-                     aux_type="causal" if causal else None, causal=causal, fused=True)
-    assert res.om.engine._mlp_args is not None, "ocf_mlp_step did not run"
-    assert_fp32(res)
-    if dropout:
-        keep_frac = sum(float(m[0].mean()) for m in res.masks) / len(res.masks)
-        assert 0.75 < keep_frac < 0.85, keep_frac
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("cd,tol", [("float16", 2e-3), ("bfloat16", 1e-2)])
-def test_low_precision_fused_generator_step(gpu, cd, tol):
-    res = run_parity(cd, "adagrad", 1, "sigmoid", dropout=0.2, envelope=True, fused=True)
-    assert res.om.engine._mlp_args is not None, "ocf_mlp_step did not run"
-    assert_low_precision(res, tol)

@@ -1,7 +1,6 @@
-"""Per-phase timing of the fused small-model step (ocf_mlp_step) on the Jester configuration (or, --config
-ml100k|ml1m, the opt-in generator path of an I-AutoRec model): workgroup 0's 100 MHz clock at the start and at
-every grid barrier (arrive / leave), averaged over steps.
-    python tools/mlp_trace.py [--dtype bfloat16] [--wgs 0] [--config jester]"""
+"""Per-phase timing of the fused small-model step (ocf_mlp_step) on the Jester configuration: workgroup 0's
+100 MHz clock at the start and at every grid barrier (arrive / leave), averaged over steps.
+    python tools/mlp_trace.py [--dtype bfloat16] [--wgs 0]"""
 import argparse
 import json
 import os
@@ -18,7 +17,6 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--dtype", default="bfloat16")
 ap.add_argument("--wgs", type=int, default=0)
 ap.add_argument("--steps", type=int, default=30)
-ap.add_argument("--config", default="jester")
 a = ap.parse_args()
 
 
@@ -28,33 +26,6 @@ def trace_of(e):
     return np.diff(t[:n]) / 100.0                  # us between marks
 
 
-if a.config != "jester":
-    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
-    from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
-    data = synthetic_fixed_split(a.config, seed=0)
-    rd = data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split", device=torch.device("cuda"))
-    om = omni_model(1, 500, data.num_cols, 256, dense_activation="sigmoid", use_causal_info=False,
-                    dropout_probability=0.2, compute_dtype=a.dtype, seed=7)
-    om.model.compile("adagrad", "mean_squared_error")
-    e = om.engine
-    e.fused_gen = True
-    e.mlp_trace = torch.zeros(24, dtype=torch.int64, device="cuda")
-    e.mlp_wgs = a.wgs
-    gen = rd.data_gen(256, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
-    rows = []
-    for s in range(min(a.steps, gen.num_batches) if hasattr(gen, "num_batches") else a.steps):
-        bi = gen.next_batch_index()
-        if bi is None:
-            break
-        e.fast_train_step(gen, bi)
-        torch.cuda.synchronize()
-        rows.append(trace_of(e))
-    d = np.mean(rows[2:], axis=0)
-    print(json.dumps({"config": a.config, "dtype": a.dtype, "wgs": a.wgs or "default",
-                      "grid": e._mlp_args.wgs if e._mlp_args is not None else None,
-                      "us_between_marks": [round(x, 2) for x in d], "total_us": round(float(d.sum()), 2),
-                      "marks": "start, then per barrier: arrive, leave; last: end"}))
-    sys.exit(0)
 inputs, observed, out_m, targets = jester_arrays(n=20000)
 om = omni_model(2, 256, 100, 128, dense_activation="tanh", use_causal_info=True, compute_dtype=a.dtype, seed=3)
 m = om.model
