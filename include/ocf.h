@@ -168,6 +168,12 @@ typedef struct OcfGatherArgs {
    * last chunk of a row resets it); rows without chunks (padding, no targets) get the zero delta.  jr->part
    * and jr->chunk_stats must be this launch's part and chunk_stats, jr->H its H. */
   const struct OcfRowsReduceArgs* jr; uint32_t* row_arrive;
+  /* optional, both gathers: range order for wide weights (W does not fit the Infinity Cache).  perm != NULL:
+   * col / val are the CSR's column-sorted view (same rp) and perm[rp[r] + k] the list position of the k-th
+   * sorted entry of row r (xval / flag / delta_e are indexed by list position); ch_j0 / ch_j1 then index the
+   * sorted view.  ch_slot != 0: the chunk table is in dispatch order and ch_row[c] = batch row | slot << 12,
+   * slot = the chunk's partial / chunk_stats index (row-major: a row's slots contiguous, row_cptr as before). */
+  const int32_t* perm; int ch_slot;
 } OcfGatherArgs;
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);
@@ -505,8 +511,10 @@ int ocf_row_lists(const OcfRowListArgs* args, void* stream);
  * scan of the column counts (row_ptr[s][n_cols] = the batch's entry count), and with live non-null
  * the OCF_LIVE_REC records of the columns holding at least one entry (a superset of the columns with
  * a nonzero gradient: an Adagrad l2 = 0 update at g = 0 is the identity, so the row skip stays exact).
- * B <= 4,096; a batch's entries < 2^31.  cnt: scratch of n_sel * n_cols + 1 + 2 * (entries / 1025 + 1)
- * ints (counts, then the queue of lists over 1,024 entries).  n_cols % 128 == 0.
+ * B <= 4,096; a batch's entries < 2^31.  n_rg (0 or 1: one; at most min(64, B)): row groups per batch --
+ * the count / fill walks split each batch's rows over n_rg workgroups (more parallelism when few batches are
+ * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols + 1 + 2 * (entries /
+ * 1025 + 1) ints (counts per row group, then the queue of lists over 1,024 entries).  n_cols % 128 == 0.
  * Extension (no reference counterpart): the data_reader.py:326-419 batch loop's structure, per epoch. */
 typedef struct OcfEpochRowListArgs {
   int n_sel; int B; int n_cols;
@@ -519,6 +527,7 @@ typedef struct OcfEpochRowListArgs {
   int32_t* row_ptr;                      /* [n_sel][n_cols + 1] */
   int32_t* row_ent;                      /* [ebase[n_sel]][2] */
   uint8_t* live;                         /* [n_sel][n_cols / 128][OCF_LIVE_REC] or null */
+  int n_rg;                              /* row groups per batch (0 / 1: one) */
 } OcfEpochRowListArgs;
 int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream);
 

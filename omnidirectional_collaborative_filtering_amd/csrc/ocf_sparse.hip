@@ -215,6 +215,15 @@ __device__ __forceinline__ void dec_zero_rows(const OcfRowsReduceArgs& r) {
   }
 }
 
+// chunk of this workgroup: batch row b and its partial / stats slot c.  Range order (ch_slot): the chunk table
+// is in dispatch order (column range, then batch row) and ch_row packs b | slot << 12, the slot being the
+// chunk's row-major index -- a row's partials stay contiguous for the row reductions (row_cptr)
+__device__ __forceinline__ void chunk_of(const OcfGatherArgs& a, int& b, int& c) {
+  const int cr = a.ch_row[blockIdx.x];
+  b = a.ch_slot ? (cr & 4095) : cr;
+  c = a.ch_slot ? (cr >> 12) : (int)blockIdx.x;
+}
+
 // A group of G lanes owns one entry at a time (RG_U entries in flight); lane l holds pieces
 // l, l+G, ... (PPL of them) of the weight row, so a group's load instruction reads G*16
 // contiguous bytes.
@@ -224,8 +233,9 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
   __shared__ float red[NG * RG_MAX_H];
-  const int c = blockIdx.x;
-  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
+  int b, c;
+  chunk_of(a, b, c);
+  const int j0 = a.ch_j0[blockIdx.x], j1 = a.ch_j1[blockIdx.x];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
   const int64_t s = r >= 0 ? a.rp[r] : 0;
@@ -234,7 +244,9 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   float acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
-  // entry indices one iteration ahead of the weight-row loads that depend on them
+  // entry indices one iteration ahead of the weight-row loads that depend on them.  With the column-sorted view
+  // (perm) an entry's input value sits at its list position perm[s + j]: the weight row is then loaded for every
+  // entry of the chunk (its column needs no perm hop; a zero input adds 0 x W)
   float x[RG_U];
   int n[RG_U];
   auto idx = [&](int j) {
@@ -242,8 +254,9 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
       const bool ok = ju < j1;
-      x[u] = ok ? a.xval[lb + ju] : 0.f;
-      n[u] = ok ? a.col[s + ju] : 0;
+      const int jl = ok ? (a.perm ? a.perm[s + ju] : ju) : 0;
+      x[u] = ok ? a.xval[lb + jl] : 0.f;
+      n[u] = ok ? a.col[s + ju] : -1;
     }
   };
   idx(j0 + grp);
@@ -253,9 +266,10 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       xc[u] = x[u];
+      const bool ld = a.perm ? n[u] >= 0 : x[u] != 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
-        w[u][i] = x[u] != 0.f ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+        w[u][i] = ld ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
     }
     idx(j + NG * RG_U);
 #pragma unroll
@@ -278,18 +292,19 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   constexpr int NG = RG_THREADS / G;
   __shared__ float red[NG * RG_MAX_H];
   __shared__ float st[NG][3];
-  const int c = blockIdx.x;
-  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
+  int b, c;
+  chunk_of(a, b, c);
+  const int j0 = a.ch_j0[blockIdx.x], j1 = a.ch_j1[blockIdx.x];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
   const int64_t s = r >= 0 ? a.rp[r] : 0;
   const int64_t lb = a.lboff[b];
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
-  if (a.zero_word && c == 0 && threadIdx.x == 0)
+  if (a.zero_word && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool fold = a.row_arrive != nullptr;
-  if (fold && c == 0) dec_zero_rows(jr);
+  if (fold && blockIdx.x == 0) dec_zero_rows(jr);
   __shared__ float a_sh[RG_MAX_H];             // (fold) the row's activation / dropout mask from the epilogue
   __shared__ uint8_t mk_sh[RG_MAX_H];
   float hv[V];
@@ -297,15 +312,16 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->
   // LDS) and this one (flag / column / target) overlap instead of running back to back
   bool live[RG_U];
-  int n[RG_U];
+  int n[RG_U], jl[RG_U];
   float t[RG_U];
   auto idx = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
       const bool ok = ju < j1;
-      live[u] = ok && a.flag[lb + ju];
-      n[u] = ok ? a.col[s + ju] : 0;
+      jl[u] = ok ? (a.perm ? a.perm[s + ju] : ju) : 0;     // the entry's list position (column-sorted view)
+      live[u] = ok && a.flag[lb + jl[u]];
+      n[u] = ok ? a.col[s + ju] : -1;
       t[u] = ok ? a.val[s + ju] : 0.f;
     }
   };
@@ -356,17 +372,21 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   for (int j = j0 + grp; j < j1; j += NG * RG_U) {
     uint4 w[RG_U][PPL];
     bool lv[RG_U];
-    int nc[RG_U];
+    int nc[RG_U], jc[RG_U];
     float tc[RG_U], bn[RG_U];
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       lv[u] = live[u];
       nc[u] = n[u];
+      jc[u] = jl[u];
       tc[u] = t[u];
-      bn[u] = live[u] ? a.bias[n[u]] : 0.f;
+      // (column-sorted view: every entry's row is loaded, so the load waits on the column only, not on the
+      // perm -> flag hop; a non-target entry's delta is 0)
+      const bool ld = a.perm ? n[u] >= 0 : live[u];
+      bn[u] = ld ? a.bias[n[u]] : 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
-        w[u][i] = live[u] ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+        w[u][i] = ld ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
     }
     idx(j + NG * RG_U);
     float dot[RG_U];
@@ -402,7 +422,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
           if (a.d_out) store_ct(a.d_out, a.d_dtype, (int64_t)b * a.ld_d + nc[u], d);
         }
       }
-      if (l == 0 && a.delta_e) a.delta_e[lb + ju] = d;
+      if (l == 0 && a.delta_e) a.delta_e[lb + jc[u]] = d;
 #pragma unroll
       for (int i = 0; i < PPL; ++i) {
         float f[E];
@@ -1019,15 +1039,20 @@ __device__ __forceinline__ void erl_stage(const OcfEpochRowListArgs& a, int s, c
   }
 }
 
-// per (column block, batch): the block's column counts
+// per (column block, batch, row group): the block's column counts over the group's batch rows.  A batch's rows
+// are split into n_rg groups (OcfEpochRowListArgs n_rg) when few batches are built at once: each workgroup
+// walks one group instead of the whole batch (the count and fill walks are latency-bound chains of loads;
+// with a window of 20 batches the grid held 60 workgroups).  Counts go to cnt[rg][s][column].
+__device__ __forceinline__ int erl_rg(const OcfEpochRowListArgs& a) { return a.n_rg > 1 ? a.n_rg : 1; }
 __global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListArgs a, int cb) {
   const ErlLds l = erl_lds(a.B);
-  const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
+  const int s = blockIdx.y, rg = blockIdx.z, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
+  const int nrg = erl_rg(a), b0 = rg * a.B / nrg, b1 = (rg + 1) * a.B / nrg;
   for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;   // nc % 128 == 0
   erl_stage(a, s, l);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int b = w; b < a.B; b += ERL_THREADS / 64) {
+  for (int b = b0 + w; b < b1; b += ERL_THREADS / 64) {
     const int n = l.off[b + 1] - l.off[b];
     const int* col = a.col + l.src[b];
     // ERL_U column loads in flight per lane (a one-load loop waited a round trip per 64 entries)
@@ -1041,24 +1066,32 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListA
     }
   }
   __syncthreads();
-  int* g = a.cnt + (int64_t)s * a.n_cols + c0;
+  int* g = a.cnt + ((int64_t)rg * a.n_sel + s) * a.n_cols + c0;
   for (int i = threadIdx.x; i < nc; i += ERL_THREADS) g[i] = (int)((l.cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
 }
 
-// per batch: exclusive scan of its column counts (4,096 columns per pass, running carry), counts zeroed
-// for the fill's cursors
+// per batch: exclusive scan of its column counts (summed over the row groups; 4,096 columns per pass, running
+// carry); each group's counts become its exclusive prefix over the earlier groups (the fill's cursor starts)
 __global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
   __shared__ int wtot[16];
   __shared__ int carry_s;
-  const int s = blockIdx.x, n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int s = blockIdx.x, n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nrg = erl_rg(a);
+  const int64_t gstride = (int64_t)a.n_sel * n;
   int* cnt = a.cnt + (int64_t)s * n;
   int* rp = a.row_ptr + (int64_t)s * (n + 1);
-  if (s == 0 && tid == 0) a.cnt[(int64_t)a.n_sel * n] = 0;   // erl_sort's long-list queue
+  if (s == 0 && tid == 0) a.cnt[(int64_t)nrg * gstride] = 0;   // erl_sort's long-list queue
   int carry = 0;
   for (int base = 0; base < n; base += 4096) {
     const int i0 = base + 4 * tid;
     int4 v = make_int4(0, 0, 0, 0);
-    if (i0 < n) v = *reinterpret_cast<const int4*>(cnt + i0);   // n % 128 == 0: all 4 columns in range or none
+    if (i0 < n) {                       // n % 128 == 0: all 4 columns in range or none
+      for (int g = 0; g < nrg; ++g) {
+        int4* q = reinterpret_cast<int4*>(cnt + g * gstride + i0);
+        const int4 c = *q;
+        if (nrg > 1) *q = v;            // the group's cursor start: the earlier groups' counts
+        v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+      }
+    }
     const int ts = v.x + v.y + v.z + v.w;
     const int incl = wave_incl_scan(ts, lane);
     if (lane == 63) wtot[w] = incl;
@@ -1083,14 +1116,21 @@ __global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
 // unordered within a column, erl_sort_kernel orders each list)
 __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListArgs a, int cb) {
   const ErlLds l = erl_lds(a.B);
-  const int s = blockIdx.y, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
-  for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;
+  const int s = blockIdx.y, rg = blockIdx.z, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
+  const int nrg = erl_rg(a), b0 = rg * a.B / nrg, b1 = (rg + 1) * a.B / nrg;
+  if (nrg > 1) {      // the group's cursors start after the earlier groups' entries (erl_scan_kernel)
+    const int* pre = a.cnt + ((int64_t)rg * a.n_sel + s) * a.n_cols + c0;
+    for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS)
+      l.cnt[i] = (uint32_t)pre[2 * i] | ((uint32_t)pre[2 * i + 1] << 16);
+  } else {
+    for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;
+  }
   erl_stage(a, s, l);
   __syncthreads();
   const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
   int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int b = w; b < a.B; b += ERL_THREADS / 64) {
+  for (int b = b0 + w; b < b1; b += ERL_THREADS / 64) {
     const int e0 = l.off[b], n = l.off[b + 1] - e0;
     const int* col = a.col + l.src[b];
     // ERL_U entries per lane in flight: their columns, then their lists' starts (a one-entry loop waited two
@@ -1146,7 +1186,7 @@ __global__ void __launch_bounds__(128) erl_sort_kernel(OcfEpochRowListArgs a) {
     else if (nm <= 16) rl_reg_sort<16>(ent + lo, n);
     else rl_reg_sort<RL_REG>(ent + lo, n);
   } else if (n > ERL_MID) {
-    int* q = a.cnt + (int64_t)a.n_sel * n_cols;      // long-list queue after the counters
+    int* q = a.cnt + (int64_t)erl_rg(a) * a.n_sel * n_cols;      // long-list queue after the counters
     const int qi = atomicAdd(q, 1);
     q[1 + 2 * qi] = s;
     q[2 + 2 * qi] = m;
@@ -1168,7 +1208,7 @@ __global__ void __launch_bounds__(128) erl_sort_kernel(OcfEpochRowListArgs a) {
 // one workgroup per queued list of more than ERL_MID entries (<= ERL_LONG_MAX: one per batch row)
 __global__ void __launch_bounds__(1024) erl_sort_long_kernel(OcfEpochRowListArgs a) {
   __shared__ int2 buf[ERL_LONG_MAX];
-  const int* q = a.cnt + (int64_t)a.n_sel * a.n_cols;
+  const int* q = a.cnt + (int64_t)erl_rg(a) * a.n_sel * a.n_cols;
   const int nq = q[0];
   for (int qi = blockIdx.x; qi < nq; qi += gridDim.x) {
     const int s = q[1 + 2 * qi], m = q[2 + 2 * qi];
@@ -1193,6 +1233,7 @@ extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream
   OCF_CHECK(a.n_cols > 0 && a.n_cols % 128 == 0, "ocf_epoch_row_lists: n_cols > 0, % 128");
   OCF_CHECK(a.B > 0 && a.B <= ERL_MAXB, "ocf_epoch_row_lists: 0 < B <= 4096 (one entry per batch row and column)");
   OCF_CHECK(a.n_sel >= 0 && a.n_sel <= 65535, "ocf_epoch_row_lists: 0 <= n_sel <= 65535");
+  OCF_CHECK(a.n_rg >= 0 && a.n_rg <= 64 && a.n_rg <= a.B, "ocf_epoch_row_lists: 0 <= n_rg <= min(64, B)");
   if (a.n_sel == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const int cb = erl_block_cols(a.B), ncb = (a.n_cols + cb - 1) / cb;
@@ -1204,9 +1245,10 @@ extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream
                hipSuccess;
   }();
   OCF_CHECK(lds_attr, "ocf_epoch_row_lists: cannot raise the dynamic LDS limit");
-  hipLaunchKernelGGL(erl_count_kernel, dim3(ncb, a.n_sel), dim3(ERL_THREADS), lds, s, a, cb);
+  const int nrg = a.n_rg > 1 ? a.n_rg : 1;
+  hipLaunchKernelGGL(erl_count_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
   hipLaunchKernelGGL(erl_scan_kernel, dim3(a.n_sel), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel), dim3(ERL_THREADS), lds, s, a, cb);
+  hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
   hipLaunchKernelGGL(erl_sort_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(128), 0, s, a);
   hipLaunchKernelGGL(erl_sort_long_kernel, dim3(64), dim3(1024), 0, s, a);
   OCF_HIP(hipGetLastError());
