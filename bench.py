@@ -93,9 +93,9 @@ def parse():
     ap.add_argument("--reduce-in-decoder", type=int, default=-1,
                     help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
                          "engine default (small weights)")
-    ap.add_argument("--gather-ranges", type=int, default=-1,
-                    help="row gathers in range order over this many column ranges (0: list order; -1: the reader's "
-                         "rule, on for weights over data_reader.GATHER_RANGE_MIN_COLS columns)")
+    ap.add_argument("--fold-reduce", type=int, default=1,
+                    help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
+                         "ocf_rows_reduce launch)")
     ap.add_argument("--fold-jobs", type=int, default=1,
                     help="stats and bias updates folded into the dW_out launch (0: separate launches)")
     ap.add_argument("--shadow-blocked", type=int, default=-1,
@@ -521,8 +521,6 @@ def main():
     np.random.seed(1234)
     # rng="numpy": the reference's own RNG stream (NumPy's MT19937 state, epoch draws on the device)
     rd = data_reader(data.num_cols, n_rows, dataset=data, eval_mode="fixed_split", rng="numpy", device=dev)
-    if args.gather_ranges >= 0:
-        rd.gather_ranges = args.gather_ranges
     om = omni_model(1, H, data.num_cols, Bg, dense_activation="sigmoid", use_causal_info=False,
                     dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev,
                     shard=shard, comm=comm)
@@ -536,6 +534,7 @@ def main():
     eng.use_sparse = bool(args.gather)
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
+    eng.fold_reduce = bool(args.fold_reduce)
     if args.reduce_in_decoder >= 0:
         eng.reduce_in_decoder = bool(args.reduce_in_decoder)
     eng.split_dw_streams = bool(args.split_dw)

@@ -168,12 +168,6 @@ typedef struct OcfGatherArgs {
    * last chunk of a row resets it); rows without chunks (padding, no targets) get the zero delta.  jr->part
    * and jr->chunk_stats must be this launch's part and chunk_stats, jr->H its H. */
   const struct OcfRowsReduceArgs* jr; uint32_t* row_arrive;
-  /* optional, both gathers: range order for wide weights (W does not fit the Infinity Cache).  perm != NULL:
-   * col / val are the CSR's column-sorted view (same rp) and perm[rp[r] + k] the list position of the k-th
-   * sorted entry of row r (xval / flag / delta_e are indexed by list position); ch_j0 / ch_j1 then index the
-   * sorted view.  ch_slot != 0: the chunk table is in dispatch order and ch_row[c] = batch row | slot << 12,
-   * slot = the chunk's partial / chunk_stats index (row-major: a row's slots contiguous, row_cptr as before). */
-  const int32_t* perm; int ch_slot;
 } OcfGatherArgs;
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);

@@ -76,7 +76,7 @@ class OcfGatherArgs(ctypes.Structure):
         ("d_out", P), ("d_dtype", I32), ("ld_d", I64),
         ("enc_part", P), ("enc_cptr", P), ("bias_h", P), ("act", I32), ("keep", F32), ("seed", U64), ("stream", U64),
         ("a_out", P), ("mask_out", P), ("m_real", I32), ("n_real", I32), ("zero_word", P),
-        ("jr", P), ("row_arrive", P), ("perm", P), ("ch_slot", I32),
+        ("jr", P), ("row_arrive", P),
     ]
 
 

@@ -215,15 +215,6 @@ __device__ __forceinline__ void dec_zero_rows(const OcfRowsReduceArgs& r) {
   }
 }
 
-// chunk of this workgroup: batch row b and its partial / stats slot c.  Range order (ch_slot): the chunk table
-// is in dispatch order (column range, then batch row) and ch_row packs b | slot << 12, the slot being the
-// chunk's row-major index -- a row's partials stay contiguous for the row reductions (row_cptr)
-__device__ __forceinline__ void chunk_of(const OcfGatherArgs& a, int& b, int& c) {
-  const int cr = a.ch_row[blockIdx.x];
-  b = a.ch_slot ? (cr & 4095) : cr;
-  c = a.ch_slot ? (cr >> 12) : (int)blockIdx.x;
-}
-
 // A group of G lanes owns one entry at a time (RG_U entries in flight); lane l holds pieces
 // l, l+G, ... (PPL of them) of the weight row, so a group's load instruction reads G*16
 // contiguous bytes.
@@ -233,9 +224,8 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
   __shared__ float red[NG * RG_MAX_H];
-  int b, c;
-  chunk_of(a, b, c);
-  const int j0 = a.ch_j0[blockIdx.x], j1 = a.ch_j1[blockIdx.x];
+  const int c = blockIdx.x;
+  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
   const int64_t s = r >= 0 ? a.rp[r] : 0;
@@ -244,9 +234,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   float acc[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
-  // entry indices one iteration ahead of the weight-row loads that depend on them.  With the column-sorted view
-  // (perm) an entry's input value sits at its list position perm[s + j]: the weight row is then loaded for every
-  // entry of the chunk (its column needs no perm hop; a zero input adds 0 x W)
+  // entry indices one iteration ahead of the weight-row loads that depend on them
   float x[RG_U];
   int n[RG_U];
   auto idx = [&](int j) {
@@ -254,9 +242,8 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
       const bool ok = ju < j1;
-      const int jl = ok ? (a.perm ? a.perm[s + ju] : ju) : 0;
-      x[u] = ok ? a.xval[lb + jl] : 0.f;
-      n[u] = ok ? a.col[s + ju] : -1;
+      x[u] = ok ? a.xval[lb + ju] : 0.f;
+      n[u] = ok ? a.col[s + ju] : 0;
     }
   };
   idx(j0 + grp);
@@ -266,10 +253,9 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       xc[u] = x[u];
-      const bool ld = a.perm ? n[u] >= 0 : x[u] != 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
-        w[u][i] = ld ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+        w[u][i] = x[u] != 0.f ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
     }
     idx(j + NG * RG_U);
 #pragma unroll
@@ -292,19 +278,18 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   constexpr int NG = RG_THREADS / G;
   __shared__ float red[NG * RG_MAX_H];
   __shared__ float st[NG][3];
-  int b, c;
-  chunk_of(a, b, c);
-  const int j0 = a.ch_j0[blockIdx.x], j1 = a.ch_j1[blockIdx.x];
+  const int c = blockIdx.x;
+  const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
   const int64_t s = r >= 0 ? a.rp[r] : 0;
   const int64_t lb = a.lboff[b];
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
-  if (a.zero_word && blockIdx.x == 0 && threadIdx.x == 0)
+  if (a.zero_word && c == 0 && threadIdx.x == 0)
     __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool fold = a.row_arrive != nullptr;
-  if (fold && blockIdx.x == 0) dec_zero_rows(jr);
+  if (fold && c == 0) dec_zero_rows(jr);
   __shared__ float a_sh[RG_MAX_H];             // (fold) the row's activation / dropout mask from the epilogue
   __shared__ uint8_t mk_sh[RG_MAX_H];
   float hv[V];
@@ -312,16 +297,15 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->
   // LDS) and this one (flag / column / target) overlap instead of running back to back
   bool live[RG_U];
-  int n[RG_U], jl[RG_U];
+  int n[RG_U];
   float t[RG_U];
   auto idx = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       const int ju = j + u * NG;
       const bool ok = ju < j1;
-      jl[u] = ok ? (a.perm ? a.perm[s + ju] : ju) : 0;     // the entry's list position (column-sorted view)
-      live[u] = ok && a.flag[lb + jl[u]];
-      n[u] = ok ? a.col[s + ju] : -1;
+      live[u] = ok && a.flag[lb + ju];
+      n[u] = ok ? a.col[s + ju] : 0;
       t[u] = ok ? a.val[s + ju] : 0.f;
     }
   };
@@ -372,21 +356,17 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   for (int j = j0 + grp; j < j1; j += NG * RG_U) {
     uint4 w[RG_U][PPL];
     bool lv[RG_U];
-    int nc[RG_U], jc[RG_U];
+    int nc[RG_U];
     float tc[RG_U], bn[RG_U];
 #pragma unroll
     for (int u = 0; u < RG_U; ++u) {
       lv[u] = live[u];
       nc[u] = n[u];
-      jc[u] = jl[u];
       tc[u] = t[u];
-      // (column-sorted view: every entry's row is loaded, so the load waits on the column only, not on the
-      // perm -> flag hop; a non-target entry's delta is 0)
-      const bool ld = a.perm ? n[u] >= 0 : live[u];
-      bn[u] = ld ? a.bias[n[u]] : 0.f;
+      bn[u] = live[u] ? a.bias[n[u]] : 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i)
-        w[u][i] = ld ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+        w[u][i] = live[u] ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
     }
     idx(j + NG * RG_U);
     float dot[RG_U];
@@ -422,7 +402,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
           if (a.d_out) store_ct(a.d_out, a.d_dtype, (int64_t)b * a.ld_d + nc[u], d);
         }
       }
-      if (l == 0 && a.delta_e) a.delta_e[lb + jc[u]] = d;
+      if (l == 0 && a.delta_e) a.delta_e[lb + ju] = d;
 #pragma unroll
       for (int i = 0; i < PPL; ++i) {
         float f[E];

@@ -44,12 +44,6 @@ ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the lib
 ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
 ROWLIST_RG_WORK = 160           # (batches x row groups) per row-list build: at least this many, row groups <= 8
 ROWS_DENSE_MAX_COLS = 170 * 128  # the row-stream kernel's small regime (ocf_gemm.hip rows_small_waves: 170 tiles)
-# range order of the row gathers (OcfGatherArgs perm / ch_slot) for weights wider than this many columns: the W
-# table (1 KB per column at H = 512) outgrows the 256 MiB Infinity Cache, and a batch reads each live row ~2-3
-# times (Netflix: 1.15 M entries over ~437 K rows).  The columns are cut into ranges of ~GATHER_RANGE_COLS and the
-# chunks dispatched range by range, so the rows' repeated reads meet in the cache (tools/probes/netflix_order.hip)
-GATHER_RANGE_MIN_COLS = 262_144
-GATHER_RANGE_COLS = 15_000
 
 
 _RNG_STREAMS = {}
@@ -85,25 +79,6 @@ class _DeviceCSR:
         self.rng_lens = csr.rng_lengths()      # entries of the full rows (RNG draws, batch offsets)
         self.dev = dev
         self._tiles = {}
-        self._sorted = None
-
-    def sorted_view(self):
-        """the entries of every row sorted by column (stable): host key (row * 2^32 + col, globally sorted) and
-        device col / val / list-position arrays (OcfGatherArgs perm), built once per CSR"""
-        if self._sorted is None:
-            from .dataset import stable_order
-            h = self.host
-            lens = h.row_lengths()
-            rows = np.repeat(np.arange(h.n_rows, dtype=np.int64), lens)
-            order = stable_order(rows, h.col.astype(np.int64))
-            col_s = h.col[order]
-            key = (rows << 32) | col_s.astype(np.int64)
-            lidx = (order - h.row_ptr[rows]).astype(np.int32)
-            d = self.dev
-            self._sorted = dict(key=key, col=torch.as_tensor(np.ascontiguousarray(col_s), device=d),
-                                val=torch.as_tensor(np.ascontiguousarray(h.val[order]), device=d),
-                                perm=torch.as_tensor(lidx, device=d))
-        return self._sorted
 
     def tiles(self, n_cols):
         """Column-sorted copy + per-row tile pointers (dataset.RatingsCSR.tile_index) on the device,
@@ -278,13 +253,8 @@ class BatchGenerator(object):
             self.tlocal = self.src2.lens[rows].sum(axis=1) if nb else np.zeros(0, np.int64)
             self.lboff2_dev = _h2d(self._local_offsets(self.src2.lens, rows), r.device)
         # row-gather chunk tables (inputs from source 1; targets from source 1 in training, else source 2)
-        R = self.gather_ranges()
-        if R:
-            self.chunks1 = self._range_chunk_tables(self.src1, rows, R, r.device)
-            self.chunks2 = self.chunks1 if self.src2 is None else self._range_chunk_tables(self.src2, rows, R, r.device)
-        else:
-            self.chunks1 = self._chunk_tables(self.src1.lens, rows, r.device)
-            self.chunks2 = self.chunks1 if self.src2 is None else self._chunk_tables(self.src2.lens, rows, r.device)
+        self.chunks1 = self._chunk_tables(self.src1.lens, rows, r.device)
+        self.chunks2 = self.chunks1 if self.src2 is None else self._chunk_tables(self.src2.lens, rows, r.device)
         self.keep_dev = None
         self.keep_off = None
         if keep is not None:
@@ -327,64 +297,6 @@ class BatchGenerator(object):
         return dict(ch_row=t(rep % B), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase,
                     max_chunks=max_chunks)
 
-    def gather_ranges(self):
-        """column ranges of the range-ordered row gathers (0: list order); data_reader.gather_ranges overrides"""
-        R = getattr(self.r, "gather_ranges", None)
-        if R is None:
-            N = self.r.num_items
-            R = 0 if N < GATHER_RANGE_MIN_COLS else max(2, round(N / GATHER_RANGE_COLS))
-        return int(R)
-
-    def _range_chunk_tables(self, src, rows, R, dev):
-        """Range order (OcfGatherArgs perm / ch_slot): each batch row's entries in its column-sorted view, cut at
-        R column ranges and into chunks of <= GATHER_CHUNK entries (equal length within a (row, range)); the
-        chunk table in dispatch order -- range, then batch row -- with ch_row = batch row | slot << 12 and the
-        slots row-major (a row's partials contiguous: row_cptr, max_chunks as in _chunk_tables)"""
-        nb, B = rows.shape
-        if B > 4096:
-            raise ValueError("range-ordered gathers take batches of at most 4,096 rows")
-        sv = src.sorted_view()
-        N = int(self.r.num_items)
-        bounds = np.arange(R + 1, dtype=np.int64) * N // R
-        rr = rows.reshape(-1).astype(np.int64)
-        ok = rr >= 0
-        rp = src.host.row_ptr
-        q = np.where(ok, rr, 0)[:, None] * (1 << 32) + bounds[None, :]
-        pos = np.searchsorted(sv["key"], q) - rp[np.where(ok, rr, 0)][:, None]
-        pos = np.where(ok[:, None], pos, 0).astype(np.int64)               # [nb*B, R+1] local sorted positions
-        cnt = np.diff(pos, axis=1)                                           # [nb*B, R]
-        per_batch = cnt.sum() / max(nb, 1)
-        chunk = GATHER_CHUNK if per_batch >= GATHER_BIG else GATHER_CHUNK_SMALL
-        pieces = (cnt + chunk - 1) // chunk                                  # [nb*B, R]
-        # row-major slots: (batch row, range, piece) within each batch
-        pr = pieces.reshape(nb, B * R)
-        slot0 = (np.cumsum(pr, axis=1) - pr).reshape(nb, B, R)
-        row_n = pieces.reshape(nb, B, R).sum(axis=2)                         # chunks per batch row
-        row_cptr = np.zeros((nb, B + 1), dtype=np.int32)
-        np.cumsum(row_n, axis=1, out=row_cptr[:, 1:])
-        cbase = np.zeros(nb + 1, dtype=np.int64)
-        np.cumsum(row_cptr[:, -1], out=cbase[1:])
-        if nb and int(row_cptr[:, -1].max()) >= (1 << 19):
-            raise ValueError("range-ordered gathers: more than 2^19 chunks in a batch")
-        # dispatch order: batch, range, batch row, piece
-        pt = pieces.reshape(nb, B, R).transpose(0, 2, 1).reshape(-1)
-        bt = np.broadcast_to(np.arange(B, dtype=np.int64)[None, None, :], (nb, R, B)).reshape(-1)
-        st = slot0.transpose(0, 2, 1).reshape(-1)
-        p0 = pos[:, :-1].reshape(nb, B, R).transpose(0, 2, 1).reshape(-1)
-        ct = cnt.reshape(nb, B, R).transpose(0, 2, 1).reshape(-1)
-        tot = int(pt.sum())
-        first = np.repeat(np.cumsum(pt) - pt, pt)
-        k = np.arange(tot, dtype=np.int64) - first
-        P_ = np.repeat(pt, pt)
-        C_ = np.repeat(ct, pt)
-        j0 = np.repeat(p0, pt) + k * C_ // P_
-        j1 = np.repeat(p0, pt) + (k + 1) * C_ // P_
-        ch_row = np.repeat(bt, pt) | ((np.repeat(st, pt) + k) << 12)
-        t = lambda x: _h2d(np.ascontiguousarray(x, dtype=np.int32), dev)
-        max_chunks = row_n.max(axis=1) if nb else np.zeros(0, np.int64)
-        return dict(ch_row=t(ch_row), ch_j0=t(j0), ch_j1=t(j1), row_cptr=t(row_cptr), cbase=cbase,
-                    max_chunks=max_chunks, sorted=sv)
-
     def gather_tables(self, bi):
         """pointer sets for the row-gather kernels of batch bi: 'enc' (source-1 inputs) and 'dec'
         (the target CSR)"""
@@ -394,15 +306,12 @@ class BatchGenerator(object):
                                  ("dec", self.src1 if self.src2 is None else self.src2, self.chunks2,
                                   self.lboff1_dev if self.src2 is None else self.lboff2_dev)):
             c0 = int(ch["cbase"][bi])
-            sv = ch.get("sorted")
-            out[key] = dict(rows=self.rows_dev.data_ptr() + 4 * bi * B, rp=ptr(src.rp),
-                            col=ptr(sv["col"] if sv else src.col), val=ptr(sv["val"] if sv else src.val),
-                            lboff=lb.data_ptr() + 8 * bi * (B + 1),
+            out[key] = dict(rows=self.rows_dev.data_ptr() + 4 * bi * B, rp=ptr(src.rp), col=ptr(src.col),
+                            val=ptr(src.val), lboff=lb.data_ptr() + 8 * bi * (B + 1),
                             ch_row=ch["ch_row"].data_ptr() + 4 * c0, ch_j0=ch["ch_j0"].data_ptr() + 4 * c0,
                             ch_j1=ch["ch_j1"].data_ptr() + 4 * c0, n_chunks=int(ch["cbase"][bi + 1]) - c0,
                             row_cptr=ch["row_cptr"].data_ptr() + 4 * bi * (B + 1),
-                            max_chunks=int(ch["max_chunks"][bi]),
-                            perm=ptr(sv["perm"]) if sv else None, ch_slot=1 if sv else 0)
+                            max_chunks=int(ch["max_chunks"][bi]))
         if self.split == "train":      # train batches: inputs = targets -> the weight-gradient row lists
             out["row_lists"] = lambda n_cols, bi=bi: self.row_lists(bi, n_cols)
             # >= 2 entries per weight row on average: (nearly) every row is live, and on a weight of few row

@@ -818,7 +818,6 @@ class Engine:
         g = _lib.OcfGatherArgs()
         for k in ("rows", "rp", "col", "val", "lboff", "ch_row", "ch_j0", "ch_j1", "n_chunks"):
             setattr(g, k, tab[k])
-        g.perm, g.ch_slot = tab.get("perm"), tab.get("ch_slot", 0)    # range-ordered gathers (wide weights)
         Wt, wdt = self._wop(layer)
         g.W, g.w_dtype, g.ldw, g.w_blocked = ptr(Wt), wdt, Wt.shape[1], self._wblk(layer)
         g.H = n_cols

@@ -86,22 +86,20 @@ def sparse_batch(csr, rows, N, aux=-1.0):
 
 def run_parity(compute_dtype, opt_name, layers, act, steps=4, B=128, H=100, aux_type=None, causal=False,
                gather=True, sparse_dw=None, dropout=None, data=None, n_rows=None, lr=None, eval_rmse=True,
-               envelope=False, model_hook=None, sparse_oracle=False, eval_batches=None, l2=None, gather_ranges=None):
+               envelope=False, model_hook=None, sparse_oracle=False, eval_batches=None, l2=None):
     """`steps` training steps through fit_generator (one call per step, so the engine's Philox
     dropout masks engine.mask[l][:B, :H] can be read back after each and fed to the oracle as Keras'
     Dropout draw, model.py:72-73), then the oracle on the same rows (the generator exposes its epoch
     plan) and compute_full_RMSE of both models on identical test batches (train.py:225-255).
     sparse_oracle: the oracle's sparse-batch form (OmniOracle.loss_and_grads_sparse; one hidden
-    layer, no aux inputs) for the ML-20M / Netflix widths; eval_batches: test batches evaluated;
-    gather_ranges: the row gathers' range order (data_reader.gather_ranges; None: the reader's rule)."""
+    layer, no aux inputs) for the ML-20M / Netflix widths; eval_batches: test batches evaluated.
+    """
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     data = data if data is not None else dataset()
     N = data.num_cols
     np.random.seed(77)
     rd = data_reader(N, n_rows or data.train.n_rows, dataset=data, eval_mode="fixed_split")
-    if gather_ranges is not None:
-        rd.gather_ranges = gather_ranges
     om = omni_model(layers, H, N, B, dense_activation=act, use_causal_info=causal, compute_dtype=compute_dtype,
                     seed=11, dropout_probability=dropout, l2_weight_regulatization=l2)
     m = om.model

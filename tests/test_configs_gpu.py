@@ -65,22 +65,6 @@ def test_ml20m_bench_step(gpu):
     assert_low_precision(res, 2e-3)
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("cd,R", [("float32", 7), ("float16", 2)])
-def test_range_ordered_gathers(gpu, cd, R):
-    """the row gathers in range order (OcfGatherArgs perm / ch_slot: each batch row's column-sorted entries cut
-    at R column ranges, chunks dispatched range by range -- the Netflix-width default, data_reader
-    GATHER_RANGE_MIN_COLS) forced on at ML-1M size, train and eval batches, against the oracle: exact fp32 at
-    1e-5, f16 inside the envelope (R = 2: rows of up to ~1,000 entries, several chunks per (row, range))"""
-    res = run_parity(cd, "adagrad", 1, "sigmoid", steps=4, B=256, H=500, dropout=0.2, data=_synth("ml1m"),
-                     envelope=cd != "float32", sparse_oracle=True, eval_batches=4, gather_ranges=R)
-    if cd == "float32":
-        assert_fp32(res)
-    else:
-        assert_low_precision(res, 2e-3)
-
-
 def _h512_hook(om):
     e = om.engine
     assert e.use_sparse and e.sparse_ok and e.Hp[0] == 512, "row gathers at H = Hp = 512 expected"

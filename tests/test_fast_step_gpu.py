@@ -10,7 +10,7 @@ import pytest
 from parity import dataset
 
 
-def _run(fast, cd, opt, sparsity, ranges=None):
+def _run(fast, cd, opt, sparsity):
     import torch
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
@@ -18,7 +18,6 @@ def _run(fast, cd, opt, sparsity, ranges=None):
     data = dataset(rows=900, cols=700, nnz=40000)
     np.random.seed(21)
     rd = data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split", rng="numpy")
-    rd.gather_ranges = ranges
     om = omni_model(1, 500, data.num_cols, 128, dense_activation="sigmoid", use_causal_info=False,
                     dropout_probability=0.2, compute_dtype=cd, seed=3)
     m = om.model
@@ -44,13 +43,11 @@ def _run(fast, cd, opt, sparsity, ranges=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cd,opt,sparsity,ranges", [("float16", "adagrad", [1.0, 1.0], None),
-                                                    ("float32", "adagrad", [0.3, 0.7], None),
-                                                    ("bfloat16", "adam", [0.5, 0.9], None),
-                                                    ("float16", "adagrad", [0.5, 0.9], 5)])
-def test_fast_step_bit_identical(gpu, cd, opt, sparsity, ranges):
-    h_f, w_f, s_f, sh_f, ready, n = _run(True, cd, opt, sparsity, ranges)
-    h_g, w_g, s_g, sh_g, ready_g, n_g = _run(False, cd, opt, sparsity, ranges)
+@pytest.mark.parametrize("cd,opt,sparsity", [("float16", "adagrad", [1.0, 1.0]), ("float32", "adagrad", [0.3, 0.7]),
+                                             ("bfloat16", "adam", [0.5, 0.9])])
+def test_fast_step_bit_identical(gpu, cd, opt, sparsity):
+    h_f, w_f, s_f, sh_f, ready, n = _run(True, cd, opt, sparsity)
+    h_g, w_g, s_g, sh_g, ready_g, n_g = _run(False, cd, opt, sparsity)
     assert ready and not ready_g and n == n_g > 0
     assert h_f == h_g and all(np.isfinite(v).all() and v[0] > 0 for h in h_f for v in h.values())
     for a, b in zip(w_f + s_f + sh_f, w_g + s_g + sh_g):
