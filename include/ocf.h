@@ -507,8 +507,9 @@ int ocf_row_lists(const OcfRowListArgs* args, void* stream);
  * a nonzero gradient: an Adagrad l2 = 0 update at g = 0 is the identity, so the row skip stays exact).
  * B <= 4,096; a batch's entries < 2^31.  n_rg (0 or 1: one; at most min(64, B)): row groups per batch --
  * the count / fill walks split each batch's rows over n_rg workgroups (more parallelism when few batches are
- * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols + 1 + 2 * (entries /
- * 1025 + 1) ints (counts per row group, then the queue of lists over 1,024 entries).  n_cols % 128 == 0.
+ * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols + n_sel * (n_cols / 4096
+ * + 1) + 1 + 2 * (entries / 1025 + 1) ints (counts per row group, per-4,096-column block totals, then the queue of
+ * lists over 1,024 entries).  n_cols % 128 == 0.
  * Extension (no reference counterpart): the data_reader.py:326-419 batch loop's structure, per epoch. */
 typedef struct OcfEpochRowListArgs {
   int n_sel; int B; int n_cols;

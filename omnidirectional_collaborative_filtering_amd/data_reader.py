@@ -352,7 +352,8 @@ class BatchGenerator(object):
         # tail of an epoch) would leave most CUs idle with one workgroup per (batch, column block)
         n_rg = int(min(8, max(1, -(-ROWLIST_RG_WORK // max(len(sel), 1)))))
         # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
-        need = dict(cnt=(n_rg * len(sel) * n_cols + 1 + 2 * (E // 1025 + 1), torch.int32),
+        need = dict(cnt=(n_rg * len(sel) * n_cols + len(sel) * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1),
+                         torch.int32),
                     row_ptr=(len(sel) * (n_cols + 1), torch.int32), row_ent=(2 * max(E, 1), torch.int32),
                     live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
                     xval=(max(E, 1), torch.float32), tflag=(max(E, 1), torch.uint8))
