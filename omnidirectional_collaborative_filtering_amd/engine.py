@@ -46,6 +46,10 @@ TILE = 128
 # (skewed ML-20M-shaped batch, rows up to ~170 chunks: fused 128 us vs 135 us for the two gathers;
 # a Netflix-sized row of 900 chunks would re-read 1.6 GB of partials)
 FUSE_MAX_CHUNKS = 256
+# ... and past this many chunks per batch row on average: every decoder chunk re-reads all of its row's encoder
+# partials (O(chunks^2) per row).  Netflix (~22 chunks per row): 2.029 -> 1.997 ms/step with the separate launch
+# (profiles/r05_cfg/nf_base.jsonl); ML-20M (~3): the fused form
+FUSE_MEAN_CHUNKS = 8
 DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
           "bfloat16": (_lib.DT_BF16, torch.bfloat16)}
 DTYPE_ALIASES = {"f32": "float32", "fp32": "float32", "f16": "float16", "fp16": "float16", "half": "float16",
@@ -840,7 +844,8 @@ class Engine:
             g.xval = xv if isinstance(xv, int) else ptr(xv)
             call("ocf_gather_encoder", g, cur_stream())
             if (self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue
-                    and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS):
+                    and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS
+                    and tab["n_chunks"] <= FUSE_MEAN_CHUNKS * self.B):
                 # the decoder gather applies bias / activation / dropout to these partials itself
                 self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id)
                 return
