@@ -40,7 +40,7 @@ def phase_of(name, seen):
     if "EpiSlab" in name:
         k = seen["slab"] = seen.get("slab", -1) + 1
         return ("enc_gemm", "dec_bwd_gemm")[k % 2]
-    if "rowpipe_pair" in name:            # both updates in one launch (ocf_gemm_pair)
+    if "rowpipe_pair" in name or "rowdual" in name:   # both updates in one launch (ocf_gemm_pair)
         return "dW_pair"
     if "EpiOptim" in name or "optim_rowpipe" in name:
         k = seen["optim"] = seen.get("optim", -1) + 1
