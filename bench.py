@@ -760,6 +760,15 @@ def main():
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))
                      if epoch_lists else "per step (ocf_row_lists)" if eng.sparse_dw else "n/a",
     }
+    # this rank's device memory (weights, slots, shadows, epoch tables, scratch): the per-rank footprint of a layout
+    line["rank_memory"] = {"peak_allocated_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
+                           "reserved_gb": round(torch.cuda.memory_reserved(dev) / 1e9, 3)}
+    if dpo is not None:
+        sync = getattr(dpo, "sync", None)
+        line["dp_layout"] = {"mode": args.dp_mode, "grad_dtype": args.dp_grad_dtype,
+                             "zero1_shards": [[int(p.numel()), int(p.numel()) // world] for p in sync.params]
+                             if sync is not None else None,
+                             "grad_bytes_per_step": int(sum(g.numel() * g.element_size() for g in dpo.views))}
     if same_batch is not None:
         # weak scaling grows the global batch with the ranks; the same global batch on ONE GPU is the reference
         # point for the speed-up, not the B = 256 line
