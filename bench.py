@@ -93,9 +93,6 @@ def parse():
     ap.add_argument("--reduce-in-decoder", type=int, default=-1,
                     help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
                          "engine default (small weights)")
-    ap.add_argument("--rowlist-split", type=int, default=1,
-                    help="row-list builds: the first batch alone, the rest on a side stream overlapping the first "
-                         "step (0: one build on the main stream)")
     ap.add_argument("--fold-reduce", type=int, default=1,
                     help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
                          "ocf_rows_reduce launch)")
@@ -498,12 +495,10 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    from omnidirectional_collaborative_filtering_amd import data_reader as _dr
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
     from omnidirectional_collaborative_filtering_amd.model import omni_model
 
-    _dr.ROWLIST_SPLIT = bool(args.rowlist_split)
     t0 = time.time()
     data_full = synthetic_fixed_split(args.config, seed=0, skew=args.skew)
     N = data_full.num_cols

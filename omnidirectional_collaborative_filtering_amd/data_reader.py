@@ -43,7 +43,6 @@ GATHER_BIG = 100_000
 ROWLIST_MAX_BATCHES = 4096      # batches per ocf_epoch_row_lists build (the library takes up to 65,535)
 ROWLIST_MAX_ENTRIES = 4096      # entries per column list of one batch (ocf_epoch_row_lists' LDS sort)
 ROWLIST_RG_WORK = 160           # (batches x row groups) per row-list build: at least this many, row groups <= 8
-ROWLIST_SPLIT = True            # build a window's first batch alone and the rest on a side stream (prepare_row_lists)
 ROWS_DENSE_MAX_COLS = 170 * 128  # the row-stream kernel's small regime (ocf_gemm.hip rows_small_waves: 170 tiles)
 
 
@@ -66,17 +65,6 @@ def _rng_stream(dev):
     if key not in _RNG_STREAMS:
         _RNG_STREAMS[key] = torch.cuda.Stream(device=key)
     return _RNG_STREAMS[key]
-
-
-_AUX_STREAMS = {}
-
-
-def _aux_stream(dev):
-    """one side stream per device for the row-list builds that overlap the first step of a window"""
-    key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
-    if key not in _AUX_STREAMS:
-        _AUX_STREAMS[key] = torch.cuda.Stream(device=key)
-    return _AUX_STREAMS[key]
 
 
 class _DeviceCSR:
@@ -347,8 +335,7 @@ class BatchGenerator(object):
         if batches is None:
             # under data parallelism a rank only trains on its own batches (parallel.shard_batches)
             batches = shard_batches(nb, *self.dp_shard) if self.dp_shard else np.arange(nb)
-        order = np.asarray(batches, dtype=np.int64)
-        sel = np.unique(order)
+        sel = np.unique(np.asarray(batches, dtype=np.int64))
         if len(sel) and (sel[0] < 0 or sel[-1] >= nb):
             raise ValueError("batch index out of range")
         # one build holds at most ROWLIST_MAX_BATCHES batches and ~1 GiB of row pointers (the library's
@@ -356,34 +343,18 @@ class BatchGenerator(object):
         cap = int(min(ROWLIST_MAX_BATCHES, max(1, (1 << 28) // (n_cols + 1))))
         if len(sel) > cap:
             sel = sel[:cap]
-        # slot 0 = the batch used first (batches are given in use order); the others follow in index order
-        first = int(order[0]) if len(order) and int(order[0]) in set(sel.tolist()) else (int(sel[0]) if len(sel) else 0)
-        if len(sel):
-            sel = np.concatenate([[first], sel[sel != first]])
         if self.src1.dup is not None and len(sel):
             self._check_list_lengths(sel)
-        old = getattr(self, "_rl", None)
-        if old is not None and old.get("pending") is not None:
-            # the previous window's side build may still be running: its tables and staged inputs are reused
-            torch.cuda.current_stream().wait_event(old["pending"])
-            old["pending"] = None
         dev = self.rows_dev.device
         ebase = np.zeros(len(sel) + 1, dtype=np.int64)
         np.cumsum(self.nnz1[sel], out=ebase[1:])
         E = int(ebase[-1])
-        # Two builds when there are several batches: slot 0 (the first step's batch) on the current stream, the
-        # rest on a side stream that overlaps the first step; the streams' consumers of slots >= 1 wait for its
-        # event first (row_lists / step_fields).  The build is a chain of latency-bound launches (~0.25 ms for 20
-        # ML-20M batches) that would otherwise run with the GPU idle at the start of a window.
-        split = torch.device(dev).type == "cuda" and len(sel) >= 2 and ROWLIST_SPLIT
-        parts = [(0, 1), (1, len(sel))] if split else [(0, len(sel))]
         # row groups per batch for the count / fill walks: a build of few batches (the bench's timed window, the
         # tail of an epoch) would leave most CUs idle with one workgroup per (batch, column block)
-        n_rgs = [int(min(8, max(1, -(-ROWLIST_RG_WORK // max(q - p, 1))))) for p, q in parts]
-        cnt_n = [rg * (q - p) * n_cols + (q - p) * (n_cols // 4096 + 1) + 1 + 2 * (int(ebase[q] - ebase[p]) // 1025 + 1)
-                 for rg, (p, q) in zip(n_rgs, parts)]
+        n_rg = int(min(8, max(1, -(-ROWLIST_RG_WORK // max(len(sel), 1)))))
         # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
-        need = dict(cnt=(sum(cnt_n), torch.int32),
+        need = dict(cnt=(n_rg * len(sel) * n_cols + len(sel) * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1),
+                         torch.int32),
                     row_ptr=(len(sel) * (n_cols + 1), torch.int32), row_ent=(2 * max(E, 1), torch.int32),
                     live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
                     xval=(max(E, 1), torch.float32), tflag=(max(E, 1), torch.uint8))
@@ -392,62 +363,32 @@ class BatchGenerator(object):
             if k not in bufs or bufs[k].numel() < n:
                 bufs[k] = torch.empty(n, dtype=dt, device=dev)
         self._rl_bufs = bufs
-        staged = self._stage([x for p, q in parts for x in (ebase[p:q + 1], sel[p:q].astype(np.int32))], dev)
+        p_ebase, p_sel = self._stage([ebase, sel.astype(np.int32)], dev)
         keep = dict(row_ptr=bufs["row_ptr"], row_ent=bufs["row_ent"], live=bufs["live"])
+        a = _lib.OcfEpochRowListArgs()
+        a.n_sel, a.B, a.n_cols, a.n_rg = len(sel), self.B, n_cols, n_rg
+        a.rows, a.rp, a.col, a.lboff = ptr(self.rows_dev), ptr(self.src1.rp), ptr(self.src1.col), ptr(self.lboff1_dev)
+        a.sel, a.ebase = p_sel, p_ebase
+        a.cnt, a.row_ptr, a.row_ent, a.live = ptr(bufs["cnt"]), ptr(bufs["row_ptr"]), ptr(bufs["row_ent"]), \
+            ptr(bufs["live"])
+        _lib.call("ocf_epoch_row_lists", a, cur_stream())
+        # ... and the batches' per-entry scatter outputs (live input value, live-target flag): the per-step
+        # ocf_scatter_batch has nothing left to do for them
         base = self.scatter_args(0) if nb else _lib.OcfScatterArgs()
-        if self.keep_dev is not None and getattr(self, "_keep_off_dev", None) is None:   # (per epoch plan: once)
-            self._keep_off_dev = _h2d(np.ascontiguousarray(self.keep_off, dtype=np.int64), dev)
-        main = cur_stream() if torch.device(dev).type == "cuda" else None
-        ready = torch.cuda.Event() if split else None
-        if split:
-            ready.record()                    # the side build starts after everything queued before it
-        cnt_off = 0
-        pending = None
-        for k, ((p, q), rg) in enumerate(zip(parts, n_rgs)):
-            p_ebase, p_sel = staged[2 * k], staged[2 * k + 1]
-            side = split and k == 1
-            a = _lib.OcfEpochRowListArgs()
-            a.n_sel, a.B, a.n_cols, a.n_rg = q - p, self.B, n_cols, rg
-            a.rows, a.rp, a.col, a.lboff = ptr(self.rows_dev), ptr(self.src1.rp), ptr(self.src1.col), \
-                ptr(self.lboff1_dev)
-            a.sel, a.ebase = p_sel, p_ebase
-            a.cnt = bufs["cnt"].data_ptr() + 4 * cnt_off
-            a.row_ptr = bufs["row_ptr"].data_ptr() + 4 * p * (n_cols + 1)
-            a.row_ent = bufs["row_ent"].data_ptr()                 # (ebase holds the window's absolute offsets)
-            a.live = bufs["live"].data_ptr() + p * (n_cols // 128) * _lib.LIVE_REC
-            cnt_off += cnt_n[k]
-            # ... and the batches' per-entry scatter outputs (live input value, live-target flag): the per-step
-            # ocf_scatter_batch has nothing left to do for them
-            es = _lib.OcfEpochScatterArgs()
-            es.keep_off = ptr(getattr(self, "_keep_off_dev", None)) if self.keep_dev is not None else None
-            es.n_sel, es.sel, es.ebase = q - p, p_sel, p_ebase
-            es.max_e = int(self.nnz1[sel[p:q]].max()) if q > p else 0
-            es.stream_mul = 2
-            es.xval, es.tflag = ptr(bufs["xval"]), ptr(bufs["tflag"])
-            if side:
-                st = _aux_stream(dev)
-                st.wait_event(ready)
-                with torch.cuda.stream(st):
-                    _lib.call("ocf_epoch_row_lists", a, cur_stream())
-                    if q > p:
-                        _lib.call("ocf_epoch_scatter", base, es, cur_stream())
-                    pending = torch.cuda.Event()
-                    pending.record()
-                for t in bufs.values():
-                    t.record_stream(st)
-            else:
-                _lib.call("ocf_epoch_row_lists", a, main)
-                if q > p:
-                    _lib.call("ocf_epoch_scatter", base, es, main)
+        es = _lib.OcfEpochScatterArgs()
+        if self.keep_dev is not None:
+            if getattr(self, "_keep_off_dev", None) is None:     # (per epoch plan: uploaded once)
+                self._keep_off_dev = _h2d(np.ascontiguousarray(self.keep_off, dtype=np.int64), dev)
+            es.keep_off = ptr(self._keep_off_dev)
+        es.n_sel, es.sel, es.ebase = len(sel), p_sel, p_ebase
+        es.max_e = int(self.nnz1[sel].max()) if len(sel) else 0
+        es.stream_mul = 2
+        es.xval, es.tflag = ptr(bufs["xval"]), ptr(bufs["tflag"])
+        if len(sel):
+            _lib.call("ocf_epoch_scatter", base, es, cur_stream())
         keep.update(xval=bufs["xval"], tflag=bufs["tflag"])
-        keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase, pending=pending)
+        keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
         self._rl = keep
-
-    def _wait_lists(self, rl, s):
-        """slots >= 1 of a split build: the current stream waits (on the device) for the side build once"""
-        if s and rl.get("pending") is not None:
-            torch.cuda.current_stream().wait_event(rl["pending"])
-            rl["pending"] = None
 
     def _stage(self, parts, dev):
         """host arrays to the device in ONE copy through a persistent pinned staging buffer (8-byte aligned
@@ -502,7 +443,6 @@ class BatchGenerator(object):
             self.prepare_row_lists(n_cols, [b for b in want if b >= bi] or [bi])
             rl = self._rl
         s = rl["slot"][bi]
-        self._wait_lists(rl, s)
         e0 = int(rl["ebase_host"][s])
         return dict(row_ptr=rl["row_ptr"].data_ptr() + 4 * s * (n_cols + 1),
                     row_ent=rl["row_ent"].data_ptr() + 8 * e0,
@@ -520,7 +460,6 @@ class BatchGenerator(object):
         s = rl["slot"].get(bi)
         if s is None:
             return None
-        self._wait_lists(rl, s)
         ff = rl.get("fields")
         if ff is None:
             B, ch = self.B, self.chunks1
