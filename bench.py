@@ -93,6 +93,10 @@ def parse():
     ap.add_argument("--reduce-in-decoder", type=int, default=-1,
                     help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
                          "engine default (small weights)")
+    ap.add_argument("--rowlist-rg-work", type=int, default=0,
+                    help="row-list builds: (batches x row groups) to aim for (0: data_reader.ROWLIST_RG_WORK)")
+    ap.add_argument("--fuse-enc-dec", type=int, default=1,
+                    help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches)")
     ap.add_argument("--fold-reduce", type=int, default=1,
                     help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
                          "ocf_rows_reduce launch)")
@@ -495,10 +499,13 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    from omnidirectional_collaborative_filtering_amd import data_reader as _dr
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
     from omnidirectional_collaborative_filtering_amd.model import omni_model
 
+    if args.rowlist_rg_work > 0:
+        _dr.ROWLIST_RG_WORK = args.rowlist_rg_work
     t0 = time.time()
     data_full = synthetic_fixed_split(args.config, seed=0, skew=args.skew)
     N = data_full.num_cols
@@ -535,6 +542,7 @@ def main():
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
     eng.fold_reduce = bool(args.fold_reduce)
+    eng.fuse_enc_dec = bool(args.fuse_enc_dec)
     if args.reduce_in_decoder >= 0:
         eng.reduce_in_decoder = bool(args.reduce_in_decoder)
     eng.split_dw_streams = bool(args.split_dw)

@@ -172,6 +172,13 @@ typedef struct OcfGatherArgs {
 
 int ocf_gather_encoder(const OcfGatherArgs* args, void* stream);
 int ocf_gather_decoder(const OcfGatherArgs* args, void* stream);
+/* ocf_gather_encdec -- ocf_gather_encoder(enc) then ocf_gather_decoder(dec) as ONE launch: a decoder chunk starts
+ * as soon as its row's encoder chunks are done (per-row arrival counters) instead of after the whole encoder.
+ * Requires: dec.enc_part == enc.part, dec.enc_cptr (the encoder's row_cptr), the decoder's folded row reduction
+ * (dec.jr + dec.row_arrive: its last chunk per row resets the counter), the same chunk table in both (ch_row /
+ * ch_j0 / ch_j1 / n_chunks: a train batch, inputs = targets) and the same H.  enc_arrive: device uint32 [Bp],
+ * zero before the first call, left zero.  Same results as the two calls (the same sums in the same order). */
+int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* dec, uint32_t* enc_arrive, void* stream);
 
 enum { OCF_REDUCE_RAW = 0, OCF_REDUCE_BIAS_ACT = 1, OCF_REDUCE_GRAD_ACT = 2 };
 
@@ -332,6 +339,7 @@ int ocf_gemm_pair(const OcfGemmArgs* a, const OcfGemmArgs* b, OcfPairSync* sync,
  * next entry point through its status and ocf_last_error()) */
 #define OCF_ASYNC_PAIR_WAIT 1
 #define OCF_ASYNC_MLP_BARRIER 2   /* ocf_mlp_step: a grid barrier gave up (workgroups not all resident) */
+#define OCF_ASYNC_ENC_WAIT 3      /* ocf_gather_encdec: a decoder chunk gave up waiting for its row's encoder chunks */
 
 /*
  * ocf_train_step_rows -- one whole single-GPU training step of a one-hidden-layer model on a sparse
@@ -361,6 +369,9 @@ typedef struct OcfRowStepArgs {
   /* (nullable) ocf_gemm_pair's hand-off counter: dW_out and dW_in as one launch (events 4 and 7 bracket
    * it); its count advances with every pair launch */
   OcfPairSync* pair_sync;
+  /* (nullable) the encoder and the decoder as one launch (ocf_gather_encdec with this counter; needs jr_on = 2):
+   * events 0 / 1 then bracket nothing, 2 / 3 the fused launch */
+  uint32_t* enc_arrive;
 } OcfRowStepArgs;
 int ocf_train_step_rows(const OcfRowStepArgs* args, void* stream);
 

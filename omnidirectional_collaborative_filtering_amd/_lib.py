@@ -130,7 +130,7 @@ ASYNC_PAIR_WAIT = 1            # ocf.h OCF_ASYNC_PAIR_WAIT
 
 class OcfRowStepArgs(ctypes.Structure):
     _fields_ = [("enc", OcfGatherArgs), ("dec", OcfGatherArgs), ("dw_out", OcfGemmArgs), ("dw_in", OcfGemmArgs),
-                ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8), ("pair_sync", P)]
+                ("jr", OcfRowsReduceArgs), ("jr_on", I32), ("ev", P * 8), ("pair_sync", P), ("enc_arrive", P)]
 
 
 class OcfBiasActArgs(ctypes.Structure):
@@ -239,6 +239,7 @@ SIGNATURES = {
     "ocf_sumsq": (I32, [P, I64, F32, P, P, P]),
     "ocf_gather_encoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
     "ocf_gather_decoder": (I32, [ctypes.POINTER(OcfGatherArgs), P]),
+    "ocf_gather_encdec": (I32, [ctypes.POINTER(OcfGatherArgs), ctypes.POINTER(OcfGatherArgs), P, P]),
     "ocf_rows_reduce": (I32, [ctypes.POINTER(OcfRowsReduceArgs), P]),
     "ocf_colsum": (I32, [P, I32, I64, I32, I32, F32, P, P]),
     "ocf_sparse_tiles": (I32, [ctypes.POINTER(OcfTileBucketArgs), P]),

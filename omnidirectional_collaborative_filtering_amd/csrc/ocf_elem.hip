@@ -23,6 +23,9 @@ const char* async_error_text(uint32_t code) {
       return "ocf_gemm_pair: an input-layer workgroup gave up waiting for the row reduction (sync word behind its "
              "target: the word was written by someone else, or the count passed does not match it) and skipped "
              "its update; the weights of that launch are not a valid step";
+    case OCF_ASYNC_ENC_WAIT:
+      return "ocf_gather_encdec: a decoder chunk gave up waiting for its row's encoder chunks; that step's "
+             "decoder outputs are not valid";
     case OCF_ASYNC_MLP_BARRIER:
       return "ocf_mlp_step: a grid barrier gave up waiting (not every workgroup was resident); that step's "
              "weights are not valid";

@@ -284,6 +284,10 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     if (previous) *previous = g_pair_wait_polls;
     OCF_CHECK(value > 0, "ocf_set_tuning: pair_wait_polls > 0");
     g_pair_wait_polls = value;
+  } else if (k == "encdec_max_polls") {   // ocf_gather_encdec's bounded wait (tests shorten it)
+    if (previous) *previous = g_encdec_max_polls;
+    OCF_CHECK(value > 0, "ocf_set_tuning: encdec_max_polls > 0");
+    g_encdec_max_polls = value;
   } else if (k == "mlp_max_polls") {      // ocf_mlp_step's bounded barrier wait (tests: < 0 injects a give-up)
     if (previous) *previous = g_mlp_max_polls;
     OCF_CHECK(value != 0, "ocf_set_tuning: mlp_max_polls != 0");
@@ -370,13 +374,16 @@ extern "C" int ocf_train_step_rows(const OcfRowStepArgs* a, void* stream) {
   auto ev = [&](int k) {
     if (a->ev[k]) OCF_HIP(hipEventRecord((hipEvent_t)a->ev[k], s));
   };
-  ev(0);
-  OCF_CHECK(ocf_gather_encoder(&a->enc, stream) == 0, ocf_last_error());
-  ev(1);
-  ev(2);
   OcfGatherArgs d = a->dec;
   d.jr = a->jr_on == 2 ? &a->jr : nullptr;      // the row reduction in the decoder (d.row_arrive) ...
-  OCF_CHECK(ocf_gather_decoder(&d, stream) == 0, ocf_last_error());
+  ev(0);
+  if (!a->enc_arrive) OCF_CHECK(ocf_gather_encoder(&a->enc, stream) == 0, ocf_last_error());
+  ev(1);
+  ev(2);
+  if (a->enc_arrive)                            // the encoder and the decoder as one launch
+    OCF_CHECK(ocf_gather_encdec(&a->enc, &d, a->enc_arrive, stream) == 0, ocf_last_error());
+  else
+    OCF_CHECK(ocf_gather_decoder(&d, stream) == 0, ocf_last_error());
   ev(3);
   OcfGemmArgs o = a->dw_out;
   o.jr = a->jr_on == 1 ? &a->jr : nullptr;      // ... or as jobs of the dW_out launch

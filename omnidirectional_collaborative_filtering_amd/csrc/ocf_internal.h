@@ -15,6 +15,7 @@ void set_error(const std::string& msg);
 uint32_t* async_error_word();        // device-visible address of the word (allocated on first use)
 void check_async_errors();
 extern int g_mlp_max_polls;          // ocf_mlp_step's barrier wait (ocf_set_tuning "mlp_max_polls")
+extern int g_encdec_max_polls;       // ocf_gather_encdec's wait (ocf_set_tuning "encdec_max_polls")
 }  // namespace ocf
 
 #define OCF_TRY_BEGIN try { ocf::check_async_errors();

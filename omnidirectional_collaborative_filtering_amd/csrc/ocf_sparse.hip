@@ -144,8 +144,12 @@ __device__ __forceinline__ void reduce_groups(const float (&acc)[V], float* red,
 // (own) and stats total (own_st, threads 0..2) are the row's, added to 0 as the chunk loop would.
 __device__ __forceinline__ void dec_row_tail(const OcfGatherArgs& a, const OcfRowsReduceArgs& r, int b,
                                              const float* a_sh, const uint8_t* mk_sh, bool stash, bool solo,
-                                             const float* own, float own_st) {
+                                             const float* own, float own_st, uint32_t* enc_arrive) {
   __shared__ int last_sh;
+  // (fused encoder -> decoder launch) every decoder chunk of the row has passed its wait once the row's last one
+  // gets here: the encoder counter goes back to zero for the next launch
+  if (enc_arrive && threadIdx.x == 0 && solo)
+    __hip_atomic_store(&enc_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!solo) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's write-through stores have landed
     __syncthreads();
@@ -154,6 +158,7 @@ __device__ __forceinline__ void dec_row_tail(const OcfGatherArgs& a, const OcfRo
       const uint32_t old = __hip_atomic_fetch_add(&a.row_arrive[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = old + 1 == nch;
       if (last) __hip_atomic_store(&a.row_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (last && enc_arrive) __hip_atomic_store(&enc_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last_sh = last ? 1 : 0;
     }
     __syncthreads();
@@ -218,13 +223,13 @@ __device__ __forceinline__ void dec_zero_rows(const OcfRowsReduceArgs& r) {
 // A group of G lanes owns one entry at a time (RG_U entries in flight); lane l holds pieces
 // l, l+G, ... (PPL of them) of the weight row, so a group's load instruction reads G*16
 // contiguous bytes.
+// chunk c of the encoder.  wt (the fused encoder -> decoder launch, gather_encdec_kernel): the partial is stored
+// write-through and the chunk counts itself in enc_arrive[b] once its stores have landed
 template <typename WT, int G, int PPL>
-__global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArgs a) {
+__device__ __forceinline__ void encoder_chunk(const OcfGatherArgs& a, const int c, float* red, uint32_t* enc_arrive) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
-  __shared__ float red[NG * RG_MAX_H];
-  const int c = blockIdx.x;
   const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
@@ -268,19 +273,33 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
         for (int k = 0; k < E; ++k) acc[i * E + k] += xc[u] * f[k];
       }
   }
-  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l);
+  reduce_groups<G, V, E, PPL>(acc, red, a.part, c, a.H, grp, l, enc_arrive != nullptr);
+  if (enc_arrive) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's write-through stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&enc_arrive[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
-// (162 VGPRs, 3 waves per SIMD; capped at 128 by amdgpu_waves_per_eu(4) it spills 144 B per lane and the ML-20M
-// step went 0.388 -> 0.523 ms)
+template <typename WT, int G, int PPL>
+__global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArgs a) {
+  __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
+  encoder_chunk<WT, G, PPL>(a, blockIdx.x, red, nullptr);
+}
+
+// chunk c of the decoder.  enc_arrive (the fused encoder -> decoder launch): before its hidden epilogue the chunk
+// waits until every encoder chunk of its row has counted itself (bounded: OCF_ASYNC_ENC_WAIT, then the chunk
+// stores nothing) and reads their write-through partials with L1-bypassing loads.  Deadlock-free: the encoder
+// chunks are the launch's first workgroups and workgroups dispatch in index order, so a waiting decoder chunk's
+// producers are resident or done.
 template <typename WT, typename HT, int G, int PPL>
-__global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a, OcfRowsReduceArgs jr) {
+__device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfRowsReduceArgs& jr, const int c,
+                                              const bool first_wg, float* red, uint32_t* enc_arrive, uint32_t* err,
+                                              int max_polls) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
-  __shared__ float red[NG * RG_MAX_H];
   __shared__ float st[NG][3];
-  const int c = blockIdx.x;
   const int b = a.ch_row[c], j0 = a.ch_j0[c], j1 = a.ch_j1[c];
   const int grp = threadIdx.x / G, l = threadIdx.x % G;
   const int r = a.rows[b];
@@ -288,10 +307,10 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
   const int64_t lb = a.lboff[b];
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
-  if (a.zero_word && c == 0 && threadIdx.x == 0)
+  if (a.zero_word && first_wg && threadIdx.x == 0)
     __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool fold = a.row_arrive != nullptr;
-  if (fold && c == 0) dec_zero_rows(jr);
+  if (fold && first_wg) dec_zero_rows(jr);
   __shared__ float a_sh[RG_MAX_H];             // (fold) the row's activation / dropout mask from the epilogue
   __shared__ uint8_t mk_sh[RG_MAX_H];
   float hv[V];
@@ -323,13 +342,30 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
     p.h_out = first ? const_cast<void*>(a.h) : nullptr; p.h_dtype = a.h_dtype; p.ld = a.H;
     p.m_real = a.m_real; p.n_real = a.n_real;
     const int e0 = a.enc_cptr[b], e1 = a.enc_cptr[b + 1];
+    if (enc_arrive) {                 // the fused launch: this row's encoder chunks done (see above)
+      __shared__ int ok_sh;
+      if (threadIdx.x == 0) {
+        const uint32_t want = (uint32_t)(e1 - e0);
+        bool ok = __hip_atomic_load(&enc_arrive[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+        for (int it = 0; !ok && it < max_polls; ++it) {
+          __builtin_amdgcn_s_sleep(1);
+          ok = __hip_atomic_load(&enc_arrive[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+        }
+        if (!ok) __hip_atomic_store(err, (uint32_t)OCF_ASYNC_ENC_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok_sh = ok ? 1 : 0;
+      }
+      __syncthreads();
+      if (!ok_sh) return;
+    }
     for (int x = threadIdx.x; x < a.H; x += RG_THREADS) {
       // the chunk partials of 4 chunks in flight together, added in chunk order (the same sums)
       float v = 0.f;
       for (int c = e0; c < e1; c += 4) {
         float q[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) q[k] = c + k < e1 ? a.enc_part[(int64_t)(c + k) * a.H + x] : 0.f;
+        for (int k = 0; k < 4; ++k)
+          q[k] = c + k < e1 ? (enc_arrive ? ld_sc1(a.enc_part, (int64_t)(c + k) * a.H + x)
+                                          : a.enc_part[(int64_t)(c + k) * a.H + x]) : 0.f;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (c + k < e1) v += q[k];
@@ -435,7 +471,33 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
       a.chunk_stats[(int64_t)c * 4 + threadIdx.x] = v;
     }
   }
-  if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr, solo, own, own_st);
+  if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr, solo, own, own_st, enc_arrive);
+}
+
+// (162 VGPRs, 3 waves per SIMD; capped at 128 by amdgpu_waves_per_eu(4) it spills 144 B per lane and the ML-20M
+// step went 0.388 -> 0.523 ms)
+template <typename WT, typename HT, int G, int PPL>
+__global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a, OcfRowsReduceArgs jr) {
+  __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
+  decoder_chunk<WT, HT, G, PPL>(a, jr, blockIdx.x, blockIdx.x == 0, red, nullptr, nullptr, 0);
+}
+
+// The encoder and the decoder as ONE launch (ocf_gather_encdec): workgroups [0, e.n_chunks) are the encoder's
+// chunks, the rest the decoder's; a decoder chunk starts its row as soon as that row's encoder chunks are done
+// (per-row arrival counters enc_arrive, reset by the row's last decoder chunk) instead of after the whole encoder
+// launch.  Needs the decoder's folded row reduction (its last chunk per row resets the counter) and the same
+// chunk table for both (train batches: inputs = targets).
+struct EncDecSync {
+  uint32_t* enc_arrive; uint32_t* err; int max_polls;
+};
+template <typename WT, typename HT, int G, int PPL>
+__global__ void __launch_bounds__(RG_THREADS) gather_encdec_kernel(OcfGatherArgs e, OcfGatherArgs d,
+                                                                   OcfRowsReduceArgs jr, EncDecSync sy) {
+  __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
+  const int bx = blockIdx.x;
+  if (bx < e.n_chunks) encoder_chunk<WT, G, PPL>(e, bx, red, sy.enc_arrive);
+  else decoder_chunk<WT, HT, G, PPL>(d, jr, bx - e.n_chunks, bx == e.n_chunks, red, sy.enc_arrive, sy.err,
+                                     sy.max_polls);
 }
 
 // per batch row: fixed-order sum of its chunk partials, then the layer epilogue
@@ -526,6 +588,24 @@ template <typename WT, typename HT> struct Dec {
   };
 };
 
+template <typename WT, typename HT>
+void launch_encdec(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& d, const EncDecSync& sy, hipStream_t s) {
+  OcfRowsReduceArgs r = *d.jr;
+  const dim3 grid(e.n_chunks + d.n_chunks), blk(RG_THREADS);
+#define OCF_ED(GG, PP) hipLaunchKernelGGL((gather_encdec_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r, sy)
+  if (G == 64 && ppl == 1) OCF_ED(64, 1);
+  else if (G == 64 && ppl == 2) OCF_ED(64, 2);
+  else if (G == 32 && ppl == 1) OCF_ED(32, 1);
+  else if (G == 32 && ppl == 2) OCF_ED(32, 2);
+  else if (G == 16 && ppl == 4) OCF_ED(16, 4);
+  else if (G == 32 && ppl == 4) OCF_ED(32, 4);
+  else if (G == 32 && ppl == 3) OCF_ED(32, 3);
+  else if (G == 16 && ppl == 1) OCF_ED(16, 1);
+  else if (G == 16 && ppl == 3) OCF_ED(16, 3);
+  else throw std::runtime_error("row gather: unsupported H / weight dtype combination");
+#undef OCF_ED
+}
+
 void check_gather(const OcfGatherArgs& a, const char* who) {
   OCF_CHECK(a.rows && a.rp && a.col && a.lboff && a.ch_row && a.ch_j0 && a.ch_j1 && a.W && a.part,
             std::string(who) + ": null pointer");
@@ -588,6 +668,42 @@ extern "C" int ocf_gather_decoder(const OcfGatherArgs* args, void* stream) {
     shape_or_throw<__bf16>(a, G, ppl);
     by_shape<Dec<__bf16, __bf16>::L>(G, ppl, a, s);
   }
+  OCF_HIP(hipGetLastError());
+  OCF_TRY_END
+}
+
+namespace ocf {
+int g_encdec_max_polls = 1 << 22;   // ocf_gather_encdec's bounded wait (ocf_set_tuning "encdec_max_polls")
+}
+
+extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* dec, uint32_t* enc_arrive,
+                                 void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(enc && dec && enc_arrive, "ocf_gather_encdec: null arguments");
+  const OcfGatherArgs& e = *enc;
+  const OcfGatherArgs& d = *dec;
+  check_gather(e, "ocf_gather_encdec (encoder)");
+  check_gather(d, "ocf_gather_encdec (decoder)");
+  OCF_CHECK(e.xval != nullptr, "ocf_gather_encdec: xval required");
+  OCF_CHECK(d.flag && d.val && d.h && d.bias && d.chunk_stats, "ocf_gather_encdec: flag/val/h/bias/chunk_stats required");
+  OCF_CHECK(d.h_dtype == d.w_dtype && e.w_dtype == d.w_dtype && e.H == d.H, "ocf_gather_encdec: one dtype and H");
+  OCF_CHECK(d.enc_part == e.part && d.enc_cptr && d.bias_h && (d.keep >= 1.f || d.mask_out) && d.a_out,
+            "ocf_gather_encdec: dec.enc_part must be enc.part, with enc_cptr, bias_h, a_out (and mask_out)");
+  OCF_CHECK(d.jr && d.row_arrive, "ocf_gather_encdec: the decoder's folded row reduction (jr, row_arrive) is required");
+  OCF_CHECK(e.ch_row == d.ch_row && e.ch_j0 == d.ch_j0 && e.ch_j1 == d.ch_j1 && e.n_chunks == d.n_chunks &&
+                e.rows == d.rows && e.lboff == d.lboff && e.rp == d.rp,
+            "ocf_gather_encdec: the encoder and the decoder must share the batch's chunk table");
+  const OcfRowsReduceArgs& r = *d.jr;
+  OCF_CHECK(r.mode == OCF_REDUCE_GRAD_ACT && r.part == d.part && r.chunk_stats == d.chunk_stats && r.H == d.H &&
+                r.row_cptr && r.h_out && r.a_in && r.stats_part && r.B <= r.Bp && (r.keep >= 1.f || r.mask_in),
+            "ocf_gather_encdec: jr must be OCF_REDUCE_GRAD_ACT over the decoder's part / chunk_stats");
+  if (d.n_chunks == 0) return 0;
+  EncDecSync sy{enc_arrive, async_error_word(), g_encdec_max_polls};
+  hipStream_t s = (hipStream_t)stream;
+  int G, ppl;
+  if (d.w_dtype == OCF_F32) { shape_or_throw<float>(d, G, ppl); launch_encdec<float, float>(G, ppl, e, d, sy, s); }
+  else if (d.w_dtype == OCF_F16) { shape_or_throw<_Float16>(d, G, ppl); launch_encdec<_Float16, _Float16>(G, ppl, e, d, sy, s); }
+  else { shape_or_throw<__bf16>(d, G, ppl); launch_encdec<__bf16, __bf16>(G, ppl, e, d, sy, s); }
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

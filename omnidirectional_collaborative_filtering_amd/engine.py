@@ -355,6 +355,10 @@ class Engine:
         self.reduce_in_decoder = None
         self._dec_reduced = False
         self.row_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
+        # the encoder and the decoder as one launch (ocf_gather_encdec) where the decoder does the hidden epilogue and
+        # the row reduction on the encoder's own chunk table; per-row encoder arrival counters
+        self.fuse_enc_dec = True
+        self.enc_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
         # ... and dW_out + dW_in as one launch (ocf_gemm_pair: a device word the launches count up, never
         # cleared, and its host-side running count)
         self.pair_dw = True
@@ -842,13 +846,15 @@ class Engine:
             g = self._gather_args(tab, 0, part, Hp0)
             xv = self.gt["xval"]
             g.xval = xv if isinstance(xv, int) else ptr(xv)
-            call("ocf_gather_encoder", g, cur_stream())
             if (self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue
                     and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS
                     and tab["n_chunks"] <= FUSE_MEAN_CHUNKS * self.B):
-                # the decoder gather applies bias / activation / dropout to these partials itself
-                self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id)
+                # the decoder gather applies bias / activation / dropout to these partials itself; the encoder's
+                # launch is deferred to the decoder's (one fused launch when the decoder can take it)
+                self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id,
+                                       args=g, tab=tab)
                 return
+            call("ocf_gather_encoder", g, cur_stream())
             if self.comm is not None:            # partial over this rank's columns -> all-reduce
                 r = self._reduce_args(tab, part, Hp0, _lib.REDUCE_RAW)
                 r.out = ptr(self.hpre)
@@ -908,7 +914,17 @@ class Engine:
             g.jr, g.row_arrive = ctypes.addressof(r), ptr(self.row_arrive)
             self._last_jr = r             # (kept alive: the recorded step's decoder arguments point at it)
             self._dec_reduced = True
+        if ef is not None:
+            ea, et = ef["args"], ef["tab"]
+            if (self.fuse_enc_dec and g.jr and et["ch_row"] == tab["ch_row"] and et["n_chunks"] == tab["n_chunks"]
+                    and et["lboff"] == tab["lboff"]):
+                call("ocf_gather_encdec", ea, g, ptr(self.enc_arrive), cur_stream())
+                return self._after_decoder(g, fold, r)
+            call("ocf_gather_encoder", ea, cur_stream())
         call("ocf_gather_decoder", g, cur_stream())
+        return self._after_decoder(g, fold, r)
+
+    def _after_decoder(self, g, fold, r):
         if g.jr:
             pass                          # done by the decoder's last chunk of each row
         elif fold:
@@ -1302,7 +1318,8 @@ class Engine:
     # must equal the template rewritten for that step, byte for byte (any field that varies and is not
     # rewritten fails the check and the engine stays on the general path).
     _STEP_CALLS = (("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm_pair"),
-                   ("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm", "ocf_gemm"))
+                   ("ocf_gather_encoder", "ocf_gather_decoder", "ocf_gemm", "ocf_gemm"),
+                   ("ocf_gather_encdec", "ocf_gemm_pair"), ("ocf_gather_encdec", "ocf_gemm", "ocf_gemm"))
     # generator step fields (BatchGenerator.step_fields): rows, lboff, ch_row, ch_j0, ch_j1, n_chunks,
     # row_cptr, max_chunks, entries, row_ptr, row_ent, live, xval, tflag -> template fields
     _F_ROWS, _F_LBOFF, _F_CHR, _F_J0, _F_J1, _F_NCH, _F_CPTR, _F_MAXCH, _F_E, _F_RPTR, _F_RENT, _F_LIVE, \
@@ -1324,7 +1341,7 @@ class Engine:
                self.row_skip, self.shadow_blocked, self.keep,
                self.seed, self.act, self.comm, self.dp_world, self.use_sparse, self.sparse_dw, self.epoch_row_lists,
                self.epoch_scatter, self.fold_jobs, self.fold_reduce, self.fuse_enc_epilogue, self.l2,
-               tuple(self.trainable), self.grad_hook, self.master_sync, self.pair_dw)
+               tuple(self.trainable), self.grad_hook, self.master_sync, self.pair_dw, self.fuse_enc_dec)
         pl = self._plan
         if pl is not None and pl["key"] == key:
             return key
@@ -1418,7 +1435,8 @@ class Engine:
 
     def _template(self, key, calls, f):
         st = _lib.OcfRowStepArgs()
-        enc, dec, g_out, g_in, sync = self._step_blocks(calls)
+        enc, dec, g_out, g_in, sync, arrive = self._step_blocks(calls)
+        st.enc_arrive = arrive
         ctypes.memmove(ctypes.addressof(st.enc), ctypes.addressof(enc), ctypes.sizeof(enc))
         ctypes.memmove(ctypes.addressof(st.dec), ctypes.addressof(dec), ctypes.sizeof(dec))
         ctypes.memmove(ctypes.addressof(st.dw_out), ctypes.addressof(g_out), ctypes.sizeof(g_out))
@@ -1440,11 +1458,16 @@ class Engine:
 
     @staticmethod
     def _step_blocks(calls):
-        """(encoder, decoder, dW_out, dW_in argument blocks, pair sync pointer or None) of a recorded step"""
+        """(encoder, decoder, dW_out, dW_in argument blocks, pair sync pointer or None, encoder counter or None) of
+        a recorded step"""
+        arrive = None
+        if calls[0][0] == "ocf_gather_encdec":
+            enc, dec, arrive, _ = calls[0][1]
+            calls = [("ocf_gather_encoder", (enc,)), ("ocf_gather_decoder", (dec,))] + list(calls[1:])
         if len(calls) == 3:
             (g_out, g_in, sync, _) = calls[2][1]
-            return calls[0][1][0], calls[1][1][0], g_out, g_in, sync
-        return calls[0][1][0], calls[1][1][0], calls[2][1][0], calls[3][1][0], None
+            return calls[0][1][0], calls[1][1][0], g_out, g_in, sync, arrive
+        return calls[0][1][0], calls[1][1][0], calls[2][1][0], calls[3][1][0], None, arrive
 
     def _bind(self, pl):
         st = pl["st"]
@@ -1478,8 +1501,8 @@ class Engine:
 
     def _same(self, pl, calls):
         st = pl["st"]
-        enc, dec, g_out, g_in, sync = self._step_blocks(calls)
-        if (sync or None) != (st.pair_sync or None):
+        enc, dec, g_out, g_in, sync, arrive = self._step_blocks(calls)
+        if (sync or None) != (st.pair_sync or None) or (arrive or None) != (st.enc_arrive or None):
             return False
         b = lambda x: ctypes.string_at(ctypes.addressof(x), ctypes.sizeof(x))
         o = type(g_out).from_buffer_copy(g_out)

@@ -51,12 +51,12 @@ def _model(opt, dropout, data):
     return om
 
 
-@pytest.mark.parametrize("opt,dropout,sparsity,pair", [("adagrad", 0.2, [1.0, 1.0], True),
-                                                       ("adagrad", None, [0.3, 0.7], True),
-                                                       ("adam", 0.2, [0.5, 0.9], True),
-                                                       ("adagrad_decay", 0.2, [1.0, 1.0], False),
-                                                       ("rmsprop", None, [1.0, 1.0], False)])
-def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity, pair):
+@pytest.mark.parametrize("opt,dropout,sparsity,pair,encdec", [("adagrad", 0.2, [1.0, 1.0], True, True),
+                                                              ("adagrad", None, [0.3, 0.7], True, False),
+                                                              ("adam", 0.2, [0.5, 0.9], True, True),
+                                                              ("adagrad_decay", 0.2, [1.0, 1.0], False, True),
+                                                              ("rmsprop", None, [1.0, 1.0], False, False)])
+def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity, pair, encdec):
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
     r, c, v = synthetic_ratings(400, 300, 9000, half_stars=True, seed=3)
@@ -67,6 +67,7 @@ def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity, pa
     om = _model(opt, dropout, data)
     eng = om.engine
     eng.pair_dw = pair
+    eng.fuse_enc_dec = encdec           # the encoder and the decoder as one launch (ocf_gather_encdec) or two
     checked = fast = 0
     for epoch in range(5):
         gen = rd.data_gen(32, sparsity, "train", True, None, -1, pass_through_input_training=False)
@@ -87,7 +88,7 @@ def test_fast_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity, pa
                 eng._grow_stats(eng.n_stats + 1)
                 eng._rewrite(cand, f, eng._per_step())
                 calls = eng._recorded_step(gen, bi)
-                assert tuple(n for n, _ in calls) == eng._STEP_CALLS[0 if pair else 1]
+                assert tuple(n for n, _ in calls) == eng._STEP_CALLS[(0 if pair else 1) + (2 if encdec else 0)]
                 assert eng._same(cand, calls), (epoch, bi)
                 checked += 1
             else:

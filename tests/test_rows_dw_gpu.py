@@ -563,3 +563,35 @@ def test_rows_dual_large_bit_identical(gpu, cd, opt, skip, H):
         assert out[0][0] == o[0]
         for a, b in zip(out[0][1], o[1]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd,shape,B", [("float16", (2000, 30000, 300000, 0.5), 256),   # large weights: dual-row
+                                        ("bfloat16", (3706, 6040, 1000209, 0.0), 256),  # ML-1M: rows of 3+ chunks
+                                        ("float32", (1682, 943, 100000, 0.0), 100)])    # padding rows
+def test_encdec_launch_bit_identical(gpu, cd, shape, B):
+    """the encoder and the decoder as ONE launch (ocf_gather_encdec: a decoder chunk starts when its row's
+    encoder chunks have counted themselves) against the two launches: identical losses, weights, slots,
+    shadows and history over a few steps; the per-row counters are back at zero after every launch"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, skew = shape
+    out = []
+    for fused in (False, True):
+        rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=5)
+        om = om_ = omni_model(1, 500 if cd != "float32" else 200, cols, B, dense_activation="sigmoid",
+                              use_causal_info=False, dropout_probability=0.2, compute_dtype=cd, seed=4)
+        eng = om.engine
+        eng.fuse_enc_dec = fused
+        m = om.model
+        m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        h = m.fit_generator(gen, min(5, gen.num_batches), epochs=1, verbose=0).history
+        torch.cuda.synchronize()
+        assert int(eng.enc_arrive.abs().sum()) == 0 and int(eng.row_arrive.abs().sum()) == 0
+        out.append(([h[k][0] for k in sorted(h)], [t.clone() for t in eng.W] + [t.clone() for t in eng.b] +
+                    [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
+                    [t.clone() for t in eng.Wsh if t is not None]))
+        del om_
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a, b)
