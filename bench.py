@@ -95,8 +95,9 @@ def parse():
                          "engine default (small weights)")
     ap.add_argument("--rowlist-rg-work", type=int, default=0,
                     help="row-list builds: (batches x row groups) to aim for (0: data_reader.ROWLIST_RG_WORK)")
-    ap.add_argument("--fuse-enc-dec", type=int, default=1,
-                    help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches)")
+    ap.add_argument("--fuse-enc-dec", type=int, default=-1,
+                    help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches; -1: "
+                         "the engine's choice, large weights)")
     ap.add_argument("--fold-reduce", type=int, default=1,
                     help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
                          "ocf_rows_reduce launch)")
@@ -542,7 +543,8 @@ def main():
     eng.row_skip = bool(args.row_skip)
     eng.fold_jobs = bool(args.fold_jobs)
     eng.fold_reduce = bool(args.fold_reduce)
-    eng.fuse_enc_dec = bool(args.fuse_enc_dec)
+    if args.fuse_enc_dec >= 0:
+        eng.fuse_enc_dec = bool(args.fuse_enc_dec)
     if args.reduce_in_decoder >= 0:
         eng.reduce_in_decoder = bool(args.reduce_in_decoder)
     eng.split_dw_streams = bool(args.split_dw)

@@ -356,8 +356,10 @@ class Engine:
         self._dec_reduced = False
         self.row_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
         # the encoder and the decoder as one launch (ocf_gather_encdec) where the decoder does the hidden epilogue and
-        # the row reduction on the encoder's own chunk table; per-row encoder arrival counters
-        self.fuse_enc_dec = True
+        # the row reduction on the encoder's own chunk table; per-row encoder arrival counters.  None: on large
+        # weights (ML-20M 0.3882 -> 0.3855 ms/step; ML-1M 0.0778 -> 0.0788, ML-100K 0.0490 -> 0.0487: the encoder
+        # chunks run at the decoder's 163 VGPRs there; profiles/r05_cfg/encdec*.jsonl)
+        self.fuse_enc_dec = None
         self.enc_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
         # ... and dW_out + dW_in as one launch (ocf_gemm_pair: a device word the launches count up, never
         # cleared, and its host-side running count)
@@ -916,7 +918,8 @@ class Engine:
             self._dec_reduced = True
         if ef is not None:
             ea, et = ef["args"], ef["tab"]
-            if (self.fuse_enc_dec and g.jr and et["ch_row"] == tab["ch_row"] and et["n_chunks"] == tab["n_chunks"]
+            fuse = self.fuse_enc_dec if self.fuse_enc_dec is not None else self.Np // TILE * 48 >= 8192
+            if (fuse and g.jr and et["ch_row"] == tab["ch_row"] and et["n_chunks"] == tab["n_chunks"]
                     and et["lboff"] == tab["lboff"]):
                 call("ocf_gather_encdec", ea, g, ptr(self.enc_arrive), cur_stream())
                 return self._after_decoder(g, fold, r)
