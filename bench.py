@@ -98,6 +98,8 @@ def parse():
     ap.add_argument("--fuse-enc-dec", type=int, default=-1,
                     help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches; -1: "
                          "the engine's choice, large weights)")
+    ap.add_argument("--gather-chunk", type=int, default=0,
+                    help="entries per row-gather chunk of large batches (0: data_reader.GATHER_CHUNK)")
     ap.add_argument("--fold-reduce", type=int, default=1,
                     help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
                          "ocf_rows_reduce launch)")
@@ -507,6 +509,8 @@ def main():
 
     if args.rowlist_rg_work > 0:
         _dr.ROWLIST_RG_WORK = args.rowlist_rg_work
+    if args.gather_chunk > 0:
+        _dr.GATHER_CHUNK = args.gather_chunk
     t0 = time.time()
     data_full = synthetic_fixed_split(args.config, seed=0, skew=args.skew)
     N = data_full.num_cols

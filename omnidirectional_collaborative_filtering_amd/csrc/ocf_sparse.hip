@@ -506,8 +506,17 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(OcfRowsReduceArgs a) {
   const bool real = b < a.B;
   const int c0 = real ? a.row_cptr[b] : 0, c1 = real ? a.row_cptr[b + 1] : 0;
   for (int x = threadIdx.x; x < a.H; x += blockDim.x) {
+    // 8 chunks' loads in flight, added in chunk order (the same sums: rows of many chunks -- Netflix's ~22 --
+    // waited a round trip per chunk)
     float v = 0.f;
-    for (int c = c0; c < c1; ++c) v += a.part[(int64_t)c * a.H + x];
+    for (int c = c0; c < c1; c += 8) {
+      float q[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = c + k < c1 ? a.part[(int64_t)(c + k) * a.H + x] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (c + k < c1) v += q[k];
+    }
     if (a.mode == OCF_REDUCE_RAW) {
       a.out[(int64_t)b * a.H + x] = v;
     } else if (a.mode == OCF_REDUCE_BIAS_ACT) {
@@ -528,7 +537,14 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(OcfRowsReduceArgs a) {
   if (a.chunk_stats && threadIdx.x < 4) {
     float v = 0.f;
     if (threadIdx.x < 3)
-      for (int c = c0; c < c1; ++c) v += a.chunk_stats[(int64_t)c * 4 + threadIdx.x];
+      for (int c = c0; c < c1; c += 8) {
+        float q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = c + k < c1 ? a.chunk_stats[(int64_t)(c + k) * 4 + threadIdx.x] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (c + k < c1) v += q[k];
+      }
     a.stats_part[(int64_t)b * 4 + threadIdx.x] = v;
     if (threadIdx.x == 0 && a.row_sse) a.row_sse[b] = v;
   }
