@@ -27,6 +27,9 @@ def per_dispatch(path, counter):
 
 
 def phase_of(name, seen):
+    if "gather_encdec" in name:           # the encoder and the decoder as one launch (ocf_gather_encdec)
+        seen["gather"] = "dec"
+        return "enc_dec"
     if "gather_encoder" in name:
         seen["gather"] = "enc"
         return "enc_gemm"
