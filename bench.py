@@ -625,14 +625,18 @@ def main():
         # the timed batches' row lists, built inside the timed region (one launch sequence, as at the
         # start of every training epoch)
         gen.prepare_row_lists(eng.Np, [batches[(args.warmup + i) % len(batches)] for i in range(args.steps)])
+    t_lists = time.perf_counter()
     # the dominant kernel's HIP events on every TIMER_EVERY-th timed step: each event record idles the
     # stream ~6 us (measured: 0 vs 5.8 us launch gaps with and without), so sampling keeps the timing
     # overhead at ~0.5 % of the step while still averaging over the whole timed region
     sampled = {dom} if dom else None
+    t_first = None
     for i in range(args.steps):
         if dom:
             eng.timer_only = sampled if i % TIMER_EVERY == 0 else {"-"}
         nnz += step(args.warmup + i)
+        if t_first is None:
+            t_first = time.perf_counter()
     t_issued = time.perf_counter()
     torch.cuda.synchronize()
     if world > 1:
@@ -769,6 +773,12 @@ def main():
                        "every %d-th step)" % (w_all, dom, TIMER_EVERY),
         "setup_s": round(setup_s, 1),
         "host_issue_ms_per_step": round(host_ms, 4),
+        # host time inside the timed region before the GPU has work: the row-list build's prelude (staging,
+        # launches) and the first step's issue (the window's step table); later steps are issued behind the GPU
+        "window_host_us": {"row_lists": round((t_lists - t_start) * 1e6, 1),
+                           "first_step": round(((t_first or t_lists) - t_lists) * 1e6, 1),
+                           "row_list_parts": {k: round(v, 1) for k, v in getattr(gen, "rl_host_us", {}).items()}
+                           if epoch_lists else None},
         "timed_step_paths": step_paths,
         "row_lists": ("per epoch: ocf_epoch_row_lists for the %d timed batches inside the timed region"
                       % len(set(batches[(args.warmup + i) % len(batches)] for i in range(args.steps))))

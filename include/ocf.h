@@ -119,12 +119,15 @@ int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
  * for many train batches of an epoch plan in one launch: base is batch 0's OcfScatterArgs (mode 0, no
  * dense / xin / bucket / count / tag outputs, E2 = 0); batch sel[s] uses base's rows1 / lboff1 / boff1
  * offset by that batch, keep1 + keep_off[sel[s]], stream = stream_mul * (sel[s] + 1) (the per-step
- * generator's seeds) and writes xval / tflag at ebase[s] .. ebase[s + 1]; max_e = max entries of a batch.
+ * generator's seeds) and writes xval / tflag at ebase[s] - ebase0 .. ebase[s + 1] - ebase0; max_e = max entries
+ * of a batch.  ebase0 lets sel / ebase point into epoch-wide device tables (a window of consecutive batches
+ * needs no upload): 0 when ebase starts at 0.
  * Extension (no reference counterpart): the data_reader.py:95-200 batch assembly, per epoch. */
 typedef struct OcfEpochScatterArgs {
   int n_sel; const int32_t* sel; const int64_t* ebase; int64_t max_e;
   const int64_t* keep_off; uint64_t stream_mul;
   float* xval; uint8_t* tflag;
+  int64_t ebase0;                        /* subtracted from every ebase[s] */
 } OcfEpochScatterArgs;
 int ocf_epoch_scatter(const OcfScatterArgs* base, const OcfEpochScatterArgs* ep, void* stream);
 
@@ -511,7 +514,7 @@ int ocf_row_lists(const OcfRowListArgs* args, void* stream);
 /* ocf_epoch_row_lists -- the row lists of ocf_row_lists for many batches of an epoch plan at once
  * (one launch sequence per epoch instead of three small launches per step), built from the plan's
  * tables rather than a scatter: for each selected batch s (epoch batch sel[s]) and column m,
- *   row_ent[ebase[s] + row_ptr[s][m] .. ebase[s] + row_ptr[s][m+1]) = (batch-local entry, batch row)
+ *   row_ent[ebase[s] - ebase0 + row_ptr[s][m] .. ebase[s] - ebase0 + row_ptr[s][m+1]) = (batch-local entry, batch row)
  * of every source entry of the batch in column m, in entry (= batch-row) order, row_ptr[s] the exclusive
  * scan of the column counts (row_ptr[s][n_cols] = the batch's entry count), and with live non-null
  * the OCF_LIVE_REC records of the columns holding at least one entry (a superset of the columns with
@@ -520,7 +523,8 @@ int ocf_row_lists(const OcfRowListArgs* args, void* stream);
  * the count / fill walks split each batch's rows over n_rg workgroups (more parallelism when few batches are
  * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols + n_sel * (n_cols / 4096
  * + 1) + 1 + 2 * (entries / 1025 + 1) ints (counts per row group, per-4,096-column block totals, then the queue of
- * lists over 1,024 entries).  n_cols % 128 == 0.
+ * lists over 1,024 entries).  n_cols % 128 == 0.  ebase0 (0 when ebase starts at 0) lets sel / ebase be a window of
+ * epoch-wide device tables (consecutive batches: nothing to upload per build).
  * Extension (no reference counterpart): the data_reader.py:326-419 batch loop's structure, per epoch. */
 typedef struct OcfEpochRowListArgs {
   int n_sel; int B; int n_cols;
@@ -534,6 +538,7 @@ typedef struct OcfEpochRowListArgs {
   int32_t* row_ent;                      /* [ebase[n_sel]][2] */
   uint8_t* live;                         /* [n_sel][n_cols / 128][OCF_LIVE_REC] or null */
   int n_rg;                              /* row groups per batch (0 / 1: one) */
+  int64_t ebase0;                        /* subtracted from every ebase[s] */
 } OcfEpochRowListArgs;
 int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream);
 

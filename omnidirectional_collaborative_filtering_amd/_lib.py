@@ -56,7 +56,7 @@ class OcfRowListArgs(ctypes.Structure):
 class OcfEpochScatterArgs(ctypes.Structure):
     _fields_ = [
         ("n_sel", I32), ("sel", P), ("ebase", P), ("max_e", I64), ("keep_off", P), ("stream_mul", U64),
-        ("xval", P), ("tflag", P),
+        ("xval", P), ("tflag", P), ("ebase0", I64),
     ]
 
 
@@ -64,6 +64,7 @@ class OcfEpochRowListArgs(ctypes.Structure):
     _fields_ = [
         ("n_sel", I32), ("B", I32), ("n_cols", I32), ("rows", P), ("rp", P), ("col", P), ("lboff", P),
         ("sel", P), ("ebase", P), ("cnt", P), ("row_ptr", P), ("row_ent", P), ("live", P), ("n_rg", I32),
+        ("ebase0", I64),
     ]
 
 

@@ -167,8 +167,8 @@ __global__ void __launch_bounds__(SC_THREADS) scatter_epoch_kernel(ScatterArgs b
   a.keep1 = base.keep1 ? base.keep1 + ep.keep_off[bi] : nullptr;
   a.stream = ep.stream_mul * (uint64_t)(bi + 1);
   a.E1 = ep.ebase[s + 1] - ep.ebase[s];
-  a.xval1 = ep.xval + ep.ebase[s];
-  a.tflag1 = ep.tflag + ep.ebase[s];
+  a.xval1 = ep.xval + (ep.ebase[s] - ep.ebase0);
+  a.tflag1 = ep.tflag + (ep.ebase[s] - ep.ebase0);
   const int64_t* lboff = a.lboff1 ? a.lboff1 : a.boff1;
   for (int i = threadIdx.x; i <= a.B; i += SC_THREADS) sh_off[i] = lboff[i];
   __syncthreads();

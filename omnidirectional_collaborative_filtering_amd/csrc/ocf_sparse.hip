@@ -1280,7 +1280,7 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListAr
   erl_stage(a, s, l);
   __syncthreads();
   const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
-  int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+  int2* ent = reinterpret_cast<int2*>(a.row_ent) + (a.ebase[s] - a.ebase0);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int b = b0 + w; b < b1; b += ERL_THREADS / 64) {
     const int e0 = l.off[b], n = l.off[b + 1] - e0;
@@ -1317,7 +1317,7 @@ __global__ void __launch_bounds__(128) erl_sort_kernel(OcfEpochRowListArgs a) {
   const int t = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n_cols = a.n_cols, m = t * 128 + tid;
   const int* rp = a.row_ptr + (int64_t)s * (n_cols + 1);
-  int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+  int2* ent = reinterpret_cast<int2*>(a.row_ent) + (a.ebase[s] - a.ebase0);
   const int lo = rp[m], n = rp[m + 1] - lo;
   if (tid == 0) nlong = 0;
   const uint64_t bal = __ballot(n > 0);
@@ -1365,7 +1365,7 @@ __global__ void __launch_bounds__(1024) erl_sort_long_kernel(OcfEpochRowListArgs
   for (int qi = blockIdx.x; qi < nq; qi += gridDim.x) {
     const int s = q[1 + 2 * qi], m = q[2 + 2 * qi];
     const int* rp = a.row_ptr + (int64_t)s * (a.n_cols + 1);
-    int2* ent = reinterpret_cast<int2*>(a.row_ent) + a.ebase[s];
+    int2* ent = reinterpret_cast<int2*>(a.row_ent) + (a.ebase[s] - a.ebase0);
     const int lo = rp[m], n = rp[m + 1] - lo;
     for (int i = threadIdx.x; i < n; i += 1024) buf[i] = ent[lo + i];
     __syncthreads();

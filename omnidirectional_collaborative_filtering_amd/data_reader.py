@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 
 import numpy as np
 import torch
@@ -257,7 +258,8 @@ class BatchGenerator(object):
         self.chunks2 = self.chunks1 if self.src2 is None else self._chunk_tables(self.src2.lens, rows, r.device)
         self.keep_dev = None
         self.keep_off = None
-        self._keep_off_dev = None
+        self._ep_tabs = None           # per-epoch device tables of the row-list builds (_epoch_tables)
+        self._ep_fields = None         # per-epoch constant step fields (step_fields)
         if keep is not None:
             self.keep_dev = keep
             self.keep_off = np.concatenate([[0], np.cumsum(self.nnz_full)])
@@ -327,6 +329,7 @@ class BatchGenerator(object):
         live-row records of the given epoch batches (default: every batch of the epoch), built on the
         device by one ocf_epoch_row_lists launch sequence instead of per step.  n_cols = the engine's
         padded column count."""
+        t0 = time.perf_counter()
         if not self.started:
             self._start()
         if self.split != "train":
@@ -335,7 +338,12 @@ class BatchGenerator(object):
         if batches is None:
             # under data parallelism a rank only trains on its own batches (parallel.shard_batches)
             batches = shard_batches(nb, *self.dp_shard) if self.dp_shard else np.arange(nb)
-        sel = np.unique(np.asarray(batches, dtype=np.int64))
+        if isinstance(batches, (list, tuple, range)):
+            sel = np.array(sorted(set(batches)), dtype=np.int64)     # (np.unique costs ~10-25 us on 20 ints)
+        else:
+            sel = np.asarray(batches, dtype=np.int64)
+            if sel.size > 1 and not bool((sel[1:] > sel[:-1]).all()):
+                sel = np.unique(sel)
         if len(sel) and (sel[0] < 0 or sel[-1] >= nb):
             raise ValueError("batch index out of range")
         # one build holds at most ROWLIST_MAX_BATCHES batches and ~1 GiB of row pointers (the library's
@@ -346,49 +354,80 @@ class BatchGenerator(object):
         if self.src1.dup is not None and len(sel):
             self._check_list_lengths(sel)
         dev = self.rows_dev.device
-        ebase = np.zeros(len(sel) + 1, dtype=np.int64)
-        np.cumsum(self.nnz1[sel], out=ebase[1:])
+        ep = self._epoch_tables(dev)
+        n = len(sel)
+        if n and int(sel[-1]) - int(sel[0]) + 1 == n:
+            # consecutive batches (an epoch, the bench's timed window): sel / ebase point into the epoch's device
+            # tables, ebase0 rebases the entry offsets -- nothing to upload (a staged copy cost 65-116 us of
+            # host time on an idle GPU at the start of a timed window)
+            b0 = int(sel[0])
+            e0 = int(ep["ebase"][b0])
+            ebase = ep["ebase"][b0:b0 + n + 1] - e0
+            p_sel, p_ebase = ep["sel_dev"].data_ptr() + 4 * b0, ep["ebase_dev"].data_ptr() + 8 * b0
+        else:
+            e0 = 0
+            ebase = np.zeros(n + 1, dtype=np.int64)
+            np.cumsum(self.nnz1[sel], out=ebase[1:])
+            p_ebase, p_sel = self._stage([ebase, sel.astype(np.int32)], dev)
         E = int(ebase[-1])
         # row groups per batch for the count / fill walks: a build of few batches (the bench's timed window, the
         # tail of an epoch) would leave most CUs idle with one workgroup per (batch, column block)
-        n_rg = int(min(8, max(1, -(-ROWLIST_RG_WORK // max(len(sel), 1)))))
+        n_rg = int(min(8, max(1, -(-ROWLIST_RG_WORK // max(n, 1)))))
         # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
-        need = dict(cnt=(n_rg * len(sel) * n_cols + len(sel) * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1),
-                         torch.int32),
-                    row_ptr=(len(sel) * (n_cols + 1), torch.int32), row_ent=(2 * max(E, 1), torch.int32),
-                    live=(max(len(sel) * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
-                    xval=(max(E, 1), torch.float32), tflag=(max(E, 1), torch.uint8))
-        bufs = getattr(self, "_rl_bufs", None) or {}
-        for k, (n, dt) in need.items():
-            if k not in bufs or bufs[k].numel() < n:
-                bufs[k] = torch.empty(n, dtype=dt, device=dev)
-        self._rl_bufs = bufs
-        p_ebase, p_sel = self._stage([ebase, sel.astype(np.int32)], dev)
-        keep = dict(row_ptr=bufs["row_ptr"], row_ent=bufs["row_ent"], live=bufs["live"])
+        need = (("cnt", n_rg * n * n_cols + n * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1), torch.int32),
+                ("row_ptr", n * (n_cols + 1), torch.int32), ("row_ent", 2 * max(E, 1), torch.int32),
+                ("live", max(n * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
+                ("xval", max(E, 1), torch.float32), ("tflag", max(E, 1), torch.uint8))
+        bufs = getattr(self, "_rl_bufs", None)
+        if bufs is None:
+            bufs = self._rl_bufs = {}
+        for k, m, dt in need:
+            b = bufs.get(k)
+            if b is None or b[1] < m:
+                t = torch.empty(m, dtype=dt, device=dev)
+                bufs[k] = (t, m, t.data_ptr())
+        t1 = time.perf_counter()
         a = _lib.OcfEpochRowListArgs()
-        a.n_sel, a.B, a.n_cols, a.n_rg = len(sel), self.B, n_cols, n_rg
-        a.rows, a.rp, a.col, a.lboff = ptr(self.rows_dev), ptr(self.src1.rp), ptr(self.src1.col), ptr(self.lboff1_dev)
+        a.n_sel, a.B, a.n_cols, a.n_rg, a.ebase0 = n, self.B, n_cols, n_rg, e0
+        a.rows, a.rp, a.col, a.lboff = ep["args_const"]
         a.sel, a.ebase = p_sel, p_ebase
-        a.cnt, a.row_ptr, a.row_ent, a.live = ptr(bufs["cnt"]), ptr(bufs["row_ptr"]), ptr(bufs["row_ent"]), \
-            ptr(bufs["live"])
+        a.cnt, a.row_ptr, a.row_ent, a.live = bufs["cnt"][2], bufs["row_ptr"][2], bufs["row_ent"][2], bufs["live"][2]
         _lib.call("ocf_epoch_row_lists", a, cur_stream())
+        t2 = time.perf_counter()
         # ... and the batches' per-entry scatter outputs (live input value, live-target flag): the per-step
         # ocf_scatter_batch has nothing left to do for them
-        base = self.scatter_args(0) if nb else _lib.OcfScatterArgs()
-        es = _lib.OcfEpochScatterArgs()
-        if self.keep_dev is not None:
-            if getattr(self, "_keep_off_dev", None) is None:     # (per epoch plan: uploaded once)
-                self._keep_off_dev = _h2d(np.ascontiguousarray(self.keep_off, dtype=np.int64), dev)
-            es.keep_off = ptr(self._keep_off_dev)
-        es.n_sel, es.sel, es.ebase = len(sel), p_sel, p_ebase
-        es.max_e = int(self.nnz1[sel].max()) if len(sel) else 0
-        es.stream_mul = 2
-        es.xval, es.tflag = ptr(bufs["xval"]), ptr(bufs["tflag"])
-        if len(sel):
-            _lib.call("ocf_epoch_scatter", base, es, cur_stream())
-        keep.update(xval=bufs["xval"], tflag=bufs["tflag"])
-        keep.update(n_cols=n_cols, slot={int(b): i for i, b in enumerate(sel)}, ebase_host=ebase)
-        self._rl = keep
+        if n:
+            es = _lib.OcfEpochScatterArgs()
+            es.keep_off = ep["keep_off"]
+            es.n_sel, es.sel, es.ebase, es.ebase0 = n, p_sel, p_ebase, e0
+            es.max_e = int(self.nnz1[sel].max())
+            es.stream_mul = 2
+            es.xval, es.tflag = bufs["xval"][2], bufs["tflag"][2]
+            _lib.call("ocf_epoch_scatter", ep["scatter_base"], es, cur_stream())
+        self._rl = dict(row_ptr=bufs["row_ptr"][0], row_ent=bufs["row_ent"][0], live=bufs["live"][0],
+                        xval=bufs["xval"][0], tflag=bufs["tflag"][0], n_cols=n_cols,
+                        slot=dict(zip(sel.tolist(), range(n))), ebase_host=ebase, fields={})
+        t3 = time.perf_counter()
+        # host time of the build's parts (us; bench.py reports them: the prelude of a timed window)
+        self.rl_host_us = dict(plan=(t1 - t0) * 1e6, lists=(t2 - t1) * 1e6, scatter=(t3 - t2) * 1e6)
+
+    def _epoch_tables(self, dev):
+        """per epoch plan, on the first row-list build: sel = 0 .. nb - 1 and ebase = the batches' cumulative
+        entry counts on the device (a build of consecutive batches points into them), the keep-flag offsets, the
+        epoch scatter's base arguments and the constant pointers of the row-list build"""
+        ep = getattr(self, "_ep_tabs", None)
+        if ep is None:
+            nb = self.num_batches
+            ebase = np.zeros(nb + 1, dtype=np.int64)
+            np.cumsum(self.nnz1, out=ebase[1:])
+            ep = dict(ebase=ebase, ebase_dev=_h2d(ebase, dev), sel_dev=_h2d(np.arange(max(nb, 1), dtype=np.int32), dev),
+                      scatter_base=self.scatter_args(0) if nb else _lib.OcfScatterArgs(),
+                      args_const=(ptr(self.rows_dev), ptr(self.src1.rp), ptr(self.src1.col), ptr(self.lboff1_dev)))
+            ep["keep_off_dev"] = None if self.keep_dev is None else \
+                _h2d(np.ascontiguousarray(self.keep_off, dtype=np.int64), dev)
+            ep["keep_off"] = None if ep["keep_off_dev"] is None else ep["keep_off_dev"].data_ptr()
+            self._ep_tabs = ep
+        return ep
 
     def _stage(self, parts, dev):
         """host arrays to the device in ONE copy through a persistent pinned staging buffer (8-byte aligned
@@ -453,30 +492,34 @@ class BatchGenerator(object):
         """batch bi's table pointers and sizes for the one-call training step (Engine.fast_train_step):
         (rows, lboff, ch_row, ch_j0, ch_j1, n_chunks, row_cptr, max_chunks, entries, row_ptr, row_ent, live,
         xval, tflag) -- the values gather_tables / targets / row_lists give -- or None when batch bi's row
-        lists are not built (row_lists builds them on the general path).  Computed once per row-list window."""
+        lists are not built (row_lists builds them on the general path).  The batch-constant part is computed
+        once per epoch plan, the window's part once per batch and window."""
         rl = getattr(self, "_rl", None)
         if self.split != "train" or rl is None or rl["n_cols"] != n_cols:
             return None
         s = rl["slot"].get(bi)
         if s is None:
             return None
-        ff = rl.get("fields")
-        if ff is None:
-            B, ch = self.B, self.chunks1
-            sel = np.fromiter(rl["slot"].keys(), dtype=np.int64, count=len(rl["slot"]))
-            slots = np.fromiter(rl["slot"].values(), dtype=np.int64, count=len(rl["slot"]))
-            order = np.argsort(slots)
-            sel, slots = sel[order], slots[order]
-            c0 = ch["cbase"][sel]
-            e0 = rl["ebase_host"][slots]
-            cols = [self.rows_dev.data_ptr() + 4 * sel * B, self.lboff1_dev.data_ptr() + 8 * sel * (B + 1),
-                    ch["ch_row"].data_ptr() + 4 * c0, ch["ch_j0"].data_ptr() + 4 * c0, ch["ch_j1"].data_ptr() + 4 * c0,
-                    ch["cbase"][sel + 1] - c0, ch["row_cptr"].data_ptr() + 4 * sel * (B + 1), ch["max_chunks"][sel],
-                    self.nnz1[sel], rl["row_ptr"].data_ptr() + 4 * slots * (n_cols + 1),
-                    rl["row_ent"].data_ptr() + 8 * e0, rl["live"].data_ptr() + slots * (n_cols // 128) * _lib.LIVE_REC,
-                    rl["xval"].data_ptr() + 4 * e0, rl["tflag"].data_ptr() + e0]
-            ff = rl["fields"] = list(zip(*[np.asarray(c, dtype=np.int64).tolist() for c in cols]))
-        return ff[s]
+        f = rl["fields"].get(bi)
+        if f is None:
+            ep = self._ep_fields
+            if ep is None:
+                # the epoch's batch-constant fields, once per epoch plan (tuples per batch)
+                B, ch = self.B, self.chunks1
+                sel = np.arange(self.num_batches, dtype=np.int64)
+                c0 = ch["cbase"][:-1]
+                cols = [self.rows_dev.data_ptr() + 4 * sel * B, self.lboff1_dev.data_ptr() + 8 * sel * (B + 1),
+                        ch["ch_row"].data_ptr() + 4 * c0, ch["ch_j0"].data_ptr() + 4 * c0,
+                        ch["ch_j1"].data_ptr() + 4 * c0, ch["cbase"][1:] - c0,
+                        ch["row_cptr"].data_ptr() + 4 * sel * (B + 1), ch["max_chunks"], self.nnz1]
+                ep = self._ep_fields = list(zip(*[np.asarray(c, dtype=np.int64).tolist() for c in cols]))
+            # ... and the row-list window's
+            e0 = int(rl["ebase_host"][s])
+            f = rl["fields"][bi] = ep[bi] + (
+                rl["row_ptr"].data_ptr() + 4 * s * (n_cols + 1), rl["row_ent"].data_ptr() + 8 * e0,
+                rl["live"].data_ptr() + s * (n_cols // 128) * _lib.LIVE_REC, rl["xval"].data_ptr() + 4 * e0,
+                rl["tflag"].data_ptr() + e0)
+        return f
 
     @staticmethod
     def _local_offsets(lens, rows):

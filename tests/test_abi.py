@@ -76,9 +76,10 @@ STRUCTS = {
     "OcfRowListArgs": (_lib.OcfRowListArgs, ["ecb", "E", "col_cnt", "cursor", "n_cols", "row_ptr", "row_ent", "rtag_in",
                                              "rtag_out", "rtag", "live_in", "live_out"]),
     "OcfEpochRowListArgs": (_lib.OcfEpochRowListArgs, ["n_sel", "B", "n_cols", "rows", "rp", "col", "lboff", "sel",
-                                                       "ebase", "cnt", "row_ptr", "row_ent", "live", "n_rg"]),
+                                                       "ebase", "cnt", "row_ptr", "row_ent", "live", "n_rg",
+                                                       "ebase0"]),
     "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
-                                                       "xval", "tflag"]),
+                                                       "xval", "tflag", "ebase0"]),
     "OcfModelDesc": (_lib.OcfModelDesc, ["n_hidden", "N", "k_blocks", "hidden", "act", "dropout", "compute_dtype",
                                          "max_batch", "seed", "W", "b"]),
     "OcfOptStepArgs": (_lib.OcfOptStepArgs, ["p", "g", "g_dtype", "s1", "s2", "n", "opt", "shadow", "shadow_dtype"]),

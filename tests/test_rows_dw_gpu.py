@@ -238,6 +238,7 @@ def _gen_for(rows, cols, nnz, B, skew, seed, sparsity=(1.0, 1.0), pass_through=T
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows,cols,nnz,B,skew,sel", [
     (900, 4000, 30000, 128, 0.0, None),          # every batch of the epoch, short lists
+    (900, 4000, 30000, 128, 0.0, [2, 3, 4]),     # consecutive batches past 0: windows of the epoch tables (ebase0)
     (3000, 1024, 400000, 512, 1.0, [1, 0, 3]),   # a subset, out of order; lists up to ~500 (LDS bitonic)
     (5000, 1024, 1500000, 2048, 1.0, None),      # lists over 1,024 entries (long-list queue)
 ])
@@ -406,16 +407,18 @@ def test_engine_fold_reduce_bit_identical(gpu, cd, B):
 @pytest.mark.gpu
 @pytest.mark.parametrize("rng", ["numpy", "device"])
 @pytest.mark.parametrize("sparsity,pt", [((1.0, 1.0), True), ((0.5, 0.9), False), ((0.3, 0.6), True)])
-def test_epoch_scatter_matches_per_batch(gpu, rng, sparsity, pt):
+@pytest.mark.parametrize("sel", [[3, 0, 5], [2, 3, 4]])
+def test_epoch_scatter_matches_per_batch(gpu, rng, sparsity, pt, sel):
     """ocf_epoch_scatter (every batch of the plan in one launch, BatchGenerator.prepare_row_lists) writes the
     same per-entry live input values and live-target flags as ocf_scatter_batch batch by batch (reciprocal
-    split from the host NumPy draws or the device Philox stream of each batch, pass-through or not)"""
+    split from the host NumPy draws or the device Philox stream of each batch, pass-through or not); a
+    selection out of order (staged sel / ebase) and a window of consecutive batches (the epoch's tables, ebase0)"""
     rd, gen = _gen_for(900, 4000, 40000, 128, 0.5, seed=17, sparsity=sparsity, pass_through=pt, rng=rng)
     gen._start()
-    gen.prepare_row_lists(4096, [3, 0, 5])
+    gen.prepare_row_lists(4096, sel)
     torch.cuda.synchronize()
     rl = gen._rl
-    for bi in (0, 3, 5):
+    for bi in sel:
         E = int(gen.nnz1[bi])
         xv = torch.full((E,), -3.0, device="cuda")
         tf = torch.full((E,), 7, dtype=torch.uint8, device="cuda")
