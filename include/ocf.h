@@ -687,6 +687,15 @@ int ocf_set_tuning(const char* key, int value, int* previous);
  * (Engine.take_stats at every epoch end), so a fault in the last launches of a run cannot go unseen. */
 int ocf_check_async(void);
 
+/* ocf_timing_event_* -- HIP timing events with a device-scope release (hipEventReleaseToDevice) for phase and
+ * kernel timing: a default event's system-scope release writes back and invalidates the L2 at every record
+ * (~6 us of stream idle in a timed loop).  The handles go where a hipEvent_t is taken (OcfRowStepArgs ev[],
+ * OcfRankStepArgs ev[]); elapsed waits for `end`.  Extension (no reference counterpart): measurement. */
+int ocf_timing_event_create(void** ev);
+int ocf_timing_event_record(void* ev, void* stream);
+int ocf_timing_event_elapsed(void* start, void* end, float* ms);
+int ocf_timing_event_destroy(void* ev);
+
 int ocf_version(void);
 const char* ocf_last_error(void);
 

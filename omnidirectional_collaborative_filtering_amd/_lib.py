@@ -259,6 +259,10 @@ SIGNATURES = {
     "ocf_backward": (I32, [P, P, I64, I32, F32, P, P, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_check_async": (I32, []),
+    "ocf_timing_event_create": (I32, [P]),
+    "ocf_timing_event_record": (I32, [P, P]),
+    "ocf_timing_event_elapsed": (I32, [P, P, P]),
+    "ocf_timing_event_destroy": (I32, [P]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }
