@@ -521,9 +521,9 @@ int ocf_row_lists(const OcfRowListArgs* args, void* stream);
  * a nonzero gradient: an Adagrad l2 = 0 update at g = 0 is the identity, so the row skip stays exact).
  * B <= 4,096; a batch's entries < 2^31.  n_rg (0 or 1: one; at most min(64, B)): row groups per batch --
  * the count / fill walks split each batch's rows over n_rg workgroups (more parallelism when few batches are
- * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols + n_sel * (n_cols / 4096
- * + 1) + 1 + 2 * (entries / 1025 + 1) ints (counts per row group, per-4,096-column block totals, then the queue of
- * lists over 1,024 entries).  n_cols % 128 == 0.  ebase0 (0 when ebase starts at 0) lets sel / ebase be a window of
+ * built at once; the lists are the same).  cnt: scratch of max(n_rg, 1) * n_sel * n_cols / 2 + n_sel * (n_cols / 4096
+ * + 1) + 1 + 2 * (entries / 1025 + 1) ints (16-bit counts per row group, per-4,096-column block totals, then the
+ * queue of lists over 1,024 entries).  n_cols % 128 == 0.  ebase0 (0 when ebase starts at 0) lets sel / ebase be a window of
  * epoch-wide device tables (consecutive batches: nothing to upload per build).
  * Extension (no reference counterpart): the data_reader.py:326-419 batch loop's structure, per epoch. */
 typedef struct OcfEpochRowListArgs {
@@ -539,6 +539,10 @@ typedef struct OcfEpochRowListArgs {
   uint8_t* live;                         /* [n_sel][n_cols / 128][OCF_LIVE_REC] or null */
   int n_rg;                              /* row groups per batch (0 / 1: one) */
   int64_t ebase0;                        /* subtracted from every ebase[s] */
+  int max_list;                          /* bound on a column's entries in one batch (B without duplicate
+                                            ratings), 0 = unknown: <= 1,024 skips the long-list sort pass */
+  int64_t entries;                       /* the build's entries (ebase[n_sel] - ebase[0]; 0 = unknown): >= 4 per
+                                            list on average sorts the lists across lanes instead of per thread */
 } OcfEpochRowListArgs;
 int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream);
 
@@ -686,15 +690,6 @@ int ocf_set_tuning(const char* key, int value, int* previous);
  * (OCF_ASYNC_*) without launching anything: hosts call it after their last step's results are read back
  * (Engine.take_stats at every epoch end), so a fault in the last launches of a run cannot go unseen. */
 int ocf_check_async(void);
-
-/* ocf_timing_event_* -- HIP timing events with a device-scope release (hipEventReleaseToDevice) for phase and
- * kernel timing: a default event's system-scope release writes back and invalidates the L2 at every record
- * (~6 us of stream idle in a timed loop).  The handles go where a hipEvent_t is taken (OcfRowStepArgs ev[],
- * OcfRankStepArgs ev[]); elapsed waits for `end`.  Extension (no reference counterpart): measurement. */
-int ocf_timing_event_create(void** ev);
-int ocf_timing_event_record(void* ev, void* stream);
-int ocf_timing_event_elapsed(void* start, void* end, float* ms);
-int ocf_timing_event_destroy(void* ev);
 
 int ocf_version(void);
 const char* ocf_last_error(void);

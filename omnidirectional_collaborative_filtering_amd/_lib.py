@@ -64,7 +64,7 @@ class OcfEpochRowListArgs(ctypes.Structure):
     _fields_ = [
         ("n_sel", I32), ("B", I32), ("n_cols", I32), ("rows", P), ("rp", P), ("col", P), ("lboff", P),
         ("sel", P), ("ebase", P), ("cnt", P), ("row_ptr", P), ("row_ent", P), ("live", P), ("n_rg", I32),
-        ("ebase0", I64),
+        ("ebase0", I64), ("max_list", I32), ("entries", I64),
     ]
 
 
@@ -259,10 +259,6 @@ SIGNATURES = {
     "ocf_backward": (I32, [P, P, I64, I32, F32, P, P, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_check_async": (I32, []),
-    "ocf_timing_event_create": (I32, [P]),
-    "ocf_timing_event_record": (I32, [P, P]),
-    "ocf_timing_event_elapsed": (I32, [P, P, P]),
-    "ocf_timing_event_destroy": (I32, [P]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

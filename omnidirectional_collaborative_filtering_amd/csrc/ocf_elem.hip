@@ -63,36 +63,6 @@ extern "C" int ocf_check_async(void) {
   OCF_TRY_END
 }
 
-// Timing events with a device-scope release: the default event's system-scope release writes back and
-// invalidates the L2 at every record, which idled the stream ~6 us per record in the bench's timed region
-// (and measured the next kernel with a cold L2)
-extern "C" int ocf_timing_event_create(void** ev) {
-  OCF_TRY_BEGIN
-  OCF_CHECK(ev, "ocf_timing_event_create: null pointer");
-  hipEvent_t e = nullptr;
-  OCF_HIP(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
-  *ev = (void*)e;
-  OCF_TRY_END
-}
-extern "C" int ocf_timing_event_record(void* ev, void* stream) {
-  OCF_TRY_BEGIN
-  OCF_CHECK(ev, "ocf_timing_event_record: null event");
-  OCF_HIP(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
-  OCF_TRY_END
-}
-extern "C" int ocf_timing_event_elapsed(void* start, void* end, float* ms) {
-  OCF_TRY_BEGIN
-  OCF_CHECK(start && end && ms, "ocf_timing_event_elapsed: null pointer");
-  OCF_HIP(hipEventSynchronize((hipEvent_t)end));
-  OCF_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)end));
-  OCF_TRY_END
-}
-extern "C" int ocf_timing_event_destroy(void* ev) {
-  OCF_TRY_BEGIN
-  if (ev) OCF_HIP(hipEventDestroy((hipEvent_t)ev));
-  OCF_TRY_END
-}
-
 namespace ocf {
 
 // Split-K reductions: grid (N/64, M/4); 256 threads = 64 columns x 4 rows, one output element per

@@ -1180,42 +1180,70 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_count_kernel(OcfEpochRowListA
     }
   }
   __syncthreads();
-  int* g = a.cnt + ((int64_t)rg * a.n_sel + s) * a.n_cols + c0;
-  for (int i = threadIdx.x; i < nc; i += ERL_THREADS) g[i] = (int)((l.cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu);
+  // 16-bit counts (a column's list holds <= 4,096 entries), stored as the LDS holds them: two per word
+  uint32_t* g = reinterpret_cast<uint32_t*>(a.cnt) + (((int64_t)rg * a.n_sel + s) * a.n_cols + c0) / 2;
+  for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) g[i] = l.cnt[i];
 }
 
 // the row pointers of every batch in two passes over blocks of 4,096 columns, grid (blocks, batches): a batch's
 // scan in one workgroup walked its 138 K (Netflix: 480 K) columns serially, 65-185 us for a window of 20 batches
 constexpr int ERL_SB = 4096;   // columns per scan block (1,024 threads x 4)
 __device__ __forceinline__ int erl_nsb(const OcfEpochRowListArgs& a) { return (a.n_cols + ERL_SB - 1) / ERL_SB; }
-// cnt layout: [n_rg][n_sel][n_cols] counts, [n_sel][blocks] block totals, the long-list queue
+// cnt layout: [n_rg][n_sel][n_cols] 16-bit counts (two per int), [n_sel][blocks] block totals, the long-list queue
 __device__ __forceinline__ int* erl_btot(const OcfEpochRowListArgs& a) {
-  return a.cnt + (int64_t)erl_rg(a) * a.n_sel * a.n_cols;
+  return a.cnt + (int64_t)erl_rg(a) * a.n_sel * a.n_cols / 2;
 }
 __device__ __forceinline__ int* erl_queue(const OcfEpochRowListArgs& a) {
   return erl_btot(a) + (int64_t)a.n_sel * erl_nsb(a);
 }
 
+// the exclusive scan of a 4,096-column block's totals (4 per thread) from `base` into rp; the last block also
+// writes rp[n]
+__device__ __forceinline__ void erl_scan_block(int* rp, int4 v, int i0, int n, int base, bool last, int* wtot) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ts = v.x + v.y + v.z + v.w;
+  const int incl = wave_incl_scan(ts, lane);
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  int off = base;
+  for (int k = 0; k < w; ++k) off += wtot[k];
+  const int ex = off + incl - ts;
+  if (i0 < n) {
+    rp[i0] = ex;
+    rp[i0 + 1] = ex + v.x;
+    rp[i0 + 2] = ex + v.x + v.y;
+    rp[i0 + 3] = ex + v.x + v.y + v.z;
+  }
+  if (last && tid == 1023) rp[n] = off + incl;
+}
+
 // pass 1, per (column block, batch): each column's count summed over the row groups (the groups' counts become
-// their exclusive prefixes: the fill's cursor starts), the totals parked in row_ptr, the block's total
+// their exclusive prefixes: the fill's cursor starts), the totals parked in row_ptr, the block's total.  ONE (a
+// single block of <= 4,096 columns: ML-100K, Jester): the block's scan right here, no second pass
+template <bool ONE>
 __global__ void __launch_bounds__(1024) erl_gsum_kernel(OcfEpochRowListArgs a) {
   __shared__ int wtot[16];
   const int blk = blockIdx.x, s = blockIdx.y, n = a.n_cols, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nrg = erl_rg(a);
-  const int64_t gstride = (int64_t)a.n_sel * n;
-  int* cnt = a.cnt + (int64_t)s * n;
+  const int64_t gstride = (int64_t)a.n_sel * n / 2;   // (32-bit words of two 16-bit counts)
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(a.cnt) + (int64_t)s * n / 2;
   int* rp = a.row_ptr + (int64_t)s * (n + 1);
   if (s == 0 && blk == 0 && tid == 0) erl_queue(a)[0] = 0;   // erl_sort's long-list queue
   const int i0 = blk * ERL_SB + 4 * tid;
   int4 v = make_int4(0, 0, 0, 0);
   if (i0 < n) {                         // n % 128 == 0: all 4 columns in range or none
     for (int g = 0; g < nrg; ++g) {
-      int4* q = reinterpret_cast<int4*>(cnt + g * gstride + i0);
-      const int4 c = *q;
-      if (nrg > 1) *q = v;
-      v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+      uint2* q = reinterpret_cast<uint2*>(cnt + g * gstride + i0 / 2);
+      const uint2 c = *q;
+      // the group's counts become its exclusive prefixes (< 4,096: 16 bits)
+      if (nrg > 1) *q = make_uint2((uint32_t)v.x | ((uint32_t)v.y << 16), (uint32_t)v.z | ((uint32_t)v.w << 16));
+      v.x += (int)(c.x & 0xFFFFu); v.y += (int)(c.x >> 16); v.z += (int)(c.y & 0xFFFFu); v.w += (int)(c.y >> 16);
     }
-    rp[i0] = v.x; rp[i0 + 1] = v.y; rp[i0 + 2] = v.z; rp[i0 + 3] = v.w;
+    if (!ONE) { rp[i0] = v.x; rp[i0 + 1] = v.y; rp[i0 + 2] = v.z; rp[i0 + 3] = v.w; }
+  }
+  if (ONE) {
+    erl_scan_block(rp, v, i0, n, 0, true, wtot);
+    return;
   }
   int t = v.x + v.y + v.z + v.w;
 #pragma unroll
@@ -1248,20 +1276,8 @@ __global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
   const int i0 = blk * ERL_SB + 4 * tid;
   int4 v = make_int4(0, 0, 0, 0);
   if (i0 < n) v = make_int4(rp[i0], rp[i0 + 1], rp[i0 + 2], rp[i0 + 3]);   // the totals pass 1 parked here
-  const int ts = v.x + v.y + v.z + v.w;
-  const int incl = wave_incl_scan(ts, lane);
-  if (lane == 63) wtot[w] = incl;
   __syncthreads();
-  int off = base_s;
-  for (int k = 0; k < w; ++k) off += wtot[k];
-  const int ex = off + incl - ts;
-  if (i0 < n) {
-    rp[i0] = ex;
-    rp[i0 + 1] = ex + v.x;
-    rp[i0 + 2] = ex + v.x + v.y;
-    rp[i0 + 3] = ex + v.x + v.y + v.z;
-  }
-  if (blk == nsb - 1 && tid == 1023) rp[n] = off + incl;
+  erl_scan_block(rp, v, i0, n, base_s, blk == nsb - 1, wtot);
 }
 
 // per (column block, batch): every entry of the block's columns at its column's next slot (LDS cursors;
@@ -1270,10 +1286,9 @@ __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListAr
   const ErlLds l = erl_lds(a.B);
   const int s = blockIdx.y, rg = blockIdx.z, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
   const int nrg = erl_rg(a), b0 = rg * a.B / nrg, b1 = (rg + 1) * a.B / nrg;
-  if (nrg > 1) {      // the group's cursors start after the earlier groups' entries (erl_scan_kernel)
-    const int* pre = a.cnt + ((int64_t)rg * a.n_sel + s) * a.n_cols + c0;
-    for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS)
-      l.cnt[i] = (uint32_t)pre[2 * i] | ((uint32_t)pre[2 * i + 1] << 16);
+  if (nrg > 1) {      // the group's cursors start after the earlier groups' entries (erl_gsum_kernel)
+    const uint32_t* pre = reinterpret_cast<const uint32_t*>(a.cnt) + (((int64_t)rg * a.n_sel + s) * a.n_cols + c0) / 2;
+    for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = pre[i];
   } else {
     for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = 0u;
   }
@@ -1357,6 +1372,90 @@ __global__ void __launch_bounds__(128) erl_sort_kernel(OcfEpochRowListArgs a) {
   }
 }
 
+// bitonic sort by .x across the S lanes of a segment (S | 64, segments aligned): lane i of the segment ends with
+// the i-th smallest; every lane of the wave takes part (pad with INT_MAX keys)
+template <int S>
+__device__ __forceinline__ int2 seg_bitonic(int2 v, int i) {
+#pragma unroll
+  for (int k = 2; k <= S; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      int2 o;
+      o.x = __shfl_xor(v.x, j, 64);
+      o.y = __shfl_xor(v.y, j, 64);
+      const bool up = (i & k) == 0, lower = (i & j) == 0;
+      if (lower == up ? o.x < v.x : o.x > v.x) v = o;
+    }
+  return v;
+}
+
+// erl_sort_kernel for builds of long lists on average (ML-100K / ML-1M: ~9-16 entries per column list): a
+// thread's odd-even network over a 32-entry list costs ~500 compare-exchanges in series (22.8 us per ML-1M
+// window); here the lists are sorted across lanes -- four lists of <= 16 per wave (16-lane segments), lists of
+// 17-64 one per wave, 65-1,024 by the workgroup in LDS, longer ones queued as before.  Same live records.
+__global__ void __launch_bounds__(256) erl_sort_wave_kernel(OcfEpochRowListArgs a) {
+  __shared__ int2 buf[ERL_MID];
+  __shared__ int s_lo[128], s_n[128], mids[128];
+  __shared__ int nmid, n0s;
+  const int t = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n_cols = a.n_cols;
+  const int* rp = a.row_ptr + (int64_t)s * (n_cols + 1);
+  int2* ent = reinterpret_cast<int2*>(a.row_ent) + (a.ebase[s] - a.ebase0);
+  int n = 0;
+  if (tid < 128) {
+    const int lo = rp[t * 128 + tid];
+    n = rp[t * 128 + tid + 1] - lo;
+    s_lo[tid] = lo;
+    s_n[tid] = n;
+  }
+  if (tid == 0) nmid = 0;
+  const uint64_t bal = __ballot(n > 0);
+  if (w == 0 && lane == 0) n0s = __popcll(bal);
+  __syncthreads();
+  if (tid < 128) {
+    if (a.live) {
+      uint8_t* rec = a.live + ((int64_t)s * (n_cols / 128) + t) * OCF_LIVE_REC;
+      const int k = (w ? n0s : 0) + __popcll(bal & ((1ull << lane) - 1));
+      if (n > 0) rec[16 + (k & 7) * 16 + (k >> 3)] = (uint8_t)tid;
+      if (w == 1 && lane == 0) *reinterpret_cast<int*>(rec) = n0s + __popcll(bal);
+    }
+    if (n > ERL_MID) {
+      int* q = erl_queue(a);
+      const int qi = atomicAdd(q, 1);
+      q[1 + 2 * qi] = s;
+      q[2 + 2 * qi] = t * 128 + tid;
+    } else if (n > 64) {
+      mids[atomicAdd(&nmid, 1)] = tid;
+    }
+  }
+  // wave w: the tile's columns 32 w .. 32 w + 31
+  const int seg = lane >> 4, sl = lane & 15;
+  for (int c0 = 32 * w; c0 < 32 * w + 32; c0 += 4) {
+    const int c = c0 + seg, nn = s_n[c];
+    const bool mine = nn > 1 && nn <= 16;
+    if (!__ballot(mine)) continue;
+    int2 v = mine && sl < nn ? ent[s_lo[c] + sl] : make_int2(0x7fffffff, 0);
+    v = seg_bitonic<16>(v, sl);
+    if (mine && sl < nn) ent[s_lo[c] + sl] = v;
+  }
+  for (int c = 32 * w; c < 32 * w + 32; ++c) {
+    const int nn = s_n[c];
+    if (nn <= 16 || nn > 64) continue;
+    int2 v = lane < nn ? ent[s_lo[c] + lane] : make_int2(0x7fffffff, 0);
+    v = nn <= 32 ? seg_bitonic<32>(v, lane & 31) : seg_bitonic<64>(v, lane);
+    if (lane < nn) ent[s_lo[c] + lane] = v;
+  }
+  __syncthreads();
+  for (int q = 0; q < nmid; ++q) {        // workgroup-uniform loop over the tile's mid-length lists
+    const int c = mids[q], lq = s_lo[c], nq = s_n[c];
+    for (int i = tid; i < nq; i += 256) buf[i] = ent[lq + i];
+    __syncthreads();
+    wg_bitonic<256>(buf, nq);
+    for (int i = tid; i < nq; i += 256) ent[lq + i] = buf[i];
+    __syncthreads();
+  }
+}
+
 // one workgroup per queued list of more than ERL_MID entries (<= ERL_LONG_MAX: one per batch row)
 __global__ void __launch_bounds__(1024) erl_sort_long_kernel(OcfEpochRowListArgs a) {
   __shared__ int2 buf[ERL_LONG_MAX];
@@ -1400,11 +1499,21 @@ extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream
   const int nrg = a.n_rg > 1 ? a.n_rg : 1;
   hipLaunchKernelGGL(erl_count_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
   const int nsb = (a.n_cols + ERL_SB - 1) / ERL_SB;
-  hipLaunchKernelGGL(erl_gsum_kernel, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(erl_scan_kernel, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
+  if (nsb == 1) {
+    hipLaunchKernelGGL(erl_gsum_kernel<true>, dim3(1, a.n_sel), dim3(1024), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(erl_gsum_kernel<false>, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(erl_scan_kernel, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
+  }
   hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
-  hipLaunchKernelGGL(erl_sort_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(128), 0, s, a);
-  hipLaunchKernelGGL(erl_sort_long_kernel, dim3(64), dim3(1024), 0, s, a);
+  // lists of ~4+ entries on average: sorted across lanes (erl_sort_wave_kernel), else a thread per list
+  if (a.entries >= 4 * (int64_t)a.n_sel * a.n_cols)
+    hipLaunchKernelGGL(erl_sort_wave_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(erl_sort_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(128), 0, s, a);
+  // the long-list pass only when a list can hold more than ERL_MID entries (max_list: the caller's bound)
+  if (a.max_list <= 0 || a.max_list > ERL_MID)
+    hipLaunchKernelGGL(erl_sort_long_kernel, dim3(64), dim3(1024), 0, s, a);
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

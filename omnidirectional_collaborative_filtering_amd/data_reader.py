@@ -374,7 +374,7 @@ class BatchGenerator(object):
         # tail of an epoch) would leave most CUs idle with one workgroup per (batch, column block)
         n_rg = int(min(8, max(1, -(-ROWLIST_RG_WORK // max(n, 1)))))
         # grow-only device tables (an epoch rebuild reuses them: no allocation on the step path)
-        need = (("cnt", n_rg * n * n_cols + n * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1), torch.int32),
+        need = (("cnt", n_rg * n * n_cols // 2 + n * (n_cols // 4096 + 1) + 1 + 2 * (E // 1025 + 1), torch.int32),
                 ("row_ptr", n * (n_cols + 1), torch.int32), ("row_ent", 2 * max(E, 1), torch.int32),
                 ("live", max(n * (n_cols // 128) * _lib.LIVE_REC, 1), torch.uint8),
                 ("xval", max(E, 1), torch.float32), ("tflag", max(E, 1), torch.uint8))
@@ -389,6 +389,8 @@ class BatchGenerator(object):
         t1 = time.perf_counter()
         a = _lib.OcfEpochRowListArgs()
         a.n_sel, a.B, a.n_cols, a.n_rg, a.ebase0 = n, self.B, n_cols, n_rg, e0
+        a.max_list = self.B if self.src1.dup is None else 0       # (duplicate ratings: a list may exceed B)
+        a.entries = E
         a.rows, a.rp, a.col, a.lboff = ep["args_const"]
         a.sel, a.ebase = p_sel, p_ebase
         a.cnt, a.row_ptr, a.row_ent, a.live = bufs["cnt"][2], bufs["row_ptr"][2], bufs["row_ent"][2], bufs["live"][2]

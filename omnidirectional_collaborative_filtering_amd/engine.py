@@ -23,7 +23,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
@@ -69,36 +68,6 @@ def cur_stream():
     """the current HIP stream of the current device, as a raw pointer for the C ABI (the torch._C getters:
     torch.cuda.current_stream() costs ~8 us of Python per call, ~9 calls per training step)"""
     return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
-
-
-_TORCH_EVENTS = os.environ.get("OCF_TIMING_EVENTS") == "torch"
-
-
-class TimingEvent:
-    """A HIP timing event with a device-scope release (ocf_timing_event_*): torch.cuda.Event's record /
-    elapsed_time for the phase timers.  A default event's system-scope release writes back and invalidates the
-    L2 at every record -- ~6 us of stream idle per sampled step in bench.py's timed region.  (Library calls
-    outside the step recorder: a recorded step's calls are the one-call template.)"""
-    __slots__ = ("h",)
-
-    def __init__(self):
-        h = ctypes.c_void_p()
-        _lib.call("ocf_timing_event_create", ctypes.byref(h))
-        self.h = h.value
-
-    def record(self, stream=None):
-        _lib.call("ocf_timing_event_record", self.h, cur_stream() if stream is None else stream)
-
-    def elapsed_time(self, end):
-        ms = ctypes.c_float()
-        _lib.call("ocf_timing_event_elapsed", self.h, end.h, ctypes.byref(ms))
-        return float(ms.value)
-
-    def __del__(self):
-        try:
-            _lib.load().ocf_timing_event_destroy(self.h)
-        except Exception:          # interpreter shutdown
-            pass
 
 
 def glorot_uniform(rng, fan_in, fan_out):
@@ -407,7 +376,7 @@ class Engine:
     # ---------------------------------------------------------------- phase timing (bench.py)
     def enable_timers(self, on=True, only=None):
         """HIP-event timing of phases (every phase, or the names in `only`).  The previous timers' events go
-        back to a pool (an event costs a HIP call to create: none is created in bench.py's timed region)."""
+        back to a pool (creating an event costs HIP calls: none is created in bench.py's timed region)."""
         pool = self.__dict__.setdefault("_ev_pool", [])
         for v in (self.timers or {}).values():
             for a, b in v:
@@ -419,12 +388,9 @@ class Engine:
         pool = self.__dict__.get("_ev_pool")
         if pool:
             return pool.pop()
-        if _TORCH_EVENTS:           # A/B diagnostics: torch's (system-scope release) events
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            e.h = e.cuda_event
-            return e
-        return TimingEvent()
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()                     # (creates the event; the library records it again where it is passed)
+        return e
 
     class _Phase:
         def __init__(self, eng, name):
@@ -1575,7 +1541,7 @@ class Engine:
                 if self.timer_only is None or name in self.timer_only:
                     a, b = self._timing_event(), self._timing_event()     # (recorded by the library)
                     i0, i1 = self._EV_SLOTS[name]
-                    st.ev[i0], st.ev[i1] = a.h, b.h
+                    st.ev[i0], st.ev[i1] = a.cuda_event, b.cuda_event
                     timed.append((i0, i1, name, a, b))
         call("ocf_train_step_rows", st, cur_stream())
         for i0, i1, name, a, b in timed:
@@ -1733,7 +1699,7 @@ class Engine:
             for name, (i0, i1) in self._RANK_EV.items():
                 if self.timer_only is None or name in self.timer_only:
                     a, b = self._timing_event(), self._timing_event()     # (recorded by the library)
-                    st.ev[i0], st.ev[i1] = a.h, b.h
+                    st.ev[i0], st.ev[i1] = a.cuda_event, b.cuda_event
                     timed.append((i0, i1, name, a, b))
         s = cur_stream()
         call("ocf_rank_step", st, 0, s)

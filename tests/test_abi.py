@@ -77,7 +77,7 @@ STRUCTS = {
                                              "rtag_out", "rtag", "live_in", "live_out"]),
     "OcfEpochRowListArgs": (_lib.OcfEpochRowListArgs, ["n_sel", "B", "n_cols", "rows", "rp", "col", "lboff", "sel",
                                                        "ebase", "cnt", "row_ptr", "row_ent", "live", "n_rg",
-                                                       "ebase0"]),
+                                                       "ebase0", "max_list", "entries"]),
     "OcfEpochScatterArgs": (_lib.OcfEpochScatterArgs, ["n_sel", "sel", "ebase", "max_e", "keep_off", "stream_mul",
                                                        "xval", "tflag", "ebase0"]),
     "OcfModelDesc": (_lib.OcfModelDesc, ["n_hidden", "N", "k_blocks", "hidden", "act", "dropout", "compute_dtype",

@@ -239,6 +239,7 @@ def _gen_for(rows, cols, nnz, B, skew, seed, sparsity=(1.0, 1.0), pass_through=T
 @pytest.mark.parametrize("rows,cols,nnz,B,skew,sel", [
     (900, 4000, 30000, 128, 0.0, None),          # every batch of the epoch, short lists
     (900, 4000, 30000, 128, 0.0, [2, 3, 4]),     # consecutive batches past 0: windows of the epoch tables (ebase0)
+    (1682, 943, 100000, 256, 0.5, None),         # ML-100K-like: ~16 per list, sorted across lanes (16 / 32 / 64)
     (3000, 1024, 400000, 512, 1.0, [1, 0, 3]),   # a subset, out of order; lists up to ~500 (LDS bitonic)
     (5000, 1024, 1500000, 2048, 1.0, None),      # lists over 1,024 entries (long-list queue)
 ])
