@@ -192,3 +192,48 @@ def test_rank_step_blocks_equal_general_path(stubbed, opt, dropout, sparsity):
                 assert eng.fast_train_step(gen, bi)
     assert checked >= 12 and fast >= 5, (checked, fast)
 
+
+
+def test_row_list_window_args(stubbed, monkeypatch):
+    """BatchGenerator.prepare_row_lists: a window of consecutive batches points sel / ebase into the epoch's device
+    tables and rebases the entry offsets with ebase0 (nothing staged); any other selection is staged and starts at
+    entry 0; both pass the list-length bound and the entry count the library picks its passes by"""
+    from omnidirectional_collaborative_filtering_amd import data_reader as DR
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    r, c, v = synthetic_ratings(400, 300, 9000, half_stars=True, seed=3)
+    data = split_ratings(r, c, v, 400, 300, rng=np.random.RandomState(3), dup_free=True)
+    np.random.seed(5)
+    rd = DR.data_reader(data.num_cols, data.train.n_rows, dataset=data, eval_mode="fixed_split", rng="numpy",
+                        device=torch.device("cpu"))
+    got = {}
+
+    def fake_call(name, *args):
+        if name in ("ocf_epoch_row_lists", "ocf_epoch_scatter"):
+            a = args[0] if name == "ocf_epoch_row_lists" else args[1]
+            got[name] = type(a).from_buffer_copy(a)
+        return 0
+    monkeypatch.setattr(_lib, "call", fake_call)
+    gen = rd.data_gen(32, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+    gen._start()
+    assert gen.num_batches >= 6
+    n_cols = 384
+    eb = np.concatenate([[0], np.cumsum(gen.nnz1)])
+    for sel, window in (([2, 3, 4], True), ([4, 1], False), ([5, 3, 4, 3], True)):
+        gen.prepare_row_lists(n_cols, sel)
+        s = sorted(set(sel))
+        el, es = got["ocf_epoch_row_lists"], got["ocf_epoch_scatter"]
+        ep = gen._ep_tabs
+        E = int(gen.nnz1[s].sum())
+        assert el.n_sel == es.n_sel == len(s) and el.entries == E and el.max_list == gen.B
+        assert el.sel == es.sel and el.ebase == es.ebase and el.ebase0 == es.ebase0
+        if window:
+            assert el.sel == ep["sel_dev"].data_ptr() + 4 * s[0]
+            assert el.ebase == ep["ebase_dev"].data_ptr() + 8 * s[0]
+            assert el.ebase0 == eb[s[0]]
+        else:
+            assert el.ebase0 == 0
+            staged = ctypes.cast(el.ebase, ctypes.POINTER(ctypes.c_int64))
+            assert [staged[i] for i in range(len(s) + 1)] == [0] + list(np.cumsum(gen.nnz1[s]))
+        rl = gen._rl
+        assert rl["slot"] == {b: i for i, b in enumerate(s)}
+        np.testing.assert_array_equal(rl["ebase_host"], np.concatenate([[0], np.cumsum(gen.nnz1[s])]))
