@@ -35,6 +35,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFS = 2500.0     # dense f16/bf16 MFMA (spec)
 OPT_STATE_BYTES = {"adagrad": 16, "rmsprop": 16, "adam": 24, "sgd": 8}
 TIMER_EVERY = 4                # timed steps per dominant-kernel event sample
+TIMER_EVERY_SHORT = 10         # ... when the dominant kernel is short (< 0.1 ms): a sample's two event records idle
+                               # the stream ~11 us, ~6 % of an ML-100K step at every 4th step
 
 
 def parse():
@@ -626,14 +628,15 @@ def main():
         # start of every training epoch)
         gen.prepare_row_lists(eng.Np, [batches[(args.warmup + i) % len(batches)] for i in range(args.steps)])
     t_lists = time.perf_counter()
-    # the dominant kernel's HIP events on every TIMER_EVERY-th timed step: each event record idles the
-    # stream ~6 us (measured: 0 vs 5.8 us launch gaps with and without), so sampling keeps the timing
-    # overhead at ~0.5 % of the step while still averaging over the whole timed region
+    # the dominant kernel's HIP events on every TIMER_EVERY-th timed step (TIMER_EVERY_SHORT-th for a kernel under
+    # 0.1 ms): each event record idles the stream ~6 us (measured: 0 vs 5.8 us launch gaps with and without), so
+    # sampling keeps the timing overhead at ~0.5 % of the step while still averaging over the whole timed region
     sampled = {dom} if dom else None
+    every = TIMER_EVERY if (not dom or phases[dom]["mean_ms"] >= 0.1) else TIMER_EVERY_SHORT
     t_first = None
     for i in range(args.steps):
         if dom:
-            eng.timer_only = sampled if i % TIMER_EVERY == 0 else {"-"}
+            eng.timer_only = sampled if i % every == 0 else {"-"}
         nnz += step(args.warmup + i)
         if t_first is None:
             t_first = time.perf_counter()
@@ -770,7 +773,7 @@ def main():
                                                         / (ms_step * 1e-3), 4)},
         "phases_ms": {k: round(v["mean_ms"], 4) for k, v in phases.items()},
         "phases_from": "warm-up steps 2..%d, every phase bracketed by HIP events (timed region: only %s, "
-                       "every %d-th step)" % (w_all, dom, TIMER_EVERY),
+                       "every %d-th step)" % (w_all, dom, every),
         "setup_s": round(setup_s, 1),
         "host_issue_ms_per_step": round(host_ms, 4),
         # host time inside the timed region before the GPU has work: the row-list build's prelude (staging,

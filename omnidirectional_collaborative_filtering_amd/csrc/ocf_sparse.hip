@@ -1389,11 +1389,36 @@ __device__ __forceinline__ int2 seg_bitonic(int2 v, int i) {
   return v;
 }
 
-// erl_sort_kernel for builds of long lists on average (ML-100K / ML-1M: ~9-16 entries per column list): a
-// thread's odd-even network over a 32-entry list costs ~500 compare-exchanges in series (22.8 us per ML-1M
-// window); here the lists are sorted across lanes -- four lists of <= 16 per wave (16-lane segments), lists of
-// 17-64 one per wave, 65-1,024 by the workgroup in LDS, longer ones queued as before.  Same live records.
-__global__ void __launch_bounds__(256) erl_sort_wave_kernel(OcfEpochRowListArgs a) {
+// a wave's lists of up to 64 entries sorted in segments of S lanes (S = the longest of them, rounded up to a
+// power of two): 64 / S lists per pass, every pass's loads issued before the first sort
+template <int S>
+__device__ __forceinline__ void erl_wave_lists(int2* ent, const int* s_lo, const int* s_n, int c0, int lane) {
+  constexpr int PER = 64 / S, IT = (8 + PER - 1) / PER;
+  const int seg = lane / S, sl = lane % S;
+  int2 v[IT];
+  bool mine[IT];
+  int base[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int k = it * PER + seg;
+    const int c = c0 + (k < 8 ? k : 0), nn = s_n[c];
+    mine[it] = k < 8 && nn > 1 && nn <= 64 && sl < nn;
+    base[it] = s_lo[c];
+    v[it] = mine[it] ? ent[base[it] + sl] : make_int2(0x7fffffff, 0);
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) v[it] = seg_bitonic<S>(v[it], sl);
+#pragma unroll
+  for (int it = 0; it < IT; ++it)
+    if (mine[it]) ent[base[it] + sl] = v[it];
+}
+
+// erl_sort_kernel for builds of long lists on average (ML-100K / ML-1M: ~9-16 entries per column list), where a
+// thread per list leaves most SIMDs idle (ML-100K: 6 K lists = 96 waves) and runs an odd-even network of ~500
+// compare-exchanges in series per 32-entry list: 16 waves per 128-column tile, 8 columns per wave, the lists
+// sorted across lanes (erl_wave_lists); 65-1,024 entries by the workgroup in LDS, longer ones queued as before.
+// Same live records.
+__global__ void __launch_bounds__(1024) erl_sort_wave_kernel(OcfEpochRowListArgs a) {
   __shared__ int2 buf[ERL_MID];
   __shared__ int s_lo[128], s_n[128], mids[128];
   __shared__ int nmid, n0s;
@@ -1428,30 +1453,24 @@ __global__ void __launch_bounds__(256) erl_sort_wave_kernel(OcfEpochRowListArgs 
       mids[atomicAdd(&nmid, 1)] = tid;
     }
   }
-  // wave w: the tile's columns 32 w .. 32 w + 31
-  const int seg = lane >> 4, sl = lane & 15;
-  for (int c0 = 32 * w; c0 < 32 * w + 32; c0 += 4) {
-    const int c = c0 + seg, nn = s_n[c];
-    const bool mine = nn > 1 && nn <= 16;
-    if (!__ballot(mine)) continue;
-    int2 v = mine && sl < nn ? ent[s_lo[c] + sl] : make_int2(0x7fffffff, 0);
-    v = seg_bitonic<16>(v, sl);
-    if (mine && sl < nn) ent[s_lo[c] + sl] = v;
-  }
-  for (int c = 32 * w; c < 32 * w + 32; ++c) {
-    const int nn = s_n[c];
-    if (nn <= 16 || nn > 64) continue;
-    int2 v = lane < nn ? ent[s_lo[c] + lane] : make_int2(0x7fffffff, 0);
-    v = nn <= 32 ? seg_bitonic<32>(v, lane & 31) : seg_bitonic<64>(v, lane);
-    if (lane < nn) ent[s_lo[c] + lane] = v;
-  }
+  // wave w: the tile's columns 8 w .. 8 w + 7
+  const int c0 = 8 * w;
+  int mx = lane < 8 ? s_n[c0 + lane] : 0;
+  if (mx > 64) mx = 0;                   // (the workgroup's LDS pass)
+#pragma unroll
+  for (int o = 4; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+  mx = __shfl(mx, 0, 64);
+  if (mx > 32) erl_wave_lists<64>(ent, s_lo, s_n, c0, lane);
+  else if (mx > 16) erl_wave_lists<32>(ent, s_lo, s_n, c0, lane);
+  else if (mx > 8) erl_wave_lists<16>(ent, s_lo, s_n, c0, lane);
+  else if (mx > 1) erl_wave_lists<8>(ent, s_lo, s_n, c0, lane);
   __syncthreads();
   for (int q = 0; q < nmid; ++q) {        // workgroup-uniform loop over the tile's mid-length lists
     const int c = mids[q], lq = s_lo[c], nq = s_n[c];
-    for (int i = tid; i < nq; i += 256) buf[i] = ent[lq + i];
+    for (int i = tid; i < nq; i += 1024) buf[i] = ent[lq + i];
     __syncthreads();
-    wg_bitonic<256>(buf, nq);
-    for (int i = tid; i < nq; i += 256) ent[lq + i] = buf[i];
+    wg_bitonic<1024>(buf, nq);
+    for (int i = tid; i < nq; i += 1024) ent[lq + i] = buf[i];
     __syncthreads();
   }
 }
@@ -1508,7 +1527,7 @@ extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream
   hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
   // lists of ~4+ entries on average: sorted across lanes (erl_sort_wave_kernel), else a thread per list
   if (a.entries >= 4 * (int64_t)a.n_sel * a.n_cols)
-    hipLaunchKernelGGL(erl_sort_wave_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(erl_sort_wave_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(1024), 0, s, a);
   else
     hipLaunchKernelGGL(erl_sort_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(128), 0, s, a);
   // the long-list pass only when a list can hold more than ERL_MID entries (max_list: the caller's bound)
