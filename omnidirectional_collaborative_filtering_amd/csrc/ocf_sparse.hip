@@ -474,8 +474,10 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
   if (fold) dec_row_tail(a, jr, b, a_sh, mk_sh, a.enc_part != nullptr, solo, own, own_st, enc_arrive);
 }
 
-// (162 VGPRs, 3 waves per SIMD; capped at 128 by amdgpu_waves_per_eu(4) it spills 144 B per lane and the ML-20M
-// step went 0.388 -> 0.523 ms)
+// (f16: 133 VGPRs, bf16: 163 -- 3 waves per SIMD.  Capped at 128 by amdgpu_waves_per_eu(4) the f16 form spills 20 B
+// per lane and the ML-20M step goes 0.381 -> 0.524 ms, same box, profiles/r05_decoder_cap128_ab.jsonl; an LDS-resident
+// hidden row instead of the per-lane pieces does not lower the peak.  Round 4: 162 VGPRs, 144 B spilled, 0.388 ->
+// 0.523 ms)
 template <typename WT, typename HT, int G, int PPL>
 __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a, OcfRowsReduceArgs jr) {
   __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
