@@ -34,6 +34,10 @@ constexpr int RG_MAX_H = 512;
 #define OCF_RG_U 4
 #endif
 constexpr int RG_U = OCF_RG_U;   // entries per group in flight
+#ifndef OCF_RG_UD
+#define OCF_RG_UD 4
+#endif
+constexpr int RG_UD = OCF_RG_UD;  // ... in the decoder
 
 template <typename WT> struct EPc { static constexpr int v = 16 / (int)sizeof(WT); };
 
@@ -317,12 +321,12 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
   // entry indices one iteration ahead; the bias of each entry's column loads with its weight row.  The
   // first indices load before the hidden layer's epilogue below: that chain (partials -> activation ->
   // LDS) and this one (flag / column / target) overlap instead of running back to back
-  bool live[RG_U];
-  int n[RG_U];
-  float t[RG_U];
+  bool live[RG_UD];
+  int n[RG_UD];
+  float t[RG_UD];
   auto idx = [&](int j) {
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u) {
+    for (int u = 0; u < RG_UD; ++u) {
       const int ju = j + u * NG;
       const bool ok = ju < j1;
       live[u] = ok && a.flag[lb + ju];
@@ -391,13 +395,13 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
   float sse = 0.f, sae = 0.f, cnt = 0.f;
-  for (int j = j0 + grp; j < j1; j += NG * RG_U) {
-    uint4 w[RG_U][PPL];
-    bool lv[RG_U];
-    int nc[RG_U];
-    float tc[RG_U], bn[RG_U];
+  for (int j = j0 + grp; j < j1; j += NG * RG_UD) {
+    uint4 w[RG_UD][PPL];
+    bool lv[RG_UD];
+    int nc[RG_UD];
+    float tc[RG_UD], bn[RG_UD];
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u) {
+    for (int u = 0; u < RG_UD; ++u) {
       lv[u] = live[u];
       nc[u] = n[u];
       tc[u] = t[u];
@@ -406,10 +410,10 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
       for (int i = 0; i < PPL; ++i)
         w[u][i] = live[u] ? load_piece_raw<WT>(W, a.ldw, a.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
     }
-    idx(j + NG * RG_U);
-    float dot[RG_U];
+    idx(j + NG * RG_UD);
+    float dot[RG_UD];
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u) {
+    for (int u = 0; u < RG_UD; ++u) {
       float d0 = 0.f;
 #pragma unroll
       for (int i = 0; i < PPL; ++i) {
@@ -423,9 +427,9 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
 #pragma unroll
     for (int off = G / 2; off > 0; off >>= 1)
 #pragma unroll
-      for (int u = 0; u < RG_U; ++u) dot[u] += __shfl_xor(dot[u], off, G);
+      for (int u = 0; u < RG_UD; ++u) dot[u] += __shfl_xor(dot[u], off, G);
 #pragma unroll
-    for (int u = 0; u < RG_U; ++u) {
+    for (int u = 0; u < RG_UD; ++u) {
       const int ju = j + u * NG;
       if (ju >= j1) break;
       float d = 0.f;
