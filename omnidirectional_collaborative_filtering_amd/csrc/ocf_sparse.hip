@@ -1288,10 +1288,32 @@ __global__ void __launch_bounds__(1024) erl_scan_kernel(OcfEpochRowListArgs a) {
 
 // per (column block, batch): every entry of the block's columns at its column's next slot (LDS cursors;
 // unordered within a column, erl_sort_kernel orders each list)
+#ifndef OCF_ERL_XCD
+#define OCF_ERL_XCD 1
+#endif
+// OCF_ERL_XCD (default): a 1-D grid whose workgroups go to the 8 XCDs round robin, remapped so that the row groups
+// of one (batch, column block) -- the workgroups writing the same part of row_ent -- run on one XCD side by side
+// (their scattered 8-byte list writes then merge in that XCD's L2 instead of reaching memory as partial lines).
+// Same box, 20-step windows: ML-20M 0.3870 -> 0.3835 ms/step, Netflix 1.958 -> 1.950 (profiles/r05_window/
+// ab_fill_xcd.jsonl); 0: the (column block, batch, row group) grid
 __global__ void __launch_bounds__(ERL_THREADS) erl_fill_kernel(OcfEpochRowListArgs a, int cb) {
   const ErlLds l = erl_lds(a.B);
-  const int s = blockIdx.y, rg = blockIdx.z, c0 = blockIdx.x * cb, nc = min(cb, a.n_cols - c0);
-  const int nrg = erl_rg(a), b0 = rg * a.B / nrg, b1 = (rg + 1) * a.B / nrg;
+  const int nrg = erl_rg(a);
+  int s, rg, cbk;
+  if (OCF_ERL_XCD) {
+    const int ncb = (a.n_cols + cb - 1) / cb, T = ncb * a.n_sel * nrg, per = (T + 7) / 8;
+    const int u = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+    if (u >= T) return;
+    rg = u % nrg;
+    cbk = (u / nrg) % ncb;
+    s = u / (nrg * ncb);
+  } else {
+    s = blockIdx.y;
+    rg = blockIdx.z;
+    cbk = blockIdx.x;
+  }
+  const int c0 = cbk * cb, nc = min(cb, a.n_cols - c0);
+  const int b0 = rg * a.B / nrg, b1 = (rg + 1) * a.B / nrg;
   if (nrg > 1) {      // the group's cursors start after the earlier groups' entries (erl_gsum_kernel)
     const uint32_t* pre = reinterpret_cast<const uint32_t*>(a.cnt) + (((int64_t)rg * a.n_sel + s) * a.n_cols + c0) / 2;
     for (int i = threadIdx.x; i < nc / 2; i += ERL_THREADS) l.cnt[i] = pre[i];
@@ -1530,7 +1552,12 @@ extern "C" int ocf_epoch_row_lists(const OcfEpochRowListArgs* args, void* stream
     hipLaunchKernelGGL(erl_gsum_kernel<false>, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(erl_scan_kernel, dim3(nsb, a.n_sel), dim3(1024), 0, s, a);
   }
-  hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
+  if (OCF_ERL_XCD) {
+    const int64_t T = (int64_t)ncb * a.n_sel * nrg;
+    hipLaunchKernelGGL(erl_fill_kernel, dim3((unsigned)((T + 7) / 8 * 8)), dim3(ERL_THREADS), lds, s, a, cb);
+  } else {
+    hipLaunchKernelGGL(erl_fill_kernel, dim3(ncb, a.n_sel, nrg), dim3(ERL_THREADS), lds, s, a, cb);
+  }
   // lists of ~4+ entries on average: sorted across lanes (erl_sort_wave_kernel), else a thread per list
   if (a.entries >= 4 * (int64_t)a.n_sel * a.n_cols)
     hipLaunchKernelGGL(erl_sort_wave_kernel, dim3(a.n_cols / 128, a.n_sel), dim3(1024), 0, s, a);
