@@ -180,7 +180,15 @@ int ocf_gather_decoder(const OcfGatherArgs* args, void* stream);
  * Requires: dec.enc_part == enc.part, dec.enc_cptr (the encoder's row_cptr), the decoder's folded row reduction
  * (dec.jr + dec.row_arrive: its last chunk per row resets the counter), the same chunk table in both (ch_row /
  * ch_j0 / ch_j1 / n_chunks: a train batch, inputs = targets) and the same H.  enc_arrive: device uint32 [Bp],
- * zero before the first call, left zero.  Same results as the two calls (the same sums in the same order). */
+ * zero before the first call, left zero.  Same results as the two calls (the same sums in the same order).
+ * Fail-safe: a decoder chunk's wait is bounded (ocf_set_tuning "encdec_max_polls"; < 0 injects a give-up on
+ * batch row 0 for tests).  A chunk that gives up still counts itself in row_arrive, so the row's last chunk
+ * returns both counters to zero, stores nothing else, closes the launch's hand-off gate (a library-internal
+ * device word set to this launch's generation) and raises OCF_ASYNC_ENC_WAIT; every ocf_gemm_pair launch
+ * issued after it (pair or dual-row form) reads the gate at entry and writes no parameter, slot, shadow, bias
+ * or statistic.  The next ocf_* call reports the error once.  (An encoder chunk that arrives after the give-up
+ * would leave its row's count behind: a host that sees OCF_ASYNC_ENC_WAIT clears enc_arrive and row_arrive
+ * after synchronising, as engine.Engine does.) */
 int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* dec, uint32_t* enc_arrive, void* stream);
 
 enum { OCF_REDUCE_RAW = 0, OCF_REDUCE_BIAS_ACT = 1, OCF_REDUCE_GRAD_ACT = 2 };
@@ -683,6 +691,9 @@ int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);
  *               (ocf_optim_ws.h); 0 = the generic tile kernel.  Bit-identical results.
  *   "optim_ws_max_k": largest K (batch rows) sent to that kernel (default 256; beyond it the K-loop
  *               outgrows the optimizer stream it hides under and the generic kernel is faster).
+ *   "pair_wait_polls", "encdec_max_polls", "mlp_max_polls": the bounded in-kernel waits of ocf_gemm_pair,
+ *               ocf_gather_encdec and ocf_mlp_step (polls of ~64 cycles); the last two take a negative value as
+ *               fault injection for tests (a give-up on workgroup 0 / batch row 0).
  * previous (nullable) receives the old value. */
 int ocf_set_tuning(const char* key, int value, int* previous);
 

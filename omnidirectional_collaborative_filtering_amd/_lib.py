@@ -286,9 +286,19 @@ def load(path: str = LIB_PATH):
     return lib
 
 
+# called (no arguments) when a library call reports OCF_ASYNC_ENC_WAIT: engines register a reset of their
+# encoder -> decoder hand-off counters (an encoder chunk that arrived after its row's decoder gave up leaves a
+# count behind; ocf.h ocf_gather_encdec)
+enc_wait_hooks = []
+
+
 def call(name, *args):
     lib = load()
     rc = getattr(lib, name)(*args)
     if rc != 0:
-        raise OcfError("%s failed: %s" % (name, lib.ocf_last_error().decode()))
+        msg = lib.ocf_last_error().decode()
+        if "ocf_gather_encdec: a decoder chunk gave up" in msg:
+            for hook in list(enc_wait_hooks):
+                hook()
+        raise OcfError("%s failed: %s" % (name, msg))
     return rc

@@ -1,5 +1,6 @@
 // Split-K reductions fused with the layer epilogues, elementwise optimizers, stats reduction,
 // and the library's error state.
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -47,6 +48,32 @@ uint32_t* async_error_word() {
     g_async_dev = static_cast<uint32_t*>(d);
   }
   return g_async_dev;
+}
+
+namespace {
+uint32_t* g_gate_dev = nullptr;
+std::atomic<uint32_t> g_encdec_gen{0};
+}  // namespace
+
+uint32_t* encdec_gate_word() {
+  std::lock_guard<std::mutex> lk(g_async_mu);
+  return g_gate_dev;
+}
+uint32_t encdec_generation() { return g_encdec_gen.load(); }
+uint32_t next_encdec_generation() {
+  {
+    std::lock_guard<std::mutex> lk(g_async_mu);
+    if (!g_gate_dev) {
+      void* d = nullptr;
+      OCF_HIP(hipMalloc(&d, 64));
+      OCF_HIP(hipMemset(d, 0, 64));
+      OCF_HIP(hipDeviceSynchronize());
+      g_gate_dev = static_cast<uint32_t*>(d);
+    }
+  }
+  uint32_t g = g_encdec_gen.fetch_add(1u) + 1u;
+  if (g == 0) g = g_encdec_gen.fetch_add(1u) + 1u;   // (wrapped: 0 means "no launch")
+  return g;
 }
 
 void check_async_errors() {

@@ -284,9 +284,9 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     if (previous) *previous = g_pair_wait_polls;
     OCF_CHECK(value > 0, "ocf_set_tuning: pair_wait_polls > 0");
     g_pair_wait_polls = value;
-  } else if (k == "encdec_max_polls") {   // ocf_gather_encdec's bounded wait (tests shorten it)
+  } else if (k == "encdec_max_polls") {   // ocf_gather_encdec's bounded wait (tests: < 0 injects a give-up)
     if (previous) *previous = g_encdec_max_polls;
-    OCF_CHECK(value > 0, "ocf_set_tuning: encdec_max_polls > 0");
+    OCF_CHECK(value != 0, "ocf_set_tuning: encdec_max_polls != 0");
     g_encdec_max_polls = value;
   } else if (k == "mlp_max_polls") {      // ocf_mlp_step's bounded barrier wait (tests: < 0 injects a give-up)
     if (previous) *previous = g_mlp_max_polls;

@@ -16,6 +16,13 @@ uint32_t* async_error_word();        // device-visible address of the word (allo
 void check_async_errors();
 extern int g_mlp_max_polls;          // ocf_mlp_step's barrier wait (ocf_set_tuning "mlp_max_polls")
 extern int g_encdec_max_polls;       // ocf_gather_encdec's wait (ocf_set_tuning "encdec_max_polls")
+// The encoder -> decoder hand-off's gate (ocf_gather_encdec): a device word a decoder chunk that gave up sets to
+// its launch's generation; the row-stream weight-update launches issued after that encdec launch (the same
+// generation) read it at entry and write nothing when it matches.  The generation only grows (never 0), so no
+// launch has to clear the word.
+uint32_t* encdec_gate_word();        // device word (allocated on first use), nullptr before any encdec launch
+uint32_t encdec_generation();        // the generation of the last encdec launch issued (0: none)
+uint32_t next_encdec_generation();   // a new generation for an encdec launch being issued
 }  // namespace ocf
 
 #define OCF_TRY_BEGIN try { ocf::check_async_errors();

@@ -421,7 +421,18 @@ struct RsPair {
   uint32_t* err;              // the library's asynchronous error word (host-coherent)
   int n_a, n_prod, max_polls;
   int parts;                  // dual-row launch: workgroups per 128-row tile
+  const uint32_t* gate;       // the encoder -> decoder hand-off's gate word (nullptr: none), closed when it holds
+  uint32_t gate_gen;          // ... this generation: a decoder chunk of the step's encdec launch gave up
 };
+
+// The hand-off gate (ocf_internal.h encdec_gate_word): true when the fused encoder -> decoder launch this update
+// follows gave up on a row -- its hidden delta and statistics are not valid, so nothing may be written from them.
+// One plain load per workgroup (the word was written by an earlier kernel; the kernel start made it visible),
+// issued at entry and consumed before the first write.
+__device__ __forceinline__ bool gate_closed(const RsPair& ps) {
+  if (!ps.gate) return false;
+  return __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile uint32_t*>(ps.gate)) == ps.gate_gen;
+}
 
 // The wait: one plain load first (L2-cached: once a consumer of this XCD has seen the count complete, the
 // later ones find it there), then relaxed agent-scope loads until the count is complete.  Measured and
@@ -453,8 +464,9 @@ template <typename CT, int KIND, int CW, int NCH, int PARTS, bool LONG>
 __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwArgs ra, WsJobs ja, RowsDwArgs rb,
                                                                         WsJobs jb, RsPair ps) {
   const int bx = blockIdx.x;
+  const bool closed = gate_closed(ps);
   if (bx < ps.n_a) {
-    rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(ra, ja, bx);
+    if (!closed) rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(ra, ja, bx);
     if (bx < ps.n_prod) {
       // every wave waits for its stores to reach the L2, then ONE release (one L2 write-back per workgroup:
       // a release per wave made the wait cost ~15 us) publishes them with the count
@@ -464,7 +476,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowpipe_pair_kernel(RowsDwAr
     }
     return;
   }
-  if (!pair_wait(ps)) return;
+  if (closed || !pair_wait(ps)) return;
   rowpipe_body<CT, KIND, CW, NCH, PARTS, LONG>(rb, jb, bx - ps.n_a);
 }
 
@@ -512,11 +524,12 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   constexpr bool ADAM = KIND == OCF_OPT_ADAM;
   using Row = RdRow<CT, KIND, CW, NCH>;
   const int bx = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool closed = gate_closed(ps);   // (consumed before this workgroup's first write)
   // producers: the output side's jobs (the row reduction), published with the pair kernel's release
   const int nprod = (jo.count() + 3) / 4;
   if (bx < nprod) {
     const int j = bx * 4 + wave;
-    if (j < jo.count()) jo.run<KIND>(j, lane);
+    if (j < jo.count() && !closed) jo.run<KIND>(j, lane);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (tid == 0 && ps.n_prod) __hip_atomic_fetch_add(ps.word, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -525,7 +538,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   // consumers of the reduction's outputs: the hidden-bias update and the stats jobs
   const int ncons = (ji.count() + 3) / 4;
   if (bx < nprod + ncons) {
-    if (ps.n_prod && !pair_wait(ps)) return;
+    if (closed || (ps.n_prod && !pair_wait(ps))) return;
     const int j = (bx - nprod) * 4 + wave;
     if (j < ji.count()) ji.run<KIND>(j, lane);
     return;
@@ -634,6 +647,7 @@ __global__ void __launch_bounds__(RS_THREADS) optim_rowdual_kernel(RowsDwArgs ro
   Row r;
   if (nr > 0) start(r, 0);
   if (ps.n_prod && !pair_wait(ps)) return;   // every wave of the workgroup, once (none: the decoder reduced)
+  if (closed) return;                        // (the hand-off gave up: no parameter, slot or shadow write)
   // PF (parts < 32: waves of two or more rows): the next row's chain and parameter loads are issued before
   // this row's entry groups (ML-1M at 16 parts: register room, 3 waves per SIMD still hold every wave)
   Row rn;

@@ -124,6 +124,8 @@ bool launch_rows_pair(const OcfGemmArgs& a, const OcfGemmArgs& b, OcfPairSync& s
   ps.want = (unsigned long long)sync.count + (unsigned long long)ps.n_prod;
   ps.err = async_error_word();
   ps.max_polls = g_pair_wait_polls;
+  ps.gate = encdec_gate_word();          // (nullptr until the first ocf_gather_encdec)
+  ps.gate_gen = encdec_generation();
   if (dual) {
     ps.n_a = 0;
     const int nprod = (A.jb.count() + 3) / 4;

@@ -291,6 +291,30 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
   encoder_chunk<WT, G, PPL>(a, blockIdx.x, red, nullptr);
 }
 
+// The fused encoder -> decoder launch's hand-off (gather_encdec_kernel): enc_arrive = per-row arrival counters of
+// the encoder chunks; err = the library's asynchronous error word; gate / gen = the hand-off's gate word and this
+// launch's generation (ocf_internal.h encdec_gate_word); max_polls < 0 = fault injection (tests): row 0's decoder
+// chunks give up after their wait has completed.  enc_arrive == nullptr: not the fused launch.
+struct EncDecSync {
+  uint32_t* enc_arrive; uint32_t* err; uint32_t* gate; uint32_t gen; int max_polls;
+};
+
+// A decoder chunk that gave up waiting for its row's encoder chunks still counts itself in row_arrive[b], so the
+// row's last chunk (this one or another) finds the count complete and returns both counters to zero; it stores
+// nothing else.  The row's hidden delta is then not valid (a partial is missing): the weight-update launch that
+// follows reads the gate word this launch closed and writes nothing.
+__device__ __forceinline__ void dec_row_abandon(const OcfGatherArgs& a, const OcfRowsReduceArgs& r, int b,
+                                                uint32_t* enc_arrive) {
+  if (threadIdx.x != 0) return;
+  const uint32_t nch = (uint32_t)(r.row_cptr[b + 1] - r.row_cptr[b]);
+  const uint32_t old = nch == 1 ? 0u : __hip_atomic_fetch_add(&a.row_arrive[b], 1u, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+  if (old + 1 == nch) {
+    if (nch > 1) __hip_atomic_store(&a.row_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&enc_arrive[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // chunk c of the decoder.  enc_arrive (the fused encoder -> decoder launch): before its hidden epilogue the chunk
 // waits until every encoder chunk of its row has counted itself (bounded: OCF_ASYNC_ENC_WAIT, then the chunk
 // stores nothing) and reads their write-through partials with L1-bypassing loads.  Deadlock-free: the encoder
@@ -298,8 +322,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encoder_kernel(OcfGatherArg
 // producers are resident or done.
 template <typename WT, typename HT, int G, int PPL>
 __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfRowsReduceArgs& jr, const int c,
-                                              const bool first_wg, float* red, uint32_t* enc_arrive, uint32_t* err,
-                                              int max_polls) {
+                                              const bool first_wg, float* red, const EncDecSync& sy) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
   constexpr int NG = RG_THREADS / G;
@@ -311,6 +334,7 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
   const int64_t lb = a.lboff[b];
   const WT* W = reinterpret_cast<const WT*>(a.W);
   const float m = a.aux;
+  uint32_t* const enc_arrive = sy.enc_arrive;
   if (a.zero_word && first_wg && threadIdx.x == 0)
     __hip_atomic_store(a.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool fold = a.row_arrive != nullptr;
@@ -350,16 +374,21 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
       __shared__ int ok_sh;
       if (threadIdx.x == 0) {
         const uint32_t want = (uint32_t)(e1 - e0);
+        const int polls = sy.max_polls < 0 ? (1 << 22) : sy.max_polls;
         bool ok = __hip_atomic_load(&enc_arrive[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
-        for (int it = 0; !ok && it < max_polls; ++it) {
+        for (int it = 0; !ok && it < polls; ++it) {
           __builtin_amdgcn_s_sleep(1);
           ok = __hip_atomic_load(&enc_arrive[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
         }
-        if (!ok) __hip_atomic_store(err, (uint32_t)OCF_ASYNC_ENC_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sy.max_polls < 0 && b == 0) ok = false;   // fault injection (every encoder chunk of the row is in)
+        if (!ok) {
+          __hip_atomic_store(sy.gate, sy.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(sy.err, (uint32_t)OCF_ASYNC_ENC_WAIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         ok_sh = ok ? 1 : 0;
       }
       __syncthreads();
-      if (!ok_sh) return;
+      if (!ok_sh) return dec_row_abandon(a, jr, b, enc_arrive);
     }
     for (int x = threadIdx.x; x < a.H; x += RG_THREADS) {
       // the chunk partials of 4 chunks in flight together, added in chunk order (the same sums)
@@ -485,7 +514,7 @@ __device__ __forceinline__ void decoder_chunk(const OcfGatherArgs& a, const OcfR
 template <typename WT, typename HT, int G, int PPL>
 __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArgs a, OcfRowsReduceArgs jr) {
   __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
-  decoder_chunk<WT, HT, G, PPL>(a, jr, blockIdx.x, blockIdx.x == 0, red, nullptr, nullptr, 0);
+  decoder_chunk<WT, HT, G, PPL>(a, jr, blockIdx.x, blockIdx.x == 0, red, EncDecSync{});
 }
 
 // The encoder and the decoder as ONE launch (ocf_gather_encdec): workgroups [0, e.n_chunks) are the encoder's
@@ -493,17 +522,13 @@ __global__ void __launch_bounds__(RG_THREADS) gather_decoder_kernel(OcfGatherArg
 // (per-row arrival counters enc_arrive, reset by the row's last decoder chunk) instead of after the whole encoder
 // launch.  Needs the decoder's folded row reduction (its last chunk per row resets the counter) and the same
 // chunk table for both (train batches: inputs = targets).
-struct EncDecSync {
-  uint32_t* enc_arrive; uint32_t* err; int max_polls;
-};
 template <typename WT, typename HT, int G, int PPL>
 __global__ void __launch_bounds__(RG_THREADS) gather_encdec_kernel(OcfGatherArgs e, OcfGatherArgs d,
                                                                    OcfRowsReduceArgs jr, EncDecSync sy) {
   __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
   const int bx = blockIdx.x;
   if (bx < e.n_chunks) encoder_chunk<WT, G, PPL>(e, bx, red, sy.enc_arrive);
-  else decoder_chunk<WT, HT, G, PPL>(d, jr, bx - e.n_chunks, bx == e.n_chunks, red, sy.enc_arrive, sy.err,
-                                     sy.max_polls);
+  else decoder_chunk<WT, HT, G, PPL>(d, jr, bx - e.n_chunks, bx == e.n_chunks, red, sy);
 }
 
 // per batch row: fixed-order sum of its chunk partials, then the layer epilogue
@@ -720,7 +745,9 @@ extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* 
                 r.row_cptr && r.h_out && r.a_in && r.stats_part && r.B <= r.Bp && (r.keep >= 1.f || r.mask_in),
             "ocf_gather_encdec: jr must be OCF_REDUCE_GRAD_ACT over the decoder's part / chunk_stats");
   if (d.n_chunks == 0) return 0;
-  EncDecSync sy{enc_arrive, async_error_word(), g_encdec_max_polls};
+  EncDecSync sy{enc_arrive, async_error_word(), nullptr, 0, g_encdec_max_polls};
+  sy.gen = next_encdec_generation();
+  sy.gate = encdec_gate_word();
   hipStream_t s = (hipStream_t)stream;
   int G, ppl;
   if (d.w_dtype == OCF_F32) { shape_or_throw<float>(d, G, ppl); launch_encdec<float, float>(G, ppl, e, d, sy, s); }

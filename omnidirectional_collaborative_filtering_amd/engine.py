@@ -70,6 +70,27 @@ def cur_stream():
     return torch._C._cuda_getCurrentRawStream(torch._C._cuda_getDevice())
 
 
+def _counter_reset(engine):
+    """a hook for _lib.enc_wait_hooks that clears the engine's hand-off counters (weakly bound: a dead engine's
+    hook removes itself)"""
+    import weakref
+    ref = weakref.ref(engine)
+
+    def hook():
+        e = ref()
+        if e is None:
+            if hook in _lib.enc_wait_hooks:
+                _lib.enc_wait_hooks.remove(hook)
+            return
+        torch.cuda.synchronize(e.dev)
+        e.enc_arrive.zero_()
+        e.row_arrive.zero_()
+        torch.cuda.synchronize(e.dev)
+    hook.ref = ref
+    _lib.enc_wait_hooks[:] = [h for h in _lib.enc_wait_hooks if getattr(h, "ref", lambda: 1)() is not None]
+    return hook
+
+
 def glorot_uniform(rng, fan_in, fan_out):
     lim = math.sqrt(6.0 / (fan_in + fan_out))
     return rng.uniform(-lim, lim, size=(fan_in, fan_out)).astype(np.float32)
@@ -361,6 +382,9 @@ class Engine:
         # chunks run at the decoder's 163 VGPRs there; profiles/r05_cfg/encdec*.jsonl)
         self.fuse_enc_dec = None
         self.enc_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
+        # a decoder chunk that gives up (OCF_ASYNC_ENC_WAIT) leaves both counters at zero itself; an encoder chunk
+        # arriving after that give-up would not, so the counters are cleared when the error is reported
+        _lib.enc_wait_hooks.append(_counter_reset(self))
         # ... and dW_out + dW_in as one launch (ocf_gemm_pair: a device word the launches count up, never
         # cleared, and its host-side running count)
         self.pair_dw = True
@@ -398,6 +422,7 @@ class Engine:
 
         def __enter__(self):
             e = self.eng
+            self.prev, e._active_phase = e.__dict__.get("_active_phase"), self
             self.on = e.timers is not None and (e.timer_only is None or self.name in e.timer_only)
             if self.on:
                 self.s = e._timing_event()
@@ -405,11 +430,23 @@ class Engine:
             return self
 
         def __exit__(self, *exc):
+            self.eng._active_phase = self.prev
             if self.on:
                 e = self.eng._timing_event()
                 e.record()
                 self.eng.timers.setdefault(self.name, []).append((self.s, e))
             return False
+
+        def restart(self):
+            """the phase's interval starts here (work issued since its start belongs to another phase)"""
+            if self.on:
+                self.s.record()
+
+        def drop(self):
+            """nothing of this phase was issued: no interval is recorded"""
+            if self.on:
+                self.on = False
+                self.eng.__dict__.setdefault("_ev_pool", []).append(self.s)
 
     def phase(self, name):
         return Engine._Phase(self, name)
@@ -857,7 +894,7 @@ class Engine:
         tab = self.gt["enc"]
         Hp0 = self.Hp[0]
         part = self._buf("part_enc", tab["n_chunks"] * Hp0)
-        with self.phase("enc_gemm"):
+        with self.phase("enc_gemm") as ph:
             g = self._gather_args(tab, 0, part, Hp0)
             xv = self.gt["xval"]
             g.xval = xv if isinstance(xv, int) else ptr(xv)
@@ -868,6 +905,7 @@ class Engine:
                 # launch is deferred to the decoder's (one fused launch when the decoder can take it)
                 self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id,
                                        args=g, tab=tab)
+                ph.drop()                        # (timed where it is launched: _output_gather)
                 return
             call("ocf_gather_encoder", g, cur_stream())
             if self.comm is not None:            # partial over this rank's columns -> all-reduce
@@ -934,9 +972,14 @@ class Engine:
             fuse = self.fuse_enc_dec if self.fuse_enc_dec is not None else self.Np // TILE * 48 >= 8192
             if (fuse and g.jr and et["ch_row"] == tab["ch_row"] and et["n_chunks"] == tab["n_chunks"]
                     and et["lboff"] == tab["lboff"]):
+                # (one launch: the caller's dec_gemm_mse phase times both, enc_gemm records nothing)
                 call("ocf_gather_encdec", ea, g, ptr(self.enc_arrive), cur_stream())
                 return self._after_decoder(g, fold, r)
-            call("ocf_gather_encoder", ea, cur_stream())
+            dec_phase = self.__dict__.get("_active_phase")
+            with self.phase("enc_gemm"):
+                call("ocf_gather_encoder", ea, cur_stream())
+            if dec_phase is not None:
+                dec_phase.restart()
         call("ocf_gather_decoder", g, cur_stream())
         return self._after_decoder(g, fold, r)
 
@@ -1519,8 +1562,10 @@ class Engine:
         pl["w4"] = (np.frombuffer(raw, dtype=np.int32), np.array(o4), np.array(i4))
 
     def _fits(self, pl, f):
+        # (every template fuses the encoder's epilogue into the decoder: _forward_gather's gates apply to it too)
         return (f[self._F_NCH] <= pl["cap_enc"] and f[self._F_NCH] <= pl["cap_dec"] and f[self._F_E] <= pl["cap_e"]
-                and f[self._F_MAXCH] <= FUSE_MAX_CHUNKS and self.n_stats < self.stats_cap)
+                and f[self._F_MAXCH] <= FUSE_MAX_CHUNKS and f[self._F_NCH] <= FUSE_MEAN_CHUNKS * self.B
+                and self.n_stats < self.stats_cap)
 
     def _rewrite(self, pl, f, per):
         v = np.array(f, dtype=np.int64)

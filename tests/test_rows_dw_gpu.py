@@ -242,6 +242,10 @@ def _gen_for(rows, cols, nnz, B, skew, seed, sparsity=(1.0, 1.0), pass_through=T
     (1682, 943, 100000, 256, 0.5, None),         # ML-100K-like: ~16 per list, sorted across lanes (16 / 32 / 64)
     (3000, 1024, 400000, 512, 1.0, [1, 0, 3]),   # a subset, out of order; lists up to ~500 (LDS bitonic)
     (5000, 1024, 1500000, 2048, 1.0, None),      # lists over 1,024 entries (long-list queue)
+    # wider than one 4,096-column scan block (the two-pass block scan, the row-group prefix across blocks): the
+    # whole epoch (7 batches) and a window of three, eight row groups per batch, skewed
+    (2000, 20000, 240000, 256, 0.5, None),
+    (2000, 20000, 240000, 256, 1.0, [1, 2, 3]),
 ])
 def test_epoch_row_lists_match_numpy(gpu, rows, cols, nnz, B, skew, sel):
     """ocf_epoch_row_lists (BatchGenerator.prepare_row_lists): per selected batch and column, the batch's
@@ -599,3 +603,62 @@ def test_encdec_launch_bit_identical(gpu, cd, shape, B):
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_encdec_gives_up_safely(gpu):
+    """A decoder chunk of the fused encoder -> decoder launch that gives up waiting (injected on batch row 0:
+    ocf_set_tuning "encdec_max_polls" < 0) still counts itself, so both per-row counters are back at zero after
+    the launch; it closes the hand-off gate, so the dual-row update that follows writes no weight, bias, slot or
+    shadow; the error is reported once; and the next step equals a twin model's step on the same batch from the
+    same state (exact: Adagrad, no dropout)"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    lib = _lib.load()
+
+    def build():
+        rd, gen = _gen_for(2000, 30000, 300000, 256, 0.5, seed=21)
+        om = omni_model(1, 500, 30000, 256, dense_activation="sigmoid", use_causal_info=False,
+                        dropout_probability=None, compute_dtype="float16", seed=4)
+        om.model.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+        om.model.fit_generator(gen, 3, epochs=1, verbose=0)
+        return om, gen
+
+    def state(eng):
+        return [t.clone() for t in eng.W + eng.b + [s for sw, sb in eng.slots for s in sw + sb if s is not None]
+                + [w for w in eng.Wsh if w is not None]]
+
+    a, ga = build()
+    ea = a.engine
+    torch.cuda.synchronize()
+    s0 = state(ea)
+    prev = ctypes.c_int32()
+    _lib.call("ocf_set_tuning", b"encdec_max_polls", -1, ctypes.byref(prev))
+    try:
+        lib.ocf_set_tuning(b"rows_dual_count", 0, None)
+        a.model._train_one(ga)
+        torch.cuda.synchronize()
+        cnt = ctypes.c_int(-1)
+        lib.ocf_set_tuning(b"rows_dual_count", 0, ctypes.byref(cnt))
+        assert cnt.value == 1, "the dual-row launch did not run"
+        assert ea.step_paths["one_call"] > 0
+        # the counters, before any other library call (no host-side reset has run)
+        assert int(ea.enc_arrive.abs().sum()) == 0 and int(ea.row_arrive.abs().sum()) == 0
+        for x, y in zip(s0, state(ea)):
+            assert torch.equal(x, y)
+        assert lib.ocf_check_async() != 0 and b"ocf_gather_encdec" in lib.ocf_last_error()
+        assert lib.ocf_check_async() == 0          # reported once
+    finally:
+        lib.ocf_set_tuning(b"encdec_max_polls", prev.value, None)
+    # the next step: against a twin that trained the same 3 batches and skips the one the failed step took
+    b, gb = build()
+    assert gb.next_batch_index() is not None
+    a.model._train_one(ga)
+    b.model._train_one(gb)
+    torch.cuda.synchronize()
+    _lib.call("ocf_check_async")                   # (raises if that step gave up)
+    sa, sb = state(ea), state(b.engine)
+    assert not torch.equal(sa[0], s0[0])
+    for x, y in zip(sa, sb):
+        assert torch.equal(x, y)
+    assert int(ea.enc_arrive.abs().sum()) == 0 and int(ea.row_arrive.abs().sum()) == 0
