@@ -148,6 +148,17 @@ class _NoComm:
         return self._Work()
 
 
+def compute_label(eng, dtype, dom):
+    """what the step's arithmetic runs on (config.compute)"""
+    dt = {"float16": "f16", "bfloat16": "bf16", "float32": "fp32"}[dtype]
+    if dom == "mlp_step":
+        return "%s operands, %s MFMA, fp32 accumulate (one ocf_mlp_step launch)" % (dt, dt)
+    if eng.use_sparse and eng.sparse_ok and eng.sparse_dw:
+        return ("%s operands, fp32 VALU accumulate (row gathers for the encoder / decoder, row-stream weight "
+                "updates)" % dt)
+    return "%s operands, %s MFMA, fp32 accumulate (dense GEMMs)" % (dt, dt)
+
+
 def optim(name, lr):
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     return {"adagrad": lambda: O.Adagrad(lr=lr, epsilon=1e-8), "rmsprop": lambda: O.RMSprop(lr=lr),
@@ -244,6 +255,140 @@ def same_batch_one_gpu(args, data_full, n_rows, Bg, dev, steps=10, warmup=3):
     del om, m, eng, gen, rd
     torch.cuda.empty_cache()
     return out
+
+
+PARITY_STEPS = 3
+
+
+def _gloo():
+    import torch.distributed as dist
+    return dist.get_backend() == "gloo"
+
+
+def _bcast(t):
+    """broadcast from rank 0 (host-staged over gloo: rehearsals with every rank on one GPU)"""
+    import torch.distributed as dist
+    if _gloo():
+        h = t.cpu()
+        dist.broadcast(h, 0)
+        t.copy_(h)
+    else:
+        dist.broadcast(t, 0)
+
+
+def _all_gather(t, world):
+    import torch.distributed as dist
+    if _gloo():
+        out = [torch.zeros_like(t, device="cpu") for _ in range(world)]
+        dist.all_gather(out, t.cpu())
+        return out
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return out
+
+
+def _delta_stats(got, want, unit):
+    """max-abs, 99th and 99.9th percentile of |got - want| (device tensors), in units of `unit`"""
+    d = (got.float() - want.float()).abs().view(-1)
+    n = d.numel()
+    if n == 0:
+        return [0.0, 0.0, 0.0, 0]
+    top = torch.topk(d, min(n, n // 100 + 1)).values
+    return [float(top[0]) / unit, float(top[min(len(top) - 1, n // 100)]) / unit,
+            float(top[min(len(top) - 1, n // 1000)]) / unit, n]
+
+
+def n_rank_parity(args, m, eng, step, data_full, n_rows, Bg, shard, dev, rank, world, batches, gen):
+    """The N-rank run checks itself (feature layout): the first PARITY_STEPS steps of this job against the SAME
+    steps of a one-GPU model of the whole network built on rank 0 (the same seed, hence the same initial weights,
+    the same global batches of B x G rows, the same dropout stream).  Reported: the per-step loss difference and
+    the max-abs / 99th / 99.9th percentile weight difference after those steps, in the units and against the bars
+    of tests/parity.py -- fp32: 1e-5 absolute; f16 / bf16: loss 2e-3 / 1e-2 relative and weights within 2, 0.02,
+    0.15 of lr x steps (max, p99, p99.9; the per-element Adagrad envelope).  Runs before the warm-up, outside the
+    timed region (the steps it takes are steps of the job: the warm-up and timed steps continue from them)."""
+    from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    k = PARITY_STEPS
+    lr = 0.005 if args.optimizer == "adagrad" else 0.001
+    N = data_full.num_cols
+    H = args.hidden
+    ref = None
+    info = torch.zeros(2, dtype=torch.float64, device=dev)    # [batches match, reference ran]
+    if rank == 0:
+        st = np.random.get_state()
+        np.random.seed(1234)                  # the job's generator seed: the same permutation, the same batches
+        rd_r = data_reader(N, n_rows, dataset=data_full, eval_mode="fixed_split", rng="numpy", device=dev)
+        om_r = omni_model(1, H, N, Bg, dense_activation="sigmoid", use_causal_info=False,
+                          dropout_probability=args.dropout or None, compute_dtype=args.dtype, seed=7, device=dev)
+        m_r = om_r.model
+        m_r.compile(optim(args.optimizer, lr), "mean_squared_error")
+        gen_r = rd_r.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
+        gen_r._start()
+        np.random.set_state(st)
+        same = all(np.array_equal(np.asarray(gen_r.rows_host[batches[i % len(batches)]]),
+                                  np.asarray(gen.rows_host[batches[i % len(batches)]])) for i in range(k))
+        e_r = om_r.engine
+        for i in range(k):
+            bi = batches[i % len(batches)]
+            if not e_r.fast_train_step(gen_r, bi):
+                m_r._load(None, gen_r, bi)
+                e_r.train_step()
+        sse_r = e_r.take_stats()[:, 0]
+        torch.cuda.synchronize()
+        ref = [e_r.W[0].clone(), e_r.W[1].clone(), e_r.b[0].clone(), e_r.b[1].clone()]
+        del om_r, m_r, e_r, gen_r, rd_r
+        torch.cuda.empty_cache()
+        info[0], info[1] = float(same), 1.0
+    for i in range(k):
+        step(i)
+    sse = eng.take_stats()[:, 0]              # (summed over the column shards)
+    torch.cuda.synchronize()
+    c0, c1, _ = shard
+    Np_full = -(-N // 128) * 128
+    Hp = eng.Hp[0]
+    if rank != 0:
+        ref = [torch.empty(Np_full, Hp, device=dev), torch.empty(Np_full, Hp, device=dev),
+               torch.empty(Hp, device=dev), torch.empty(Np_full, device=dev)]
+    for t in ref + [info]:
+        _bcast(t)
+    fp32 = args.dtype == "float32"
+    unit = 1.0 if fp32 else lr * k
+    n = c1 - c0
+    rows = [_delta_stats(eng.W[0][:n, :H], ref[0][c0:c1, :H], unit),
+            _delta_stats(eng.W[1][:n, :H], ref[1][c0:c1, :H], unit),
+            _delta_stats(eng.b[0][:H], ref[2][:H], unit),
+            _delta_stats(eng.b[1][:n], ref[3][c0:c1], unit)]
+    mine = torch.tensor([x for r in rows for x in r[:3]], dtype=torch.float64, device=dev)
+    allr = _all_gather(mine, world)
+    del ref
+    torch.cuda.empty_cache()
+    if rank != 0:
+        return None
+    a = torch.stack([x.cpu() for x in allr]).numpy().reshape(world, 4, 3).max(0)     # worst rank per tensor and statistic
+    rel = [abs(float(x) - float(y)) / max(abs(float(y)), 1e-30) for x, y in zip(sse, sse_r)]
+    worst = a.max(0)
+    bars = ([1e-5, 1e-5, 1e-5] if fp32 else [2.0, 0.02, 0.15])
+    loss_bar = 1e-5 if fp32 else (2e-3 if args.dtype == "float16" else 1e-2)
+    ok = bool(info[0].item() == 1.0 and max(rel) <= loss_bar and all(w <= b for w, b in zip(worst, bars)))
+    return {"ok": ok, "steps": k, "batches_match": bool(info[0].item() == 1.0),
+            "loss_rel_diff_per_step": [float("%.3g" % r) for r in rel], "loss_bar": loss_bar,
+            "weights": {name: {"max": float("%.4g" % v[0]), "p99": float("%.4g" % v[1]), "p999": float("%.4g" % v[2])}
+                        for name, v in zip(("W1", "W_out", "b1", "b_out"), a)},
+            "weight_units": "absolute" if fp32 else "lr x steps (%g)" % unit,
+            "weight_bars": {"max": bars[0], "p99": bars[1], "p999": bars[2]},
+            "against": "one GPU, the whole model, the same seed and global batches (rank 0, before the warm-up)"}
+
+
+def replica_consistency(eng, dev, world):
+    """DP layout: after the warm-up every rank must hold the same weights (16-bit shadows, biases): per-tensor
+    float64 sums and abs-sums, all-gathered, equal on every rank"""
+    ts = [sh if sh is not None else w for w, sh in zip(eng.W, eng.Wsh)] + list(eng.b)
+    v = torch.tensor([x for t in ts for x in (float(t.double().sum()), float(t.double().abs().sum()))],
+                     dtype=torch.float64, device=dev)
+    allv = [x.cpu() for x in _all_gather(v, world)]
+    same = all(torch.equal(allv[0], x) for x in allv[1:])
+    return {"replicas_identical": bool(same), "tensors": len(ts),
+            "note": "data-parallel replicas after the warm-up (sums and abs-sums of every shadow and bias)"}
 
 
 def fp32_mode(args, data, rd, n_rows, dev, steps):
@@ -365,15 +510,37 @@ def jester_main(args):
         step(i)
     torch.cuda.synchronize()
     phases = e.phase_times_ms(skip=1 if args.warmup > 1 else 0)
-    e.enable_timers(False)
+    cand = {k: v for k, v in phases.items()
+            if k in ("dW_in", "dW_out", "dW_pair", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm", "mlp_step")}
+    dom = max(cand, key=lambda k: cand[k]["mean_ms"]) if cand else None
+    # the dominant kernel's duration inside the timed region.  The one-launch step (ocf_mlp_step): workgroup 0's
+    # constant-rate clock at the kernel's start and end, written by the kernel itself into one row per step (no
+    # event records on the stream: at ~45 us per launch an event pair's own ~5-10 us would make the sampled
+    # kernel look longer than the step); other kernels: HIP events every TIMER_EVERY_SHORT-th step
+    trace = dom == "mlp_step"
+    tr_rows = torch.zeros(args.steps, 24, dtype=torch.int64, device=dev) if trace else None
+    e.enable_timers(dom is not None and not trace, only=[dom] if dom else None)
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     nnz = 0
     for i in range(args.steps):
+        if trace:
+            e.mlp_trace = tr_rows[i]
+        elif dom:
+            e.timer_only = {dom} if i % TIMER_EVERY_SHORT == 0 else {"-"}
         nnz += step(args.warmup + i)
     t_issued = time.perf_counter()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    if trace:
+        e.mlp_trace = None
+        t = tr_rows.cpu().numpy().astype(np.float64)
+        dur = [(r[r > 0].max() - r[0]) / 100.0 for r in t if (r > 0).sum() >= 2]      # 100 MHz clock -> us
+        dom_timed = {"mean_ms": float(np.mean(dur)) * 1e-3, "n": len(dur),
+                     "source": "the kernel's own clock (workgroup 0, start to end), every timed step"} if dur else None
+    else:
+        dom_timed = e.phase_times_ms().get(dom) if dom else None
+    e.enable_timers(False)
     e.take_stats()
     ms = elapsed / args.steps * 1e3
     # algorithmic work per step: dims 200 -> 256 -> 256 -> 100, no input gradient
@@ -382,9 +549,8 @@ def jester_main(args):
     flops = sum(6.0 * B * a * b for a, b in zip(dims[:-1], dims[1:])) - 2.0 * B * dims[0] * dims[1]
     w_b = 4 if args.dtype == "float32" else 2
     step_bytes = P * (16 + 4) + w_b * (sum(a * b for a, b in zip(dims[:-1], dims[1:])) * 2) + 5 * B * N * 4
-    cand = {k: v for k, v in phases.items()
-            if k in ("dW_in", "dW_out", "dW_pair", "enc_gemm", "dec_gemm_mse", "dec_bwd_gemm", "mlp_step")}
-    dom = max(cand, key=lambda k: cand[k]["mean_ms"]) if cand else None
+    if dom is not None and not dom_timed:
+        dom = None
     line = {
         "metric": METRIC, "value": round(nnz / elapsed, 1), "unit": "ratings/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -394,7 +560,8 @@ def jester_main(args):
         "config": {"workload": "Jester omnidirectional denoising AE train step, Model.fit (BASELINE configs[4], "
                                "train_jester.py:44-79)", "rows": n, "N": N, "hidden": [H, H], "input": 2 * N,
                    "batch_per_gpu": B, "global_batch": B, "optimizer": "rmsprop", "activation": "tanh",
-                   "compute": args.dtype + " MFMA, fp32 accumulate", "parallelism": "dp1"},
+                   "compute": compute_label(e, args.dtype, "mlp_step" if e.fused_mlp else None),
+                   "parallelism": "dp1"},
         "roofline": None,
         "step_roofline": {"alg_bytes": int(step_bytes), "alg_flops": int(flops),
                           "hbm_bound_ms": round(step_bytes / (HBM_PEAK_GBS * 1e9) * 1e3, 5),
@@ -408,14 +575,16 @@ def jester_main(args):
     }
     if dom == "mlp_step":
         # the whole step in one launch (ocf_mlp_step): against the step's own bytes and flops (the binding one)
-        kms = cand[dom]["mean_ms"]
+        kms = dom_timed["mean_ms"]
         hb, mf = step_bytes / (kms * 1e-3) / 1e9, flops / (kms * 1e-3) / 1e12
         by_bytes = hb / HBM_PEAK_GBS >= mf / MFMA_F16_PEAK_TFS
         line["roofline"] = {"bound": "hbm" if by_bytes else "mfma", "achieved": round(hb if by_bytes else mf, 2),
                             "peak": HBM_PEAK_GBS if by_bytes else MFMA_F16_PEAK_TFS,
                             "unit": "GB/s" if by_bytes else "TFLOP/s",
                             "frac": round(hb / HBM_PEAK_GBS if by_bytes else mf / MFMA_F16_PEAK_TFS, 5), "traffic": None,
-                            "kernel": dom, "kernel_mean_us": round(kms * 1e3, 2), "alg_bytes_per_launch": int(step_bytes),
+                            "kernel": dom, "kernel_mean_us": round(kms * 1e3, 2), "kernel_samples": dom_timed["n"],
+                            "kernel_time_source": dom_timed.get("source", "HIP events"),
+                            "alg_bytes_per_launch": int(step_bytes),
                             "alg_flops_per_launch": int(flops),
                             "note": "the whole step of a 0.14 M-parameter model in one persistent launch (ocf_mlp_step): "
                                     "latency-bound (phases separated by grid barriers); reported, not a target"}
@@ -424,7 +593,7 @@ def jester_main(args):
         Pd = {"dW_in": dims[0] * dims[1], "dW_out": dims[2] * dims[3], "enc_gemm": dims[0] * dims[1],
               "dec_gemm_mse": dims[2] * dims[3], "dec_bwd_gemm": dims[2] * dims[3]}[dom]
         alg = Pd * (16 if dom.startswith("dW") else w_b) + 2 * B * max(dims) * w_b
-        kms = cand[dom]["mean_ms"]
+        kms = dom_timed["mean_ms"]
         line["roofline"] = {"bound": "hbm", "achieved": round(alg / (kms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                             "unit": "GB/s", "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5), "traffic": None,
                             "kernel": dom, "kernel_mean_us": round(kms * 1e3, 2), "alg_bytes_per_launch": int(alg),
@@ -459,7 +628,7 @@ SIDE_CONFIGS = [
     ("ml1m_u", ["--config", "ml1m_u", "--dtype", "bfloat16"], 240),
     ("jester", ["--config", "jester", "--dtype", "bfloat16"], 240),
     ("train_py_ml1m_h512_b128", ["--config", "ml1m", "--dtype", "float32", "--hidden", "512", "--batch", "128"], 240),
-    ("netflix", ["--config", "netflix", "--steps", "10"], 420),
+    ("netflix", ["--config", "netflix"], 420),
 ]
 
 
@@ -597,6 +766,11 @@ def main():
             eng.train_step()
         return int(nnz_of[bi])
 
+    # N > 1: this run's first steps against one GPU (feature layout), before the warm-up
+    parity = None
+    if fp and world > 1 and not args.emulate_shards:
+        parity = n_rank_parity(args, m, eng, step, data_full, n_rows, Bg, shard, dev, rank, world, batches, gen)
+
     # warm-up (untimed): every phase bracketed by HIP events -> per-phase breakdown and the dominant
     # kernel.  The timed region then brackets only that kernel, so the timers cost ~2 events/step.
     # the first W - 2 warm-up steps with every phase timed (the general path), the last two with only the dominant
@@ -650,6 +824,8 @@ def main():
                   for k, v in eng.step_paths.items()}                            # steps (and why)
     dom_timed = eng.phase_times_ms().get(dom) if dom else None
     eng.timers = None
+    if dpo is not None:
+        parity = replica_consistency(eng, dev, world)
     row_skip_used = eng._rtag_live          # (the eval batches below reset it)
     tot = torch.tensor([elapsed, float(nnz)], device=dev, dtype=torch.float64)
     if world > 1:
@@ -732,11 +908,15 @@ def main():
                             "data_gen arrays, fused masked MSE, optimizer updates")
         # HBM bytes per launch from the latest round's PMC passes (tools/pmc_traffic.py output)
         # the latest round's PMC summary that measured this kernel (r03_, r03b_, r03c_ ... sort in round order)
+        # (measured on the default workloads: ML-20M -> r*_pmc_traffic.json, Netflix -> r*_netflix_pmc_traffic.json;
+        # B = 256, f16, one GPU)
+        others = [c for c in CONFIGS if c != args.config]
         pmcs = [f for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]*_pmc_traffic.json")))
-                if dom in json.load(open(f))]
-        # (measured on the default headline workload only: ML-20M, B = 256, f16, one GPU)
-        if pmcs and world == 1 and args.config == "ml20m" and args.batch == 256 and args.dtype == "float16" \
-                and not args.emulate_shards:
+                if not any("_%s_" % c in os.path.basename(f) for c in others)
+                and (args.config == "ml20m" or "_%s_" % args.config in os.path.basename(f))
+                and dom in json.load(open(f))]
+        if pmcs and world == 1 and args.config in ("ml20m", "netflix") and args.batch == 256 and \
+                args.dtype == "float16" and args.hidden == 500 and not args.emulate_shards:
             with open(pmcs[-1]) as f:
                 tr = json.load(f).get(dom)
             if tr:
@@ -759,8 +939,9 @@ def main():
         "config": {"workload": "%s %s train step (BASELINE configs[%d])" % (args.config, "U-AutoRec" if args.config.endswith("_u")
                                                                             else "I-AutoRec", CONFIGS[args.config][0]),
                    "rows": n_rows, "N": N,
-                   "hidden": H, "batch_per_gpu": B, "global_batch": B * world, "optimizer": args.optimizer,
-                   "activation": "sigmoid", "dropout": args.dropout, "compute": args.dtype + " MFMA, fp32 accumulate",
+                   "hidden": H, "batch_per_gpu": B, "global_batch": Bg if fp else B * world,
+                   "optimizer": args.optimizer, "activation": "sigmoid", "dropout": args.dropout,
+                   "compute": compute_label(eng, args.dtype, dom),
                    "parallelism": ("feature%d" % world) if fp else ("dp%d" % world)},
         "masked_rmse": rmse,
         "roofline": roof,
@@ -796,6 +977,8 @@ def main():
                              "zero1_shards": [[int(p.numel()), int(p.numel()) // world] for p in sync.params]
                              if sync is not None else None,
                              "grad_bytes_per_step": int(sum(g.numel() * g.element_size() for g in dpo.views))}
+    if parity is not None:
+        line["n_rank_parity"] = parity
     if same_batch is not None:
         # weak scaling grows the global batch with the ranks; the same global batch on ONE GPU is the reference
         # point for the speed-up, not the B = 256 line

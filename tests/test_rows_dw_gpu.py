@@ -638,16 +638,17 @@ def test_encdec_gives_up_safely(gpu):
         lib.ocf_set_tuning(b"rows_dual_count", 0, None)
         a.model._train_one(ga)
         torch.cuda.synchronize()
-        cnt = ctypes.c_int(-1)
-        lib.ocf_set_tuning(b"rows_dual_count", 0, ctypes.byref(cnt))
-        assert cnt.value == 1, "the dual-row launch did not run"
         assert ea.step_paths["one_call"] > 0
         # the counters, before any other library call (no host-side reset has run)
         assert int(ea.enc_arrive.abs().sum()) == 0 and int(ea.row_arrive.abs().sum()) == 0
         for x, y in zip(s0, state(ea)):
             assert torch.equal(x, y)
+        # (every entry point reports a pending error first, so this is the first library call after the step)
         assert lib.ocf_check_async() != 0 and b"ocf_gather_encdec" in lib.ocf_last_error()
         assert lib.ocf_check_async() == 0          # reported once
+        cnt = ctypes.c_int(-1)
+        _lib.call("ocf_set_tuning", b"rows_dual_count", 0, ctypes.byref(cnt))
+        assert cnt.value == 1, "the dual-row launch (which found the gate closed) did not run"
     finally:
         lib.ocf_set_tuning(b"encdec_max_polls", prev.value, None)
     # the next step: against a twin that trained the same 3 batches and skips the one the failed step took
