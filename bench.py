@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--fuse-enc-dec", type=int, default=-1,
                     help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches; -1: "
                          "the engine's choice, large weights)")
+    ap.add_argument("--enc-tiles", type=int, default=-1,
+                    help="the encoder over column tiles on the matrix cores (ocf_encoder_tiles; 1), the row gathers (0), "
+                         "or the engine's choice by entries per weight row (-1)")
     ap.add_argument("--gather-chunk", type=int, default=0,
                     help="entries per row-gather chunk of large batches (0: data_reader.GATHER_CHUNK)")
     ap.add_argument("--fold-reduce", type=int, default=1,
@@ -722,6 +725,8 @@ def main():
         eng.fuse_enc_dec = bool(args.fuse_enc_dec)
     if args.reduce_in_decoder >= 0:
         eng.reduce_in_decoder = bool(args.reduce_in_decoder)
+    if args.enc_tiles >= 0:
+        eng.enc_tiles = bool(args.enc_tiles)
     eng.split_dw_streams = bool(args.split_dw)
     eng.fuse_enc_epilogue = bool(args.fuse_enc)
     eng.epoch_row_lists = bool(args.epoch_lists)

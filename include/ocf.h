@@ -191,6 +191,30 @@ int ocf_gather_decoder(const OcfGatherArgs* args, void* stream);
  * after synchronising, as engine.Engine does.) */
 int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* dec, uint32_t* enc_arrive, void* stream);
 
+/* ocf_encoder_tiles -- the encoder's X W1 (model.py:64-71) as an MFMA contraction over 128-column tiles of W1, for
+ * batches whose weight rows carry many entries (Netflix width, feature-parallel ranks): each W1 tile is read once
+ * per 256 batch rows (the row gathers read a W1 row per entry) and multiplied by the batch's X tile, densified in
+ * LDS from the rows' column-sorted entries.  Writes split-K partials part[b][s][h] (s < splits: contiguous tile
+ * ranges); the caller sums them with ocf_rows_reduce (row_cptr[b] = b * splits).  X = the live input values
+ * (xval, list order; duplicates added) rounded to the compute dtype; fp32 accumulation. */
+typedef struct OcfEncTileArgs {
+  const int32_t* rows;    /* [B] dataset row per batch row (-1 = none)                                      */
+  const int64_t* rp;      /* row pointers of the dataset CSR                                                */
+  const int32_t* tptr;    /* [rows][n_tiles + 1] per-row tile pointers of the column-sorted view (RatingsCSR.tile_index) */
+  const int32_t* tcol;    /* view: column of each entry (row-relative positions from rp)                    */
+  const int32_t* tlidx;   /* view: the entry's index in the row's list order                                */
+  const int64_t* lboff;   /* [B + 1] batch-local offset of each row's entries                              */
+  const float* xval;      /* per batch-local entry: live input value (0 = not an input)                    */
+  const void* W;          /* 16-bit weight shadow, row-major [n_tiles * 128][ldw]                           */
+  int64_t ldw; int w_dtype;
+  int B, Bp;              /* real batch rows, padded rows (multiple of 128)                                 */
+  int n_tiles;            /* 128-column tiles                                                               */
+  int H;                  /* hidden width (multiple of 128)                                                 */
+  int splits;             /* tile ranges (split-K)                                                          */
+  float* part;            /* [Bp][splits][H] fp32                                                           */
+} OcfEncTileArgs;
+int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream);
+
 enum { OCF_REDUCE_RAW = 0, OCF_REDUCE_BIAS_ACT = 1, OCF_REDUCE_GRAD_ACT = 2 };
 
 typedef struct OcfRowsReduceArgs {

@@ -68,6 +68,14 @@ class OcfEpochRowListArgs(ctypes.Structure):
     ]
 
 
+class OcfEncTileArgs(ctypes.Structure):
+    _fields_ = [
+        ("rows", P), ("rp", P), ("tptr", P), ("tcol", P), ("tlidx", P), ("lboff", P), ("xval", P),
+        ("W", P), ("ldw", I64), ("w_dtype", I32), ("B", I32), ("Bp", I32), ("n_tiles", I32), ("H", I32),
+        ("splits", I32), ("part", P),
+    ]
+
+
 class OcfGatherArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("col", P), ("val", P), ("lboff", P), ("xval", P), ("flag", P),
@@ -259,6 +267,7 @@ SIGNATURES = {
     "ocf_backward": (I32, [P, P, I64, I32, F32, P, P, P]),
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_check_async": (I32, []),
+    "ocf_encoder_tiles": (I32, [ctypes.POINTER(OcfEncTileArgs), P]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

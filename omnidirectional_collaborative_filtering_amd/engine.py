@@ -50,6 +50,12 @@ FUSE_MAX_CHUNKS = 256
 # partials (O(chunks^2) per row).  Netflix (~22 chunks per row): 2.029 -> 1.997 ms/step with the separate launch
 # (profiles/r05_cfg/nf_base.jsonl); ML-20M (~3): the fused form
 FUSE_MEAN_CHUNKS = 8
+# the encoder as an MFMA contraction over 128-column tiles of W1 (ocf_encoder_tiles) instead of row gathers: when
+# a weight row carries this many batch entries on average (the gathers read a W1 row per entry, the tiles read
+# each tile once per 256 batch rows) on a weight of at least ENC_TILES_MIN_TILES tiles, 16-bit compute
+ENC_TILES_MIN_ENTRIES = 2.0
+ENC_TILES_MIN_TILES = 64
+ENC_TILES_WGS = 256           # workgroups to aim for (one per CU): splits = WGS / (row groups x hidden slices)
 DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
           "bfloat16": (_lib.DT_BF16, torch.bfloat16)}
 DTYPE_ALIASES = {"f32": "float32", "fp32": "float32", "f16": "float16", "fp16": "float16", "half": "float16",
@@ -382,6 +388,11 @@ class Engine:
         # chunks run at the decoder's 163 VGPRs there; profiles/r05_cfg/encdec*.jsonl)
         self.fuse_enc_dec = None
         self.enc_arrive = torch.zeros(Bp, device=d, dtype=torch.int32)
+        # the encoder over column tiles on the matrix cores (ocf_encoder_tiles): None = where weight rows carry
+        # many entries (ENC_TILES_MIN_ENTRIES), True / False forced
+        self.enc_tiles = None
+        self._enc_tiles_used = False
+        self.enc_tiles_count = 0      # (diagnostics: ocf_encoder_tiles launches)
         # a decoder chunk that gives up (OCF_ASYNC_ENC_WAIT) leaves both counters at zero itself; an encoder chunk
         # arriving after that give-up would not, so the counters are cleared when the error is reported
         _lib.enc_wait_hooks.append(_counter_reset(self))
@@ -889,10 +900,64 @@ class Engine:
         r.part, r.row_cptr, r.B, r.Bp, r.H, r.mode = ptr(part), tab["row_cptr"], self.B, self.Bp, H, mode
         return r
 
+    def _enc_tiles_ok(self):
+        """the encoder over column tiles (ocf_encoder_tiles) for this batch"""
+        Wt, wdt = self._wop(0)
+        # (train batches: the target view the kernel reads is then the input CSR's own, inputs = targets)
+        if (self.k != 1 or wdt == _lib.DT_F32 or self._wblk(0) or self.tseg is None or "t_tptr" not in self.tseg
+                or "row_lists" not in self.gt):
+            return False
+        if self.enc_tiles is not None:
+            return bool(self.enc_tiles)
+        return self.n_tiles >= ENC_TILES_MIN_TILES and self.gt["E"] >= ENC_TILES_MIN_ENTRIES * self.Np
+
+    def _enc_splits(self, Hp0):
+        n_rg, n_hs = -(-self.Bp // 256), Hp0 // 128
+        S = max(1, min(self.n_tiles, round(ENC_TILES_WGS / (n_rg * n_hs))))
+        while (n_hs * S) % 8 and S < self.n_tiles:          # whole groups of 8 (one per XCD)
+            S += 1
+        return S
+
+    def _encoder_tiles(self, part_name, Hp0, xv):
+        """ocf_encoder_tiles -> split-K partials [Bp][S][Hp0] and their row table (row_cptr[b] = b S)"""
+        S = self._enc_splits(Hp0)
+        part = self._buf(part_name, self.Bp * S * Hp0)
+        t = self.tseg
+        a = _lib.OcfEncTileArgs()
+        a.rows, a.rp, a.tptr, a.tcol, a.tlidx, a.lboff = (t["t_rows"], t["t_rp"], ptr(t["t_tptr"]), ptr(t["t_col"]),
+                                                          ptr(t["t_lidx"]), t["t_lboff"])
+        a.xval = xv
+        Wt, wdt = self._wop(0)
+        a.W, a.ldw, a.w_dtype = ptr(Wt), Wt.shape[1], wdt
+        a.B, a.Bp, a.n_tiles, a.H, a.splits, a.part = self.B, self.Bp, self.n_tiles, Hp0, S, ptr(part)
+        call("ocf_encoder_tiles", a, cur_stream())
+        cp = self._gbuf.get("tile_cptr_%d" % S)
+        if cp is None:
+            cp = self._gbuf["tile_cptr_%d" % S] = torch.arange(0, (self.Bp + 1) * S, S, device=self.dev,
+                                                                dtype=torch.int32)
+        self._enc_tiles_used = True
+        self.enc_tiles_count += 1
+        return part, ptr(cp)
+
     def _forward_gather(self, keep, stream_id):
         """layer 0 as a row gather over the batch's live input entries + fused bias/act/dropout"""
         tab = self.gt["enc"]
         Hp0 = self.Hp[0]
+        self._enc_tiles_used = False
+        if self._enc_tiles_ok():
+            with self.phase("enc_gemm"):
+                xv = self.gt["xval"]
+                part, cptr = self._encoder_tiles("part_enc", Hp0, xv if isinstance(xv, int) else ptr(xv))
+                r = self._reduce_args(dict(tab, row_cptr=cptr), part, Hp0,
+                                      _lib.REDUCE_RAW if self.comm is not None else _lib.REDUCE_BIAS_ACT)
+                if self.comm is not None:        # partial over this rank's columns -> all-reduce
+                    r.out = ptr(self.hpre)
+                else:
+                    r.bias, r.act, r.keep, r.seed, r.stream = ptr(self.b[0]), self.act, keep, self.seed, stream_id
+                    r.mask_out = ptr(self.mask[0]) if keep < 1 else None
+                    r.a_out, r.h_out, r.h_dtype, r.n_real = ptr(self.a[0]), ptr(self.h[0]), self.cdt, self.H[0]
+                call("ocf_rows_reduce", r, cur_stream())
+            return
         part = self._buf("part_enc", tab["n_chunks"] * Hp0)
         with self.phase("enc_gemm") as ph:
             g = self._gather_args(tab, 0, part, Hp0)
