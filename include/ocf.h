@@ -212,6 +212,8 @@ typedef struct OcfEncTileArgs {
   int H;                  /* hidden width (multiple of 128)                                                 */
   int splits;             /* tile ranges (split-K)                                                          */
   float* part;            /* [Bp][splits][H] fp32                                                           */
+  int64_t nnz;            /* entries of the view, n_entries: entries of xval (bounds of the clamped loads)  */
+  int64_t n_entries;
 } OcfEncTileArgs;
 int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream);
 

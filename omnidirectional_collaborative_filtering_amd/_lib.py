@@ -72,7 +72,7 @@ class OcfEncTileArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("tcol", P), ("tlidx", P), ("lboff", P), ("xval", P),
         ("W", P), ("ldw", I64), ("w_dtype", I32), ("B", I32), ("Bp", I32), ("n_tiles", I32), ("H", I32),
-        ("splits", I32), ("part", P),
+        ("splits", I32), ("part", P), ("nnz", I64), ("n_entries", I64),
     ]
 
 

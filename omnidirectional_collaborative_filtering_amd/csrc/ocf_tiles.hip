@@ -13,17 +13,18 @@
 // every MFMA operand of the dense path is.
 //
 // Workgroup (256 threads, 4 waves) = (row group of 256 batch rows, hidden slice of 128, split s).  Per tile t:
-//   * the W1 tile [128 columns][128 hidden] (32 KB, 16-bit shadow, row-major) is staged through LDS in its
-//     natural row layout with the 256-B-row XOR swizzle and read as the MFMA B operand by the transposing
-//     ds_read_b64_tr_b16 (8 consecutive columns of one hidden unit per lane);
+//   * the W1 tile [128 columns][128 hidden] (32 KB, 16-bit shadow, row-major) goes to LDS by direct-to-LDS loads
+//     (global_load_lds_dwordx4: no registers, double-buffered, the next tile's in flight during this tile's
+//     MFMAs) in its natural row layout with the 256-B-row XOR swizzle, and is read as the MFMA B operand by the
+//     transposing ds_read_b64_tr_b16 (8 consecutive columns of one hidden unit per lane);
 //   * the X tile [256 rows][128 columns] lives in LDS (64 KB, row-swizzled for the ds_read_b128 A reads): thread
 //     b owns row b and writes its <= 8 entries of the tile (the row's column-sorted view, 128-column tile
 //     pointers), then clears exactly those positions after the tile's MFMAs;
 //   * wave w computes rows [64 w, 64 w + 64) x the 128 hidden units: 2 x 4 tiles of v_mfma_f32_32x32x16, fp32
 //     accumulators in registers across all tiles of the split.
-// The next tile's W1 loads, its entries' values and the entry indices of the tile after it are issued before the
-// current tile's MFMAs (a three-stage pipeline of the dependent chain tile pointer -> column / list index ->
-// value), so one workgroup per CU keeps its HBM reads in flight.  Rows with more than ET_EMAX entries in a tile
+// The entries go through a branch-free pipeline (clamped addresses, masked results) of the dependent chain tile
+// pointer (4 tiles ahead) -> column / list index (2 ahead) -> value (1 ahead), every stage's loads issued before
+// the current tile's MFMAs, so one workgroup per CU keeps its reads in flight.  Rows with more than ET_EMAX entries in a tile
 // take a slow path for the rest (rare: ~1.2 entries per row per tile at Netflix width).
 #include <hip/hip_runtime.h>
 
@@ -63,16 +64,13 @@ template <> struct Frag<__bf16> {
   __device__ static f16v mfma(T a, T b, f16v c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 };
 
-struct Rows {          // a thread's batch row
-  int64_t rp0, lb;     // start of the dataset row in the view, the batch-local entry offset
-  const int32_t* tp;   // the row's tile pointers (nullptr: no entries)
-};
-
 template <typename CT>
 __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_rg, int n_q, int tiles_per) {
-  __shared__ __attribute__((aligned(16))) char lds[BM * ROWB + BK * ROWB];
-  char* const xs = lds;
-  char* const ws = lds + BM * ROWB;
+  // three separate LDS objects: the compiler then knows a direct-to-LDS load into one W buffer does not alias the
+  // reads of the other or of the X image, and does not wait for it (vmcnt) before them
+  __shared__ __attribute__((aligned(16))) char xs[BM * ROWB];
+  __shared__ __attribute__((aligned(16))) char wsA[BK * ROWB];
+  __shared__ __attribute__((aligned(16))) char wsB[BK * ROWB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // workgroups -> (row group, hidden slice, split): the row groups of one (slice, split) -- readers of the same
   // W1 tiles -- on one XCD (blockIdx round-robins over the 8 XCDs), so the second and later reads hit its L2
@@ -91,100 +89,109 @@ __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_
   const int h0 = hs * BH;
   using F = Frag<CT>;
   using FT = typename F::T;
-  // ---- this thread's batch row
-  Rows me{0, 0, nullptr};
+  // ---- this thread's batch row (rows without entries read row 0's pointers, masked: every load is branch-free)
+  int64_t rp0 = 0, lb = 0;
+  bool live = false;
+  const int32_t* tp = a.tptr;
   {
     const int b = rg * BM + tid;
-    if (b < a.B) {
-      const int r = a.rows[b];
-      if (r >= 0) {
-        me.rp0 = a.rp[r];
-        me.lb = a.lboff[b];
-        me.tp = a.tptr + (int64_t)r * (a.n_tiles + 1);
-      }
+    const int rr = b < a.B ? a.rows[b] : -1;
+    live = rr >= 0;
+    if (live) {
+      rp0 = a.rp[rr];
+      lb = a.lboff[b];
+      tp = a.tptr + (int64_t)rr * (a.n_tiles + 1);
     }
   }
-  // ---- W1 tile staging: 16 rows x 16 chunks per pass, 8 passes
-  const int wrow = tid >> 4, wch = tid & 15;
+  // ---- W1 tiles: direct-to-LDS loads (global_load_lds_dwordx4, no registers), two buffers.  Instruction i of wave
+  // w fills 1 KB = rows n0 .. n0 + 3 (n0 = 4 (4 i + w)) of the image; lane L lands at slot L % 16 of row n0 + L / 16,
+  // so it loads the global chunk that the swizzle puts there
   const char* Wb = reinterpret_cast<const char*>(a.W);
-  auto wload = [&](int t, uint4 (&v)[8]) {
+  auto wload = [&](int t, char* dst) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int64_t n = (int64_t)t * BK + wrow + 16 * i;
-      v[i] = *reinterpret_cast<const uint4*>(Wb + (n * a.ldw + h0) * 2 + 16 * wch);
+      const int n0 = 4 * (4 * i + wave), n = n0 + (lane >> 4), c = (lane & 15) ^ (((n & 3) << 2) | ((n >> 2) & 3));
+      const char* src = Wb + (((int64_t)t * BK + n) * a.ldw + h0) * 2 + 16 * c;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + n0 * ROWB), 16, 0, 0);
     }
   };
-  auto wstore = [&](const uint4 (&v)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(ws + woff(wrow + 16 * i, wch)) = v[i];
-  };
-  // ---- the entry chain: tile pointers (4 tiles ahead) -> columns / list indices (2 ahead) -> values (1 ahead)
-  auto tpl = [&](int t) { return (me.tp && t <= t1) ? me.tp[t] : 0; };
-  int tpA = tpl(t0), tpB = tpl(t0 + 1), tpC = tpl(t0 + 2), tpD = tpl(t0 + 3);   // tp[t], tp[t+1], ...
-  int cl0[EMAX], li0[EMAX], n0;      // tile t+1's columns / list indices (for the values)
-  int cl1[EMAX], li1[EMAX], n1;      // tile t+2's
-  float xv[EMAX];                    // tile t+1's values
-  int cw[EMAX], nw = 0;              // the positions this thread wrote for the current tile (to clear)
-  bool over_w = false;
-  auto idx = [&](int lo, int hi, int (&cl)[EMAX], int (&li)[EMAX]) {
-    const int n = hi - lo;
+  // ---- the entry chain, branch-free (clamped addresses, masked results): tile pointers 4 tiles ahead, the packed
+  // (column in tile | list index << 7) of the entries 2 ahead, their values 1 ahead
+  const int64_t last = a.nnz - 1, elast = a.n_entries - 1;
+  auto tpl = [&](int t) { return live ? tp[min(t, t1)] : 0; };
+  // (the loads' results are not touched here -- the caller packs them a stage later -- so nothing waits for them)
+  auto idx = [&](int lo, int (&col)[EMAX], int (&li)[EMAX]) {
 #pragma unroll
     for (int e = 0; e < EMAX; ++e) {
-      const bool ok = e < n;
-      cl[e] = ok ? a.tcol[me.rp0 + lo + e] : 0;
-      li[e] = ok ? a.tlidx[me.rp0 + lo + e] : 0;
+      const int64_t v = min(rp0 + lo + e, last);
+      col[e] = a.tcol[v];
+      li[e] = a.tlidx[v];
     }
-    return n;
   };
-  auto vals = [&](int n, const int (&li)[EMAX]) {
+  auto pack = [&](int t, int n, const int (&col)[EMAX], const int (&li)[EMAX], int (&pk)[EMAX]) {
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e) xv[e] = e < n ? a.xval[me.lb + li[e]] : 0.f;
+    for (int e = 0; e < EMAX; ++e) pk[e] = e < n ? ((col[e] - t * BK) & 127) | (li[e] << 7) : -1;
   };
-  // write the tile's entries into row tid of the X image (t: the tile, lo: its first entry in the view)
-  auto xwrite = [&](int t, int n, int lo, const int (&cl)[EMAX]) {
-    nw = n < EMAX ? n : EMAX;
-    over_w = n > EMAX;
-    // (added, not stored: a duplicate rating's entries meet in one column, and the gathers sum over entries)
-    auto put = [&](int kk, float x) {
-      CT* p = reinterpret_cast<CT*>(xs + xoff(tid, kk >> 3) + 2 * (kk & 7));
-      *p = CvtT<CT>::to(CvtT<CT>::from(*p) + x);
-    };
+  // (raw loads, masked where they are used: xwrite skips pk < 0 -- a select here would wait for the loads)
+  auto vals = [&](const int (&pk)[EMAX], float (&xv)[EMAX]) {
 #pragma unroll
-    for (int e = 0; e < EMAX; ++e)
-      if (e < n) {
-        const int kk = cl[e] - t * BK;
-        cw[e] = kk;
-        put(kk, xv[e]);
-      }
+    for (int e = 0; e < EMAX; ++e) xv[e] = a.xval[min(lb + (pk[e] >= 0 ? (pk[e] >> 7) : 0), elast)];
+  };
+  // (added, not stored: a duplicate rating's entries meet in one column, and the gathers sum over entries)
+  auto put = [&](int kk, float x) {
+    CT* p = reinterpret_cast<CT*>(xs + xoff(tid, kk >> 3) + 2 * (kk & 7));
+    *p = CvtT<CT>::to(CvtT<CT>::from(*p) + x);
+  };
+  int cw[EMAX];                      // the positions written for the current tile (cleared after its MFMAs)
+  bool over = false;
+  auto xwrite = [&](int t, int n, int lo, const int (&pk)[EMAX], const float (&xv)[EMAX]) {
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      cw[e] = pk[e];
+      if (pk[e] >= 0) put(pk[e] & 127, xv[e]);
+    }
+    over = n > EMAX;
     for (int e = EMAX; e < n; ++e)                    // (rare) the rest of a long row
-      put(a.tcol[me.rp0 + lo + e] - t * BK, a.xval[me.lb + a.tlidx[me.rp0 + lo + e]]);
+      put(a.tcol[rp0 + lo + e] - t * BK, a.xval[lb + a.tlidx[rp0 + lo + e]]);
   };
   auto xclear = [&]() {
-    if (over_w) {
+    if (over) {
 #pragma unroll
       for (int ch = 0; ch < 16; ++ch) *reinterpret_cast<uint4*>(xs + xoff(tid, ch)) = make_uint4(0, 0, 0, 0);
     } else {
 #pragma unroll
       for (int e = 0; e < EMAX; ++e)
-        if (e < nw) *reinterpret_cast<CT*>(xs + xoff(tid, cw[e] >> 3) + 2 * (cw[e] & 7)) = CvtT<CT>::to(0.f);
+        if (cw[e] >= 0)
+          *reinterpret_cast<CT*>(xs + xoff(tid, (cw[e] & 127) >> 3) + 2 * (cw[e] & 7)) = CvtT<CT>::to(0.f);
     }
   };
-  // ---- prologue: clear the X image, stage tile t0
+  // ---- prologue: clear the X image; tile t0 staged, t0 + 1's entries and values, t0 + 2's entries in flight
   for (int i = tid; i < BM * ROWB / 16; i += 256) reinterpret_cast<uint4*>(xs)[i] = make_uint4(0, 0, 0, 0);
+  wload(t0, wsA);
+  int tq[5];                                          // tp[t + 1 .. t + 5] while processing tile t
+  const int tp0 = tpl(t0);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) tq[i] = tpl(t0 + 1 + i);
+  int P1[EMAX], P2[EMAX], C2[EMAX], L2[EMAX];
+  float X1[EMAX];
+  int n1 = tq[1] - tq[0], n2 = tq[2] - tq[1];
   {
-    uint4 v[8];
-    wload(t0, v);
-    n0 = idx(tpA, tpB, cl0, li0);
-    vals(n0, li0);
+    int P0[EMAX], C0[EMAX], L0[EMAX];
+    float X0[EMAX];
+    const int n0 = tq[0] - tp0;
+    idx(tp0, C0, L0);
+    pack(t0, n0, C0, L0, P0);
+    vals(P0, X0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    wstore(v);
-    xwrite(t0, n0, tpA, cl0);
+    xwrite(t0, n0, tp0, P0, X0);
+    idx(tq[0], C0, L0);
+    pack(t0 + 1, n1, C0, L0, P1);
   }
-  // tile t0 + 1's indices and values, t0 + 2's indices
-  n0 = idx(tpB, tpC, cl0, li0);
-  n1 = idx(tpC, tpD, cl1, li1);
-  vals(n0, li0);
-  int tpE = tpl(t0 + 4);
+  idx(tq[1], C2, L2);
+  pack(t0 + 2, n2, C2, L2, P2);
+  vals(P1, X1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // ---- MFMA state
   f16v acc[2][4];
@@ -195,29 +202,33 @@ __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][c][k] = 0.f;
   const int r = lane & 31, hf = lane >> 5, g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
-  for (int t = t0; t < t1; ++t) {
+  // one tile: t's MFMAs from wcur while t + 1's W1 tile streams into wnext; false after the split's last tile
+  auto step = [&](int t, const char* wcur, char* wnext) -> bool {
     const bool more = t + 1 < t1;
-    uint4 wn[8];
-    if (more) wload(t + 1, wn);
-    // (the entry chain of the tiles ahead is already in flight: values of t + 1, indices of t + 2)
+    if (more) wload(t + 1, wnext);
+    // tile t + 3's entries (tile pointers t + 3, t + 4; packed after this tile's MFMAs) and tile t + 6's pointer
+    int C3[EMAX], L3[EMAX];
+    const int n3 = tq[3] - tq[2];
+    idx(tq[2], C3, L3);
+    const int tnew = tpl(t + 6);
+    const char* wsb = wcur;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       FT fa[2], fb[4];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = 64 * wave + 32 * i + r;
-        __builtin_memcpy(&fa[i], xs + xoff(row, 2 * ks + hf), 16);
+        fa[i] = *reinterpret_cast<const FT*>(xs + xoff(row, 2 * ks + hf));
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        s4 lo, hi;
         const int ch = 4 * c + 2 * (g & 1) + (gp >> 1);
-        const int n0r = 16 * ks + 8 * (g >> 1) + gq;
-        lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s4*)(ws + woff(n0r, ch) + 8 * (gp & 1)));
-        hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s4*)(ws + woff(n0r + 4, ch) + 8 * (gp & 1)));
-        short e[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const int nr = 16 * ks + 8 * (g >> 1) + gq;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(wsb + woff(nr, ch) + 8 * (gp & 1)));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(wsb + woff(nr + 4, ch) + 8 * (gp & 1)));
+        const short e[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         __builtin_memcpy(&fb[c], e, 16);
       }
 #pragma unroll
@@ -225,23 +236,27 @@ __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[i][c] = F::mfma(fa[i], fb[c], acc[i][c]);
     }
-    if (!more) break;
-    // next stage of the entry chain (issued before the barrier: its loads overlap the other waves' MFMAs)
-    int cl2[EMAX], li2[EMAX];
-    const int n2 = idx(tpD, tpE, cl2, li2);           // tile t + 3's indices
-    const int tpF = tpl(t + 5);
+    if (!more) return false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t + 1's W1 image, t + 3's entries, t + 2's values
     __syncthreads();                                  // every wave is done with tile t's images
     xclear();
-    wstore(wn);
-    xwrite(t + 1, n0, tpB, cl0);
-    // rotate: t + 2 -> t + 1 (values now), t + 3 -> t + 2
-    tpA = tpB; tpB = tpC; tpC = tpD; tpD = tpE; tpE = tpF;
-    n0 = n1;
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) { cl0[e] = cl1[e]; li0[e] = li1[e]; cl1[e] = cl2[e]; li1[e] = li2[e]; }
+    xwrite(t + 1, n1, tq[0], P1, X1);
+    __syncthreads();                                  // tile t + 1's X image complete
+    // rotate: t + 2 -> t + 1, t + 3 -> t + 2; then t + 2's values (after the barrier: a barrier's release would
+    // wait for them; in flight during the next tile's MFMAs instead)
     n1 = n2;
-    vals(n0, li0);
-    __syncthreads();
+    n2 = n3;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) P1[e] = P2[e];
+    pack(t + 3, n3, C3, L3, P2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tq[i] = tq[i + 1];
+    tq[4] = tnew;
+    vals(P1, X1);
+    return true;
+  };
+  for (int t = t0; t < t1; t += 2) {                  // (two tiles per trip: each W1 buffer a static LDS object)
+    if (!step(t, wsA, wsB) || !step(t + 1, wsB, wsA)) break;
   }
   // ---- partials: C layout of v_mfma_f32_32x32x16 (register k: row (k & 3) + 8 (k >> 2) + 4 hf, column lane & 31)
 #pragma unroll
@@ -273,6 +288,7 @@ extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
   OCF_CHECK(a.ldw >= a.H && a.ldw % 8 == 0, "ocf_encoder_tiles: ldw");
   OCF_CHECK(a.B >= 0 && a.B <= a.Bp && a.Bp % 128 == 0, "ocf_encoder_tiles: B <= Bp, Bp a multiple of 128");
   OCF_CHECK(a.n_tiles >= 1 && a.splits >= 1, "ocf_encoder_tiles: n_tiles, splits >= 1");
+  OCF_CHECK(a.nnz >= 1 && a.n_entries >= 1, "ocf_encoder_tiles: nnz, n_entries >= 1 (the clamp bounds)");
   if (a.Bp == 0) return 0;
   const int n_rg = (a.Bp + et::BM - 1) / et::BM, n_hs = a.H / et::BH;
   const int tiles_per = (a.n_tiles + a.splits - 1) / a.splits;

@@ -930,6 +930,7 @@ class Engine:
         Wt, wdt = self._wop(0)
         a.W, a.ldw, a.w_dtype = ptr(Wt), Wt.shape[1], wdt
         a.B, a.Bp, a.n_tiles, a.H, a.splits, a.part = self.B, self.Bp, self.n_tiles, Hp0, S, ptr(part)
+        a.nnz, a.n_entries = t["t_col"].numel(), max(int(self.gt["E"]), 1)
         call("ocf_encoder_tiles", a, cur_stream())
         cp = self._gbuf.get("tile_cptr_%d" % S)
         if cp is None:

@@ -25,7 +25,8 @@ def _model_and_batch(cd, rows, cols, nnz, B, tiles, dup, seed=3):
         data = split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(seed))
     np.random.seed(seed)
     rd = data_reader(cols, rows, dataset=data, eval_mode="fixed_split")
-    om = omni_model(1, 500, cols, B, dense_activation="sigmoid", use_causal_info=False, compute_dtype=cd, seed=9)
+    # (linear: the stored activation a = the pre-activation itself)
+    om = omni_model(1, 500, cols, B, dense_activation="linear", use_causal_info=False, compute_dtype=cd, seed=9)
     om.engine.enc_tiles = tiles
     om.engine.fuse_enc_epilogue = False      # (the gather encoder's epilogue in its own launch: forward() alone)
     m = om.model
