@@ -103,6 +103,8 @@ def parse():
     ap.add_argument("--enc-tiles", type=int, default=-1,
                     help="the encoder over column tiles on the matrix cores (ocf_encoder_tiles; 1), the row gathers (0), "
                          "or the engine's choice by entries per weight row (-1)")
+    ap.add_argument("--enc-tiles-pack", type=int, default=-1,
+                    help="ocf_encoder_tiles' packed pre-pass (1, library default) or the per-row entry chain (0)")
     ap.add_argument("--gather-chunk", type=int, default=0,
                     help="entries per row-gather chunk of large batches (0: data_reader.GATHER_CHUNK)")
     ap.add_argument("--fold-reduce", type=int, default=1,
@@ -747,6 +749,8 @@ def main():
         _lib.call("ocf_set_tuning", b"rows_dual_pf", int(args.rows_dual_pf), None)
     if args.rows_dual_large >= 0:
         _lib.call("ocf_set_tuning", b"rows_dual_large", int(args.rows_dual_large), None)
+    if args.enc_tiles_pack >= 0:
+        _lib.call("ocf_set_tuning", b"enc_tiles_pack", int(args.enc_tiles_pack), None)
     if args.rows_small_waves >= 0:
         _lib.call("ocf_set_tuning", b"rows_small_waves", int(args.rows_small_waves), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)

@@ -214,7 +214,10 @@ typedef struct OcfEncTileArgs {
   float* part;            /* [Bp][splits][H] fp32                                                           */
   int64_t nnz;            /* entries of the view, n_entries: entries of xval (bounds of the clamped loads)  */
   int64_t n_entries;
+  void* work; int64_t work_bytes;   /* device scratch of ocf_encoder_tiles_workspace(args) bytes: the batch's
+                                       entries packed per (256-row group, tile) by a pre-pass in the same call */
 } OcfEncTileArgs;
+int64_t ocf_encoder_tiles_workspace(const OcfEncTileArgs* args);
 int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream);
 
 enum { OCF_REDUCE_RAW = 0, OCF_REDUCE_BIAS_ACT = 1, OCF_REDUCE_GRAD_ACT = 2 };
@@ -717,6 +720,8 @@ int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);
  *               (ocf_optim_ws.h); 0 = the generic tile kernel.  Bit-identical results.
  *   "optim_ws_max_k": largest K (batch rows) sent to that kernel (default 256; beyond it the K-loop
  *               outgrows the optimizer stream it hides under and the generic kernel is faster).
+ *   "enc_tiles_pack": ocf_encoder_tiles with its packed pre-pass (1, default) or each row's entries read by the
+ *               tile kernel itself (0).
  *   "pair_wait_polls", "encdec_max_polls", "mlp_max_polls": the bounded in-kernel waits of ocf_gemm_pair,
  *               ocf_gather_encdec and ocf_mlp_step (polls of ~64 cycles); the last two take a negative value as
  *               fault injection for tests (a give-up on workgroup 0 / batch row 0).

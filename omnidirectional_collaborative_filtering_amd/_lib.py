@@ -72,7 +72,7 @@ class OcfEncTileArgs(ctypes.Structure):
     _fields_ = [
         ("rows", P), ("rp", P), ("tptr", P), ("tcol", P), ("tlidx", P), ("lboff", P), ("xval", P),
         ("W", P), ("ldw", I64), ("w_dtype", I32), ("B", I32), ("Bp", I32), ("n_tiles", I32), ("H", I32),
-        ("splits", I32), ("part", P), ("nnz", I64), ("n_entries", I64),
+        ("splits", I32), ("part", P), ("nnz", I64), ("n_entries", I64), ("work", P), ("work_bytes", I64),
     ]
 
 
@@ -268,6 +268,7 @@ SIGNATURES = {
     "ocf_set_tuning": (I32, [ctypes.c_char_p, I32, ctypes.POINTER(I32)]),
     "ocf_check_async": (I32, []),
     "ocf_encoder_tiles": (I32, [ctypes.POINTER(OcfEncTileArgs), P]),
+    "ocf_encoder_tiles_workspace": (I64, [ctypes.POINTER(OcfEncTileArgs)]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }

@@ -292,6 +292,9 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     if (previous) *previous = g_mlp_max_polls;
     OCF_CHECK(value != 0, "ocf_set_tuning: mlp_max_polls != 0");
     g_mlp_max_polls = value;
+  } else if (k == "enc_tiles_pack") {     // ocf_encoder_tiles: packed pre-pass (1) or per-row entry chain (0)
+    if (previous) *previous = g_enc_tiles_pack;
+    g_enc_tiles_pack = value ? 1 : 0;
   } else if (k == "optim_ws_max_k") {
     if (previous) *previous = g_optim_ws_max_k;
     g_optim_ws_max_k = value;

@@ -28,6 +28,8 @@
 // take a slow path for the rest (rare: ~1.2 entries per row per tile at Netflix width).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ocf_epilogues.h"
 #include "ocf_internal.h"
 
@@ -65,19 +67,20 @@ template <> struct Frag<__bf16> {
 };
 
 template <typename CT>
-__global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_rg, int n_q, int tiles_per) {
+__global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_rg, int n_hs, int tiles_per) {
   // three separate LDS objects: the compiler then knows a direct-to-LDS load into one W buffer does not alias the
   // reads of the other or of the X image, and does not wait for it (vmcnt) before them
   __shared__ __attribute__((aligned(16))) char xs[BM * ROWB];
   __shared__ __attribute__((aligned(16))) char wsA[BK * ROWB];
   __shared__ __attribute__((aligned(16))) char wsB[BK * ROWB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // workgroups -> (row group, hidden slice, split): the row groups of one (slice, split) -- readers of the same
-  // W1 tiles -- on one XCD (blockIdx round-robins over the 8 XCDs), so the second and later reads hit its L2
-  const int bx = blockIdx.x, xcd = bx & 7, j = bx >> 3;
-  const int rg = j % n_rg, q = (j / n_rg) * 8 + xcd;
-  if (q >= n_q) return;
-  const int S = a.splits, s = q % S, hs = q / S;
+  // workgroups -> (split, row group, hidden slice): every workgroup of one split on one XCD (blockIdx round-robins
+  // over the 8 XCDs) -- the row groups read the same W1 tiles, the hidden slices the same entries -- so only the
+  // first read of each goes to HBM, the others hit the XCD's L2
+  const int per = n_rg * n_hs;                        // workgroups per split
+  const int bx = blockIdx.x, xcd = bx & 7, slot = bx >> 3;
+  const int S = a.splits, s = (slot / per) * 8 + xcd, rem = slot % per, rg = rem / n_hs, hs = rem % n_hs;
+  if (s >= S) return;
   const int t0 = s * tiles_per, t1 = min(a.n_tiles, t0 + tiles_per);
   if (t0 >= t1) {                                     // an empty split: zero partials
     for (int i = tid; i < BM * BH; i += 256) {
@@ -272,10 +275,265 @@ __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_
     }
 }
 
+
+// ---- the packed form.  The thread-per-row chain above reads, per tile and workgroup, one or two 64-B lines of the
+// view (columns, list indices) and of xval per batch row: ~48 KB of scattered lines against the tile's 32 KB of W1,
+// and once per hidden slice.  A pre-pass (three launches per batch) packs the batch's entries into buckets per (row
+// group, tile) instead -- one 32-bit word per entry: row in group (8 bits) | column in tile (7 bits) | valid (1) |
+// the input value in the compute dtype (16 bits), duplicates of a (row, column) merged into one word (their values
+// added, the others left invalid) -- so the tile kernel reads each tile's entries as ~1.2 KB of contiguous words.
+constexpr int PK_TPB = 256;        // tiles per pre-pass workgroup (a thread per tile)
+
+__device__ __forceinline__ int row_of(const OcfEncTileArgs& a, int b) { return b < a.B ? a.rows[b] : -1; }
+
+// cnt[rg][t] = entries of the row group's rows in tile t
+__global__ void __launch_bounds__(PK_TPB) pack_count_kernel(OcfEncTileArgs a, int32_t* cnt) {
+  const int rg = blockIdx.y, t = blockIdx.x * PK_TPB + threadIdx.x;
+  __shared__ int rows_sh[BM];
+  rows_sh[threadIdx.x] = row_of(a, rg * BM + threadIdx.x);
+  __syncthreads();
+  if (t >= a.n_tiles) return;
+  int c = 0;
+  for (int i = 0; i < BM; ++i) {
+    const int r = rows_sh[i];
+    if (r < 0) continue;
+    const int32_t* tp = a.tptr + (int64_t)r * (a.n_tiles + 1) + t;
+    c += tp[1] - tp[0];
+  }
+  cnt[(int64_t)rg * (a.n_tiles + 1) + t] = c;
+}
+
+// exclusive scan of one row group's counts (in place) -> bucket pointers; the group's base = the previous groups'
+// totals (groups scanned in order by one workgroup each: group rg adds the totals of groups < rg from the bases)
+__global__ void __launch_bounds__(1024) pack_scan_kernel(OcfEncTileArgs a, int32_t* cnt, int n_rg) {
+  __shared__ int part[1024];
+  __shared__ int base_sh;
+  const int n = a.n_tiles;
+  if (threadIdx.x == 0) base_sh = 0;
+  __syncthreads();
+  for (int rg = 0; rg < n_rg; ++rg) {
+    int32_t* c = cnt + (int64_t)rg * (n + 1);
+    const int per = (n + 1023) / 1024, i0 = threadIdx.x * per;
+    int s = 0;
+    for (int i = i0; i < min(n, i0 + per); ++i) s += c[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {       // inclusive scan of the thread sums
+      const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    int run = base_sh + (threadIdx.x ? part[threadIdx.x - 1] : 0);
+    for (int i = i0; i < min(n, i0 + per); ++i) {
+      const int v = c[i];
+      c[i] = run;
+      run += v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) {
+      c[n] = base_sh + part[1023];
+      base_sh += part[1023];
+    }
+    __syncthreads();
+  }
+}
+
+template <typename CT>
+__global__ void __launch_bounds__(PK_TPB) pack_fill_kernel(OcfEncTileArgs a, const int32_t* bptr, uint32_t* ent) {
+  const int rg = blockIdx.y, t = blockIdx.x * PK_TPB + threadIdx.x;
+  __shared__ int rows_sh[BM];
+  __shared__ int64_t lb_sh[BM];
+  {
+    const int b = rg * BM + threadIdx.x;
+    rows_sh[threadIdx.x] = row_of(a, b);
+    lb_sh[threadIdx.x] = b < a.B ? a.lboff[b] : 0;
+  }
+  __syncthreads();
+  if (t >= a.n_tiles) return;
+  int64_t o = bptr[(int64_t)rg * (a.n_tiles + 1) + t];
+  for (int i = 0; i < BM; ++i) {
+    const int r = rows_sh[i];
+    if (r < 0) continue;
+    const int32_t* tp = a.tptr + (int64_t)r * (a.n_tiles + 1) + t;
+    const int64_t e0 = a.rp[r] + tp[0], e1 = a.rp[r] + tp[1];
+    for (int64_t e = e0; e < e1; ++e) {
+      const int col = a.tcol[e];
+      float x = a.xval[lb_sh[i] + a.tlidx[e]];
+      uint32_t w = 0;                                    // (an invalid word: merged into the one before it)
+      if (e == e0 || a.tcol[e - 1] != col) {
+        for (int64_t f = e + 1; f < e1 && a.tcol[f] == col; ++f) x += a.xval[lb_sh[i] + a.tlidx[f]];
+        const CT v = CvtT<CT>::to(x);
+        uint16_t vb;
+        __builtin_memcpy(&vb, &v, 2);
+        w = (uint32_t)i | ((uint32_t)(col - t * BK) << 8) | (1u << 15) | ((uint32_t)vb << 16);
+      }
+      ent[o++] = w;
+    }
+  }
+}
+
+constexpr int PEMAX = 4;   // bucket words per thread per tile held in registers (a bucket of <= 1,024 words)
+
+template <typename CT>
+__global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a, const int32_t* bptr,
+                                                                const uint32_t* ent, int n_rg, int n_hs,
+                                                                int tiles_per) {
+  __shared__ __attribute__((aligned(16))) char xs[BM * ROWB];
+  __shared__ __attribute__((aligned(16))) char wsA[BK * ROWB];
+  __shared__ __attribute__((aligned(16))) char wsB[BK * ROWB];
+  __shared__ int bp_sh[1056];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = n_rg * n_hs;
+  const int bx = blockIdx.x, xcd = bx & 7, slot = bx >> 3;
+  const int S = a.splits, s = (slot / per) * 8 + xcd, rem = slot % per, rg = rem / n_hs, hs = rem % n_hs;
+  if (s >= S) return;
+  const int t0 = s * tiles_per, t1 = min(a.n_tiles, t0 + tiles_per);
+  if (t0 >= t1) {
+    for (int i = tid; i < BM * BH; i += 256) {
+      const int b = rg * BM + i / BH;
+      if (b < a.Bp) a.part[((int64_t)b * S + s) * a.H + hs * BH + (i % BH)] = 0.f;
+    }
+    return;
+  }
+  const int h0 = hs * BH;
+  using F = Frag<CT>;
+  using FT = typename F::T;
+  // the split's bucket pointers, once
+  for (int i = tid; i <= t1 - t0; i += 256) bp_sh[i] = bptr[(int64_t)rg * (a.n_tiles + 1) + t0 + i];
+  const char* Wb = reinterpret_cast<const char*>(a.W);
+  auto wload = [&](int t, char* dst) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int n0 = 4 * (4 * i + wave), n = n0 + (lane >> 4), c = (lane & 15) ^ (((n & 3) << 2) | ((n >> 2) & 3));
+      const char* src = Wb + (((int64_t)t * BK + n) * a.ldw + h0) * 2 + 16 * c;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + n0 * ROWB), 16, 0, 0);
+    }
+  };
+  // a tile's words: thread tid takes words lo + tid + 256 j (j < PEMAX; the rest of a bucket over 1,024 words in a
+  // loop, rare); loads clamped to the bucket, masked where used
+  const int64_t elast = bptr[(int64_t)n_rg * (a.n_tiles + 1) - 1] - 1;   // (the last group's total - 1)
+  auto eload = [&](int tl, uint32_t (&w)[PEMAX]) {
+    const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
+#pragma unroll
+    for (int j = 0; j < PEMAX; ++j) {
+      const int64_t i = lo + tid + 256 * j;
+      w[j] = i < hi ? ent[min(i, elast < 0 ? 0 : elast)] : 0u;
+    }
+  };
+  uint32_t cwd[PEMAX];       // the words written for the current tile (cleared after its MFMAs)
+  bool over = false;
+  auto wput = [&](uint32_t w, bool zero) {
+    if (!(w & 0x8000u)) return;
+    const int row = w & 255, kk = (w >> 8) & 127;
+    const uint16_t vb = zero ? 0 : (uint16_t)(w >> 16);
+    *reinterpret_cast<uint16_t*>(xs + xoff(row, kk >> 3) + 2 * (kk & 7)) = vb;
+  };
+  auto xwrite = [&](int tl, const uint32_t (&w)[PEMAX]) {
+#pragma unroll
+    for (int j = 0; j < PEMAX; ++j) {
+      cwd[j] = w[j];
+      wput(w[j], false);
+    }
+    const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
+    over = hi - lo > 256 * PEMAX;
+    for (int64_t i = lo + tid + 256 * PEMAX; i < hi; i += 256) wput(ent[i], false);
+  };
+  auto xclear = [&](int tl) {
+#pragma unroll
+    for (int j = 0; j < PEMAX; ++j) wput(cwd[j], true);
+    if (over) {
+      const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
+      for (int64_t i = lo + tid + 256 * PEMAX; i < hi; i += 256) wput(ent[i], true);
+    }
+  };
+  for (int i = tid; i < BM * ROWB / 16; i += 256) reinterpret_cast<uint4*>(xs)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();                                   // (bp_sh)
+  wload(t0, wsA);
+  uint32_t W1[PEMAX];
+  {
+    uint32_t W0[PEMAX];
+    eload(t0, W0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    xwrite(t0, W0);
+  }
+  if (t0 + 1 < t1) eload(t0 + 1, W1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f16v acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[i][c][k] = 0.f;
+  const int r = lane & 31, hf = lane >> 5, g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
+  auto step = [&](int t, const char* wcur, char* wnext) -> bool {
+    const bool more = t + 1 < t1;
+    if (more) wload(t + 1, wnext);
+    uint32_t W2[PEMAX];
+    if (t + 2 < t1) eload(t + 2, W2);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      FT fa[2], fb[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const FT*>(xs + xoff(64 * wave + 32 * i + r, 2 * ks + hf));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int ch = 4 * c + 2 * (g & 1) + (gp >> 1);
+        const int nr = 16 * ks + 8 * (g >> 1) + gq;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(wcur + woff(nr, ch) + 8 * (gp & 1)));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(wcur + woff(nr + 4, ch) + 8 * (gp & 1)));
+        const short e[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        __builtin_memcpy(&fb[c], e, 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[i][c] = F::mfma(fa[i], fb[c], acc[i][c]);
+    }
+    if (!more) return false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1's W1 image, t + 2's words
+    __syncthreads();
+    xclear(t);
+    xwrite(t + 1, W1);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PEMAX; ++j) W1[j] = W2[j];
+    return true;
+  };
+  for (int t = t0; t < t1; t += 2)
+    if (!step(t, wsA, wsB) || !step(t + 1, wsB, wsA)) break;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int b = rg * BM + 64 * wave + 32 * i + (k & 3) + 8 * (k >> 2) + 4 * hf;
+      if (b < a.Bp) {
+        float* dst = a.part + ((int64_t)b * S + s) * a.H + h0 + r;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) dst[32 * c] = acc[i][c][k];
+      }
+    }
+}
+
 }  // namespace et
 }  // namespace ocf
 
 using namespace ocf;
+
+namespace ocf {
+int g_enc_tiles_pack = 1;   // ocf_set_tuning "enc_tiles_pack": the packed pre-pass (1) or the per-row chain (0)
+}
+
+extern "C" int64_t ocf_encoder_tiles_workspace(const OcfEncTileArgs* a) {
+  if (!a || a->Bp < 0 || a->n_tiles < 1 || a->n_entries < 0) return -1;
+  const int64_t n_rg = (a->Bp + et::BM - 1) / et::BM;
+  return (n_rg * (a->n_tiles + 1) * 4 + 255) / 256 * 256 + (std::max<int64_t>(a->n_entries, 1) * 4 + 255) / 256 * 256;
+}
 
 extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
   OCF_TRY_BEGIN
@@ -292,13 +550,33 @@ extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
   if (a.Bp == 0) return 0;
   const int n_rg = (a.Bp + et::BM - 1) / et::BM, n_hs = a.H / et::BH;
   const int tiles_per = (a.n_tiles + a.splits - 1) / a.splits;
-  const int n_q = n_hs * a.splits;
-  const int grid = n_rg * ((n_q + 7) / 8) * 8;
+  OCF_CHECK(tiles_per <= 1024, "ocf_encoder_tiles: more than 1,024 tiles per split (raise splits)");
+  const int grid = (a.splits + 7) / 8 * 8 * n_rg * n_hs;
   hipStream_t s = (hipStream_t)stream;
-  if (a.w_dtype == OCF_F16)
-    hipLaunchKernelGGL(et::enc_tiles_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, n_rg, n_q, tiles_per);
-  else
-    hipLaunchKernelGGL(et::enc_tiles_kernel<__bf16>, dim3(grid), dim3(256), 0, s, a, n_rg, n_q, tiles_per);
+  const bool f16 = a.w_dtype == OCF_F16;
+  if (g_enc_tiles_pack) {
+    const int64_t need = ocf_encoder_tiles_workspace(&a);
+    OCF_CHECK(a.work && a.work_bytes >= need, "ocf_encoder_tiles: workspace too small (ocf_encoder_tiles_workspace)");
+    int32_t* cnt = reinterpret_cast<int32_t*>(a.work);
+    uint32_t* ent = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.work) +
+                                                 ((int64_t)n_rg * (a.n_tiles + 1) * 4 + 255) / 256 * 256);
+    const dim3 pg((a.n_tiles + et::PK_TPB - 1) / et::PK_TPB, n_rg);
+    hipLaunchKernelGGL(et::pack_count_kernel, pg, dim3(et::PK_TPB), 0, s, a, cnt);
+    hipLaunchKernelGGL(et::pack_scan_kernel, dim3(1), dim3(1024), 0, s, a, cnt, n_rg);
+    if (f16) {
+      hipLaunchKernelGGL(et::pack_fill_kernel<_Float16>, pg, dim3(et::PK_TPB), 0, s, a, cnt, ent);
+      hipLaunchKernelGGL(et::enc_tiles_packed_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
+                         tiles_per);
+    } else {
+      hipLaunchKernelGGL(et::pack_fill_kernel<__bf16>, pg, dim3(et::PK_TPB), 0, s, a, cnt, ent);
+      hipLaunchKernelGGL(et::enc_tiles_packed_kernel<__bf16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
+                         tiles_per);
+    }
+  } else if (f16) {
+    hipLaunchKernelGGL(et::enc_tiles_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, n_rg, n_hs, tiles_per);
+  } else {
+    hipLaunchKernelGGL(et::enc_tiles_kernel<__bf16>, dim3(grid), dim3(256), 0, s, a, n_rg, n_hs, tiles_per);
+  }
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }

@@ -914,8 +914,8 @@ class Engine:
     def _enc_splits(self, Hp0):
         n_rg, n_hs = -(-self.Bp // 256), Hp0 // 128
         S = max(1, min(self.n_tiles, round(ENC_TILES_WGS / (n_rg * n_hs))))
-        while (n_hs * S) % 8 and S < self.n_tiles:          # whole groups of 8 (one per XCD)
-            S += 1
+        if S > 8:                                           # whole groups of 8 splits (one per XCD)
+            S = min(self.n_tiles, -(-S // 8) * 8)
         return S
 
     def _encoder_tiles(self, part_name, Hp0, xv):
@@ -931,6 +931,11 @@ class Engine:
         a.W, a.ldw, a.w_dtype = ptr(Wt), Wt.shape[1], wdt
         a.B, a.Bp, a.n_tiles, a.H, a.splits, a.part = self.B, self.Bp, self.n_tiles, Hp0, S, ptr(part)
         a.nnz, a.n_entries = t["t_col"].numel(), max(int(self.gt["E"]), 1)
+        nb = int(_lib.load().ocf_encoder_tiles_workspace(ctypes.byref(a)))
+        if nb < 0:
+            raise _lib.OcfError("ocf_encoder_tiles_workspace: bad arguments")
+        w = self._buf("enc_tiles_work", -(-nb // 4), torch.int32)
+        a.work, a.work_bytes = ptr(w), w.numel() * 4
         call("ocf_encoder_tiles", a, cur_stream())
         cp = self._gbuf.get("tile_cptr_%d" % S)
         if cp is None:

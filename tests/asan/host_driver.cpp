@@ -28,7 +28,7 @@ static bool last_error_has(const char* s) { return std::strstr(ocf_last_error(),
 
 static void tuning() {
   struct K { const char* key; int good; int bad; };
-  const K keys[] = {{"optim_rows", 1, -99}, {"rows_long", -1, -99}, {"rows_dual", 1, -99},
+  const K keys[] = {{"optim_rows", 1, -99}, {"enc_tiles_pack", 1, -99}, {"rows_long", -1, -99}, {"rows_dual", 1, -99},
                     {"rows_dual_parts", 23, 99}, {"rows_dual_pf", -1, -99}, {"rows_dual_large", 1, -99},
                     {"rows_dual_count", 0, -99}, {"rows_small_waves", 4096, -99}, {"optim_ws", 1, -99},
                     {"pair_wait_polls", 1 << 22, 0}, {"encdec_max_polls", 1 << 22, 0}, {"mlp_max_polls", 1 << 22, 0},
@@ -85,6 +85,18 @@ static void argument_checks() {
   EXPECT(ocf_recip_keep_workspace(-1, 4, 10, 624) == -1, "recip_keep_workspace: negative");
   EXPECT(ocf_recip_keep_workspace(3, 256, 200000, 17) > 0, "recip_keep_workspace: layout");
   EXPECT(ocf_mlp_step(nullptr, nullptr) == 1, "mlp_step: null");
+  OcfEncTileArgs et{};
+  EXPECT(ocf_encoder_tiles(&et, nullptr) == 1 && last_error_has("null pointer"), "encoder_tiles: null tables");
+  EXPECT(ocf_encoder_tiles_workspace(nullptr) == -1, "encoder_tiles_workspace: null");
+  et.Bp = 256; et.n_tiles = 3753; et.n_entries = 1150000;
+  EXPECT(ocf_encoder_tiles_workspace(&et) >= 3754 * 4 + 1150000 * 4, "encoder_tiles_workspace: layout");
+  et.rows = dummy_i; et.rp = dummy_l; et.tptr = dummy_i; et.tcol = dummy_i; et.tlidx = dummy_i; et.lboff = dummy_l;
+  et.xval = dummy_f; et.W = dummy_f; et.part = dummy_f; et.w_dtype = OCF_DT_F32;
+  EXPECT(ocf_encoder_tiles(&et, nullptr) == 1 && last_error_has("16-bit"), "encoder_tiles: fp32 weights refused");
+  et.w_dtype = OCF_DT_F16; et.H = 512; et.ldw = 512; et.B = 256; et.splits = 1; et.nnz = 10;
+  EXPECT(ocf_encoder_tiles(&et, nullptr) == 1 && last_error_has("1,024 tiles"), "encoder_tiles: tiles per split");
+  et.splits = 64;
+  EXPECT(ocf_encoder_tiles(&et, nullptr) == 1 && last_error_has("workspace"), "encoder_tiles: workspace");
 }
 
 static void model_logic() {

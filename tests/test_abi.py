@@ -56,6 +56,8 @@ STRUCTS = {
                                        "jb_ld", "jb_op", "js_sp", "js_M", "row_live", "sp_rowptr",
                                        "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
     "OcfPairSync": (_lib.OcfPairSync, ["word", "count"]),
+    "OcfEncTileArgs": (_lib.OcfEncTileArgs, ["rows", "xval", "ldw", "w_dtype", "B", "splits", "part", "nnz",
+                                             "n_entries", "work", "work_bytes"]),
     "OcfMlpStepArgs": (_lib.OcfMlpStepArgs, ["n_hidden", "Bp", "k_blocks", "hidden", "hidden_p", "x", "ld_x", "rows",
                                              "targets", "ld_t", "W", "b", "sW2", "sb2", "shadow", "shadow_blocked",
                                              "act", "compute_dtype", "opt", "stats", "work", "work_bytes", "barrier",
