@@ -499,6 +499,7 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1's W1 image, t + 2's words
     __syncthreads();
     xclear(t);
+    __syncthreads();          // (a row's words of two tiles may share a position and belong to different threads)
     xwrite(t + 1, W1);
     __syncthreads();
 #pragma unroll

@@ -39,10 +39,23 @@ def _model_and_batch(cd, rows, cols, nnz, B, tiles, dup, seed=3):
 @pytest.mark.parametrize("cd,rows,cols,nnz,B,dup", [
     ("float16", 1500, 20000, 600000, 256, False),   # ~2 entries per live column, 157 tiles
     ("bfloat16", 1500, 9000, 400000, 100, True),    # padding rows (B = 100 of a 256-row group), duplicates
-    ("float16", 3000, 16384, 2000000, 512, False),  # two row groups (the XCD-shared W tiles)
+    ("float16", 3000, 16384, 600000, 512, False),   # two row groups (the XCD-shared W tiles)
+    ("float16", 3000, 16384, 2000000, 256, False),  # buckets over 1,024 words (~4 entries per row per tile)
+    ("float16", 3000, 16384, 2000000, 512, False),  # both
 ])
-def test_encoder_tiles_preactivation(gpu, cd, rows, cols, nnz, B, dup):
+@pytest.mark.parametrize("pack", [1, 0])
+def test_encoder_tiles_preactivation(gpu, cd, rows, cols, nnz, B, dup, pack):
+    from omnidirectional_collaborative_filtering_amd import _lib
     from oracle.batch_oracle import scatter_rows_numpy
+    prev = _lib.ctypes.c_int32()
+    _lib.call("ocf_set_tuning", b"enc_tiles_pack", pack, _lib.ctypes.byref(prev))
+    try:
+        _preactivation(cd, rows, cols, nnz, B, dup, scatter_rows_numpy)
+    finally:
+        _lib.call("ocf_set_tuning", b"enc_tiles_pack", prev.value, None)
+
+
+def _preactivation(cd, rows, cols, nnz, B, dup, scatter_rows_numpy):
     out = {}
     for tiles in (True, False):
         data, om, gen = _model_and_batch(cd, rows, cols, nnz, B, tiles, dup)
@@ -64,7 +77,8 @@ def test_encoder_tiles_preactivation(gpu, cd, rows, cols, nnz, B, dup):
             scale = np.abs(xq) @ np.abs(W)
         del om, e, gen
     err_t = np.abs(out[True] - ref)
-    assert (err_t <= 1e-5 * scale + 1e-6).all(), float((err_t / (scale + 1e-30)).max())
+    bad = np.argwhere(err_t > 1e-5 * scale + 1e-6)
+    assert len(bad) == 0, (len(bad), bad[:8].tolist(), float((err_t / (scale + 1e-30)).max()))
     err_g = np.abs(out[False] - ref)
     assert (err_g <= 1e-5 * scale + 1e-6).all()
     assert np.abs(out[True] - out[False]).max() <= 2e-5 * scale.max()
