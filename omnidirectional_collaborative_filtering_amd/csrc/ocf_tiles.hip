@@ -282,25 +282,37 @@ __global__ void __launch_bounds__(256) enc_tiles_kernel(OcfEncTileArgs a, int n_
 // group, tile) instead -- one 32-bit word per entry: row in group (8 bits) | column in tile (7 bits) | valid (1) |
 // the input value in the compute dtype (16 bits), duplicates of a (row, column) merged into one word (their values
 // added, the others left invalid) -- so the tile kernel reads each tile's entries as ~1.2 KB of contiguous words.
-constexpr int PK_TPB = 256;        // tiles per pre-pass workgroup (a thread per tile)
+constexpr int PK_TB = 16;          // tiles per pre-pass workgroup (a thread per batch row of the group)
 
 __device__ __forceinline__ int row_of(const OcfEncTileArgs& a, int b) { return b < a.B ? a.rows[b] : -1; }
 
-// cnt[rg][t] = entries of the row group's rows in tile t
-__global__ void __launch_bounds__(PK_TPB) pack_count_kernel(OcfEncTileArgs a, int32_t* cnt) {
-  const int rg = blockIdx.y, t = blockIdx.x * PK_TPB + threadIdx.x;
-  __shared__ int rows_sh[BM];
-  rows_sh[threadIdx.x] = row_of(a, rg * BM + threadIdx.x);
-  __syncthreads();
-  if (t >= a.n_tiles) return;
-  int c = 0;
-  for (int i = 0; i < BM; ++i) {
-    const int r = rows_sh[i];
-    if (r < 0) continue;
-    const int32_t* tp = a.tptr + (int64_t)r * (a.n_tiles + 1) + t;
-    c += tp[1] - tp[0];
+// thread b's counts of its row's entries in tiles [t0, t0 + PK_TB) (0 past the last tile / for an empty row)
+__device__ __forceinline__ void row_counts(const OcfEncTileArgs& a, int r, int t0, int (&tp)[PK_TB + 1]) {
+#pragma unroll
+  for (int j = 0; j <= PK_TB; ++j) tp[j] = 0;
+  if (r < 0) return;
+  const int32_t* p = a.tptr + (int64_t)r * (a.n_tiles + 1);
+#pragma unroll
+  for (int j = 0; j <= PK_TB; ++j) tp[j] = p[min(t0 + j, a.n_tiles)];
+}
+
+// cnt[rg][t] = entries of the row group's rows in tile t: a workgroup per (group, 16 tiles), a thread per row, the
+// 256 rows summed per tile by the four waves' reductions (integer sums: order-free)
+__global__ void __launch_bounds__(BM) pack_count_kernel(OcfEncTileArgs a, int32_t* cnt) {
+  const int rg = blockIdx.y, t0 = blockIdx.x * PK_TB, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int tot[4][PK_TB];
+  int tp[PK_TB + 1];
+  row_counts(a, row_of(a, rg * BM + tid), t0, tp);
+#pragma unroll
+  for (int j = 0; j < PK_TB; ++j) {
+    int c = tp[j + 1] - tp[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) tot[wave][j] = c;
   }
-  cnt[(int64_t)rg * (a.n_tiles + 1) + t] = c;
+  __syncthreads();
+  if (tid < PK_TB && t0 + tid < a.n_tiles)
+    cnt[(int64_t)rg * (a.n_tiles + 1) + t0 + tid] = tot[0][tid] + tot[1][tid] + tot[2][tid] + tot[3][tid];
 }
 
 // exclusive scan of one row group's counts (in place) -> bucket pointers; the group's base = the previous groups'
@@ -339,34 +351,66 @@ __global__ void __launch_bounds__(1024) pack_scan_kernel(OcfEncTileArgs a, int32
   }
 }
 
+// the words: a workgroup per (group, 16 tiles), thread b = row b of the group; the row's position in each tile's
+// bucket = the bucket pointer + the entries of rows < b in that tile (wave prefix sums + the waves before it); the
+// row's entries of the 16 tiles are contiguous in the view and are walked 8 at a time (all loads in flight)
 template <typename CT>
-__global__ void __launch_bounds__(PK_TPB) pack_fill_kernel(OcfEncTileArgs a, const int32_t* bptr, uint32_t* ent) {
-  const int rg = blockIdx.y, t = blockIdx.x * PK_TPB + threadIdx.x;
-  __shared__ int rows_sh[BM];
-  __shared__ int64_t lb_sh[BM];
-  {
-    const int b = rg * BM + threadIdx.x;
-    rows_sh[threadIdx.x] = row_of(a, b);
-    lb_sh[threadIdx.x] = b < a.B ? a.lboff[b] : 0;
+__global__ void __launch_bounds__(BM) pack_fill_kernel(OcfEncTileArgs a, const int32_t* bptr, uint32_t* ent) {
+  const int rg = blockIdx.y, t0 = blockIdx.x * PK_TB, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ int tot[4][PK_TB];
+  const int b = rg * BM + tid, r = row_of(a, b);
+  int tp[PK_TB + 1];
+  row_counts(a, r, t0, tp);
+  int pre[PK_TB];
+#pragma unroll
+  for (int j = 0; j < PK_TB; ++j) {
+    const int c = tp[j + 1] - tp[j];
+    int v = c;                                          // inclusive scan over the wave's lanes
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int u = __shfl_up(v, off);
+      if (lane >= off) v += u;
+    }
+    pre[j] = v - c;
+    if (lane == 63) tot[wave][j] = v;
   }
   __syncthreads();
-  if (t >= a.n_tiles) return;
-  int64_t o = bptr[(int64_t)rg * (a.n_tiles + 1) + t];
-  for (int i = 0; i < BM; ++i) {
-    const int r = rows_sh[i];
-    if (r < 0) continue;
-    const int32_t* tp = a.tptr + (int64_t)r * (a.n_tiles + 1) + t;
-    const int64_t e0 = a.rp[r] + tp[0], e1 = a.rp[r] + tp[1];
-    for (int64_t e = e0; e < e1; ++e) {
-      const int col = a.tcol[e];
-      float x = a.xval[lb_sh[i] + a.tlidx[e]];
-      uint32_t w = 0;                                    // (an invalid word: merged into the one before it)
-      if (e == e0 || a.tcol[e - 1] != col) {
-        for (int64_t f = e + 1; f < e1 && a.tcol[f] == col; ++f) x += a.xval[lb_sh[i] + a.tlidx[f]];
-        const CT v = CvtT<CT>::to(x);
+  if (r < 0) return;
+  const int64_t rp0 = a.rp[r], lb = a.lboff[b];
+  const int64_t e_end = rp0 + tp[PK_TB];
+  int j = 0;                                            // the tile of the current entry
+  int64_t o = 0;                                        // its word position
+  auto start_of = [&](int jj) {
+    int w = 0;
+    for (int k = 0; k < wave; ++k) w += tot[k][jj];
+    return (int64_t)bptr[(int64_t)rg * (a.n_tiles + 1) + t0 + jj] + w + pre[jj];
+  };
+  for (int64_t e0 = rp0 + tp[0]; e0 < e_end; e0 += 8) {
+    int col[8], li[8];
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = min(e0 + k, e_end - 1);
+      col[k] = a.tcol[e];
+      li[k] = a.tlidx[e];
+    }
+    const int prev = e0 > rp0 + tp[0] ? a.tcol[e0 - 1] : -1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = a.xval[lb + li[k]];
+    for (int k = 0; k < 8 && e0 + k < e_end; ++k) {
+      const int64_t e = e0 + k;
+      while (e >= rp0 + tp[j + 1]) ++j;                 // (entries are column-sorted: tiles in order)
+      if (e == rp0 + tp[j]) o = start_of(j);
+      const int t = t0 + j;
+      const bool first = (k == 0 ? prev : col[k - 1]) != col[k] || e == rp0 + tp[j];
+      uint32_t w = 0;                                   // (an invalid word: merged into the one before it)
+      if (first) {
+        float v = x[k];
+        for (int64_t f = e + 1; f < rp0 + tp[j + 1] && a.tcol[f] == col[k]; ++f) v += a.xval[lb + a.tlidx[f]];
+        const CT h = CvtT<CT>::to(v);
         uint16_t vb;
-        __builtin_memcpy(&vb, &v, 2);
-        w = (uint32_t)i | ((uint32_t)(col - t * BK) << 8) | (1u << 15) | ((uint32_t)vb << 16);
+        __builtin_memcpy(&vb, &h, 2);
+        w = (uint32_t)tid | ((uint32_t)(col[k] - t * BK) << 8) | (1u << 15) | ((uint32_t)vb << 16);
       }
       ent[o++] = w;
     }
@@ -374,7 +418,10 @@ __global__ void __launch_bounds__(PK_TPB) pack_fill_kernel(OcfEncTileArgs a, con
 }
 
 constexpr int PEMAX = 4;   // bucket words per thread per tile held in registers (a bucket of <= 1,024 words)
+constexpr int STEP_LOADS = 8 + 1 + PEMAX;   // VMEM instructions one step issues (W1 tile, a bucket pointer, words)
 
+// W1 tiles three deep (two in flight during a tile's MFMAs: at one wave per SIMD a single 32-KB tile in flight left
+// the loads' latency exposed); LDS = the X image + three W1 buffers = 160 KB
 template <typename CT>
 __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a, const int32_t* bptr,
                                                                 const uint32_t* ent, int n_rg, int n_hs,
@@ -382,7 +429,7 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
   __shared__ __attribute__((aligned(16))) char xs[BM * ROWB];
   __shared__ __attribute__((aligned(16))) char wsA[BK * ROWB];
   __shared__ __attribute__((aligned(16))) char wsB[BK * ROWB];
-  __shared__ int bp_sh[1056];
+  __shared__ __attribute__((aligned(16))) char wsC[BK * ROWB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int per = n_rg * n_hs;
   const int bx = blockIdx.x, xcd = bx & 7, slot = bx >> 3;
@@ -399,10 +446,10 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
   const int h0 = hs * BH;
   using F = Frag<CT>;
   using FT = typename F::T;
-  // the split's bucket pointers, once
-  for (int i = tid; i <= t1 - t0; i += 256) bp_sh[i] = bptr[(int64_t)rg * (a.n_tiles + 1) + t0 + i];
   const char* Wb = reinterpret_cast<const char*>(a.W);
+  // every step issues the same loads (clamped to the split's last tile) so that one vmcnt count fits every step
   auto wload = [&](int t, char* dst) {
+    t = min(t, t1 - 1);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int n0 = 4 * (4 * i + wave), n = n0 + (lane >> 4), c = (lane & 15) ^ (((n & 3) << 2) | ((n >> 2) & 3));
@@ -410,56 +457,39 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
       __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + n0 * ROWB), 16, 0, 0);
     }
   };
-  // a tile's words: thread tid takes words lo + tid + 256 j (j < PEMAX; the rest of a bucket over 1,024 words in a
-  // loop, rare); loads clamped to the bucket, masked where used
-  const int64_t elast = bptr[(int64_t)n_rg * (a.n_tiles + 1) - 1] - 1;   // (the last group's total - 1)
-  auto eload = [&](int tl, uint32_t (&w)[PEMAX]) {
-    const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
+  const int32_t* bpr = bptr + (int64_t)rg * (a.n_tiles + 1);
+  auto bpl = [&](int t) { return bpr[min(t, t1)]; };
+  const int64_t elast = max(bptr[(int64_t)n_rg * (a.n_tiles + 1) - 1] - 1, 0);   // (every group's words - 1)
+  // a tile's words (bucket [lo, hi)): thread tid takes words lo + tid + 256 j; raw clamped loads, masked where used
+  auto eload = [&](int lo, uint32_t (&w)[PEMAX]) {
 #pragma unroll
-    for (int j = 0; j < PEMAX; ++j) {
-      const int64_t i = lo + tid + 256 * j;
-      w[j] = i < hi ? ent[min(i, elast < 0 ? 0 : elast)] : 0u;
-    }
+    for (int j = 0; j < PEMAX; ++j) w[j] = ent[min((int64_t)lo + tid + 256 * j, elast)];
   };
-  uint32_t cwd[PEMAX];       // the words written for the current tile (cleared after its MFMAs)
-  bool over = false;
   auto wput = [&](uint32_t w, bool zero) {
     if (!(w & 0x8000u)) return;
     const int row = w & 255, kk = (w >> 8) & 127;
-    const uint16_t vb = zero ? 0 : (uint16_t)(w >> 16);
-    *reinterpret_cast<uint16_t*>(xs + xoff(row, kk >> 3) + 2 * (kk & 7)) = vb;
+    *reinterpret_cast<uint16_t*>(xs + xoff(row, kk >> 3) + 2 * (kk & 7)) = zero ? (uint16_t)0 : (uint16_t)(w >> 16);
   };
-  auto xwrite = [&](int tl, const uint32_t (&w)[PEMAX]) {
+  // write (zero = false) or clear (zero = true) a tile's words
+  auto xput = [&](const uint32_t (&w)[PEMAX], int lo, int hi, bool zero) {
 #pragma unroll
-    for (int j = 0; j < PEMAX; ++j) {
-      cwd[j] = w[j];
-      wput(w[j], false);
-    }
-    const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
-    over = hi - lo > 256 * PEMAX;
-    for (int64_t i = lo + tid + 256 * PEMAX; i < hi; i += 256) wput(ent[i], false);
+    for (int j = 0; j < PEMAX; ++j)
+      if (lo + tid + 256 * j < hi) wput(w[j], zero);
+    for (int i = lo + tid + 256 * PEMAX; i < hi; i += 256) wput(ent[i], zero);   // (rare) a bucket over 1,024
   };
-  auto xclear = [&](int tl) {
-#pragma unroll
-    for (int j = 0; j < PEMAX; ++j) wput(cwd[j], true);
-    if (over) {
-      const int lo = bp_sh[tl - t0], hi = bp_sh[tl - t0 + 1];
-      for (int64_t i = lo + tid + 256 * PEMAX; i < hi; i += 256) wput(ent[i], true);
-    }
-  };
+  // ---- prologue: X image clear, tiles t0 and t0 + 1 in flight, tile t0's words written
   for (int i = tid; i < BM * ROWB / 16; i += 256) reinterpret_cast<uint4*>(xs)[i] = make_uint4(0, 0, 0, 0);
-  __syncthreads();                                   // (bp_sh)
+  int q0 = bpl(t0), q1 = bpl(t0 + 1), q2 = bpl(t0 + 2), q3 = bpl(t0 + 3), q4 = bpl(t0 + 4);   // bp(t) .. bp(t + 4)
   wload(t0, wsA);
-  uint32_t W1[PEMAX];
-  {
-    uint32_t W0[PEMAX];
-    eload(t0, W0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    xwrite(t0, W0);
-  }
-  if (t0 + 1 < t1) eload(t0 + 1, W1);
+  wload(t0 + 1, wsB);
+  // the words of three consecutive tiles in arrays whose roles rotate with the W1 buffers (no register moves of
+  // words still in flight at the loop's back edge)
+  uint32_t WX[PEMAX], WY[PEMAX], WZ[PEMAX];
+  eload(q0, WX);
+  eload(q1, WY);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  xput(WX, q0, q1, false);
   __syncthreads();
   f16v acc[2][4];
 #pragma unroll
@@ -469,11 +499,13 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
 #pragma unroll
       for (int k = 0; k < 16; ++k) acc[i][c][k] = 0.f;
   const int r = lane & 31, hf = lane >> 5, g = lane >> 4, gi = lane & 15, gq = gi >> 2, gp = gi & 3;
-  auto step = [&](int t, const char* wcur, char* wnext) -> bool {
-    const bool more = t + 1 < t1;
-    if (more) wload(t + 1, wnext);
-    uint32_t W2[PEMAX];
-    if (t + 2 < t1) eload(t + 2, W2);
+  // one tile: t's MFMAs from wcur while t + 1 (issued a step ago) and t + 2 (now, into w2) stream in
+  // (the bucket pointer first: moving it into the window waits for it alone, not for the tiles behind it)
+  auto step = [&](int t, const char* wcur, char* w2, uint32_t (&W0)[PEMAX], const uint32_t (&W1)[PEMAX],
+                  uint32_t (&W2)[PEMAX]) -> bool {
+    const int q5 = bpl(t + 5);
+    wload(t + 2, w2);
+    eload(q2, W2);                                    // tile t + 2's words (bucket [q2, q3))
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       FT fa[2], fb[4];
@@ -495,19 +527,23 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[i][c] = F::mfma(fa[i], fb[c], acc[i][c]);
     }
-    if (!more) return false;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1's W1 image, t + 2's words
-    __syncthreads();
-    xclear(t);
-    __syncthreads();          // (a row's words of two tiles may share a position and belong to different threads)
-    xwrite(t + 1, W1);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PEMAX; ++j) W1[j] = W2[j];
+    if (t + 1 >= t1) return false;
+    // the previous step's loads (tile t + 1's W1 image and words, bp(t + 4)) are done; this step's may still fly.
+    // The barriers here are bare s_barrier + lgkmcnt(0) (LDS writes visible): __syncthreads' workgroup release
+    // would also wait for this step's direct-to-LDS loads (vmcnt(0)), i.e. undo the prefetch
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEP_LOADS) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave is done with tile t's images
+    xput(W0, q0, q1, true);                           // clear tile t's words
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (a row's words of two tiles may share a position)
+    xput(W1, q1, q2, false);                          // tile t + 1's
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
     return true;
   };
-  for (int t = t0; t < t1; t += 2)
-    if (!step(t, wsA, wsB) || !step(t + 1, wsB, wsA)) break;
+  for (int t = t0; t < t1; t += 3)                    // (three tiles per trip: each W1 buffer a static LDS object)
+    if (!step(t, wsA, wsC, WX, WY, WZ) || !step(t + 1, wsB, wsA, WY, WZ, WX) || !step(t + 2, wsC, wsB, WZ, WX, WY))
+      break;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // (the last steps' unused loads land before the exit)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -561,15 +597,15 @@ extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
     int32_t* cnt = reinterpret_cast<int32_t*>(a.work);
     uint32_t* ent = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.work) +
                                                  ((int64_t)n_rg * (a.n_tiles + 1) * 4 + 255) / 256 * 256);
-    const dim3 pg((a.n_tiles + et::PK_TPB - 1) / et::PK_TPB, n_rg);
-    hipLaunchKernelGGL(et::pack_count_kernel, pg, dim3(et::PK_TPB), 0, s, a, cnt);
+    const dim3 pg((a.n_tiles + et::PK_TB - 1) / et::PK_TB, n_rg);
+    hipLaunchKernelGGL(et::pack_count_kernel, pg, dim3(et::BM), 0, s, a, cnt);
     hipLaunchKernelGGL(et::pack_scan_kernel, dim3(1), dim3(1024), 0, s, a, cnt, n_rg);
     if (f16) {
-      hipLaunchKernelGGL(et::pack_fill_kernel<_Float16>, pg, dim3(et::PK_TPB), 0, s, a, cnt, ent);
+      hipLaunchKernelGGL(et::pack_fill_kernel<_Float16>, pg, dim3(et::BM), 0, s, a, cnt, ent);
       hipLaunchKernelGGL(et::enc_tiles_packed_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
                          tiles_per);
     } else {
-      hipLaunchKernelGGL(et::pack_fill_kernel<__bf16>, pg, dim3(et::PK_TPB), 0, s, a, cnt, ent);
+      hipLaunchKernelGGL(et::pack_fill_kernel<__bf16>, pg, dim3(et::BM), 0, s, a, cnt, ent);
       hipLaunchKernelGGL(et::enc_tiles_packed_kernel<__bf16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
                          tiles_per);
     }
