@@ -522,10 +522,15 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
         const short e[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         __builtin_memcpy(&fb[c], e, 16);
       }
+#ifndef OCF_ET_NOMFMA
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[i][c] = F::mfma(fa[i], fb[c], acc[i][c]);
+#else
+      acc[0][0][ks] += (float)fa[0][0] + (float)fb[0][0] + (float)fa[1][1] + (float)fb[1][1] + (float)fb[2][2] +
+                       (float)fb[3][3];
+#endif
     }
     if (t + 1 >= t1) return false;
     // the previous step's loads (tile t + 1's W1 image and words, bp(t + 4)) are done; this step's may still fly.
@@ -533,10 +538,12 @@ __global__ void __launch_bounds__(256) enc_tiles_packed_kernel(OcfEncTileArgs a,
     // would also wait for this step's direct-to-LDS loads (vmcnt(0)), i.e. undo the prefetch
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STEP_LOADS) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave is done with tile t's images
+#ifndef OCF_ET_NOX
     xput(W0, q0, q1, true);                           // clear tile t's words
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // (a row's words of two tiles may share a position)
     xput(W1, q1, q2, false);                          // tile t + 1's
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5;
     return true;
   };
@@ -598,10 +605,14 @@ extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
     uint32_t* ent = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.work) +
                                                  ((int64_t)n_rg * (a.n_tiles + 1) * 4 + 255) / 256 * 256);
     const dim3 pg((a.n_tiles + et::PK_TB - 1) / et::PK_TB, n_rg);
+#ifndef OCF_ET_NOPACK
     hipLaunchKernelGGL(et::pack_count_kernel, pg, dim3(et::BM), 0, s, a, cnt);
     hipLaunchKernelGGL(et::pack_scan_kernel, dim3(1), dim3(1024), 0, s, a, cnt, n_rg);
+#endif
     if (f16) {
+#ifndef OCF_ET_NOPACK
       hipLaunchKernelGGL(et::pack_fill_kernel<_Float16>, pg, dim3(et::BM), 0, s, a, cnt, ent);
+#endif
       hipLaunchKernelGGL(et::enc_tiles_packed_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
                          tiles_per);
     } else {
