@@ -216,6 +216,7 @@ typedef struct OcfEncTileArgs {
   int64_t n_entries;
   void* work; int64_t work_bytes;   /* device scratch of ocf_encoder_tiles_workspace(args) bytes: the batch's
                                        entries packed per (256-row group, tile) by a pre-pass in the same call */
+  int64_t max_row_len;    /* an upper bound of the batch rows' lengths (the pre-pass grid)                  */
 } OcfEncTileArgs;
 int64_t ocf_encoder_tiles_workspace(const OcfEncTileArgs* args);
 int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream);

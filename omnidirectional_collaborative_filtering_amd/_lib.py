@@ -73,6 +73,7 @@ class OcfEncTileArgs(ctypes.Structure):
         ("rows", P), ("rp", P), ("tptr", P), ("tcol", P), ("tlidx", P), ("lboff", P), ("xval", P),
         ("W", P), ("ldw", I64), ("w_dtype", I32), ("B", I32), ("Bp", I32), ("n_tiles", I32), ("H", I32),
         ("splits", I32), ("part", P), ("nnz", I64), ("n_entries", I64), ("work", P), ("work_bytes", I64),
+        ("max_row_len", I64),
     ]
 
 

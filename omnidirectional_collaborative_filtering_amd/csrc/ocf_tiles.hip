@@ -351,11 +351,9 @@ __global__ void __launch_bounds__(1024) pack_scan_kernel(OcfEncTileArgs a, int32
   }
 }
 
-// the words: a workgroup per (group, 16 tiles), thread b = row b of the group; the row's position in each tile's
-// bucket = the bucket pointer + the entries of rows < b in that tile (wave prefix sums + the waves before it); the
-// row's entries of the 16 tiles are contiguous in the view and are walked 8 at a time (all loads in flight)
-template <typename CT>
-__global__ void __launch_bounds__(BM) pack_fill_kernel(OcfEncTileArgs a, const int32_t* bptr, uint32_t* ent) {
+// each (batch row, tile)'s first word position: the bucket pointer + the entries of the group's rows before it in
+// that tile (wave prefix sums + the waves before it): a workgroup per (group, 16 tiles), thread b = row b of the group
+__global__ void __launch_bounds__(BM) pack_base_kernel(OcfEncTileArgs a, const int32_t* bptr, int32_t* base) {
   const int rg = blockIdx.y, t0 = blockIdx.x * PK_TB, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __shared__ int tot[4][PK_TB];
   const int b = rg * BM + tid, r = row_of(a, b);
@@ -375,45 +373,45 @@ __global__ void __launch_bounds__(BM) pack_fill_kernel(OcfEncTileArgs a, const i
     if (lane == 63) tot[wave][j] = v;
   }
   __syncthreads();
-  if (r < 0) return;
-  const int64_t rp0 = a.rp[r], lb = a.lboff[b];
-  const int64_t e_end = rp0 + tp[PK_TB];
-  int j = 0;                                            // the tile of the current entry
-  int64_t o = 0;                                        // its word position
-  auto start_of = [&](int jj) {
+  if (b >= a.B) return;
+#pragma unroll
+  for (int j = 0; j < PK_TB; ++j) {
+    if (t0 + j >= a.n_tiles) break;
     int w = 0;
-    for (int k = 0; k < wave; ++k) w += tot[k][jj];
-    return (int64_t)bptr[(int64_t)rg * (a.n_tiles + 1) + t0 + jj] + w + pre[jj];
-  };
-  for (int64_t e0 = rp0 + tp[0]; e0 < e_end; e0 += 8) {
-    int col[8], li[8];
-    float x[8];
+    for (int k = 0; k < wave; ++k) w += tot[k][j];
+    // (relative to the row's first entry of the tile: word position = base + entry position in the row's view)
+    base[(int64_t)b * a.n_tiles + t0 + j] = bptr[(int64_t)rg * (a.n_tiles + 1) + t0 + j] + w + pre[j] - tp[j];
+  }
+}
+
+// the words themselves, a thread per entry of the batch rows' views (grid: batch row x chunks of 1,024 entries):
+// word position = base[b][tile] + the entry's position in the row's view; a run of one (row, column) -- duplicate
+// ratings, adjacent in the column-sorted view -- becomes one word holding the run's sum and invalid words
+constexpr int PK_CHUNK = 1024;
+template <typename CT>
+__global__ void __launch_bounds__(256) pack_words_kernel(OcfEncTileArgs a, const int32_t* base, uint32_t* ent) {
+  const int b = blockIdx.y, r = row_of(a, b);
+  if (r < 0) return;
+  const int64_t rp0 = a.rp[r], len = a.rp[r + 1] - rp0, lb = a.lboff[b];
+  const int32_t* bs = base + (int64_t)b * a.n_tiles;
+  const int rl = b % BM;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int64_t e = min(e0 + k, e_end - 1);
-      col[k] = a.tcol[e];
-      li[k] = a.tlidx[e];
+  for (int k = 0; k < PK_CHUNK / 256; ++k) {
+    const int64_t p = (int64_t)blockIdx.x * PK_CHUNK + 256 * k + threadIdx.x;
+    if (p >= len) break;
+    const int64_t e = rp0 + p;
+    const int col = a.tcol[e], t = col / BK;
+    const bool head = p == 0 || a.tcol[e - 1] != col;
+    uint32_t w = 0;
+    if (head) {
+      float x = a.xval[lb + a.tlidx[e]];
+      for (int64_t f = e + 1; f < rp0 + len && a.tcol[f] == col; ++f) x += a.xval[lb + a.tlidx[f]];
+      const CT h = CvtT<CT>::to(x);
+      uint16_t vb;
+      __builtin_memcpy(&vb, &h, 2);
+      w = (uint32_t)rl | ((uint32_t)(col - t * BK) << 8) | (1u << 15) | ((uint32_t)vb << 16);
     }
-    const int prev = e0 > rp0 + tp[0] ? a.tcol[e0 - 1] : -1;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = a.xval[lb + li[k]];
-    for (int k = 0; k < 8 && e0 + k < e_end; ++k) {
-      const int64_t e = e0 + k;
-      while (e >= rp0 + tp[j + 1]) ++j;                 // (entries are column-sorted: tiles in order)
-      if (e == rp0 + tp[j]) o = start_of(j);
-      const int t = t0 + j;
-      const bool first = (k == 0 ? prev : col[k - 1]) != col[k] || e == rp0 + tp[j];
-      uint32_t w = 0;                                   // (an invalid word: merged into the one before it)
-      if (first) {
-        float v = x[k];
-        for (int64_t f = e + 1; f < rp0 + tp[j + 1] && a.tcol[f] == col[k]; ++f) v += a.xval[lb + a.tlidx[f]];
-        const CT h = CvtT<CT>::to(v);
-        uint16_t vb;
-        __builtin_memcpy(&vb, &h, 2);
-        w = (uint32_t)tid | ((uint32_t)(col[k] - t * BK) << 8) | (1u << 15) | ((uint32_t)vb << 16);
-      }
-      ent[o++] = w;
-    }
+    ent[bs[t] + p] = w;
   }
 }
 
@@ -573,10 +571,25 @@ namespace ocf {
 int g_enc_tiles_pack = 1;   // ocf_set_tuning "enc_tiles_pack": the packed pre-pass (1) or the per-row chain (0)
 }
 
+namespace {
+struct TileWork {   // the pre-pass scratch: bucket pointers [n_rg][n_tiles + 1], row bases [B][n_tiles], words
+  int64_t cnt, base, ent, total;
+};
+TileWork tile_work(const OcfEncTileArgs& a) {
+  const int64_t n_rg = (a.Bp + et::BM - 1) / et::BM;
+  auto r = [](int64_t bytes) { return (bytes + 255) / 256 * 256; };
+  TileWork w;
+  w.cnt = 0;
+  w.base = r(n_rg * (a.n_tiles + 1) * 4);
+  w.ent = w.base + r((int64_t)std::max(a.B, 1) * a.n_tiles * 4);
+  w.total = w.ent + r(std::max<int64_t>(a.n_entries, 1) * 4);
+  return w;
+}
+}  // namespace
+
 extern "C" int64_t ocf_encoder_tiles_workspace(const OcfEncTileArgs* a) {
-  if (!a || a->Bp < 0 || a->n_tiles < 1 || a->n_entries < 0) return -1;
-  const int64_t n_rg = (a->Bp + et::BM - 1) / et::BM;
-  return (n_rg * (a->n_tiles + 1) * 4 + 255) / 256 * 256 + (std::max<int64_t>(a->n_entries, 1) * 4 + 255) / 256 * 256;
+  if (!a || a->Bp < 0 || a->B < 0 || a->n_tiles < 1 || a->n_entries < 0) return -1;
+  return tile_work(*a).total;
 }
 
 extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
@@ -601,22 +614,30 @@ extern "C" int ocf_encoder_tiles(const OcfEncTileArgs* args, void* stream) {
   if (g_enc_tiles_pack) {
     const int64_t need = ocf_encoder_tiles_workspace(&a);
     OCF_CHECK(a.work && a.work_bytes >= need, "ocf_encoder_tiles: workspace too small (ocf_encoder_tiles_workspace)");
-    int32_t* cnt = reinterpret_cast<int32_t*>(a.work);
-    uint32_t* ent = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.work) +
-                                                 ((int64_t)n_rg * (a.n_tiles + 1) * 4 + 255) / 256 * 256);
+    const TileWork tw = tile_work(a);
+    char* wb = reinterpret_cast<char*>(a.work);
+    int32_t* cnt = reinterpret_cast<int32_t*>(wb + tw.cnt);
+    int32_t* base = reinterpret_cast<int32_t*>(wb + tw.base);
+    uint32_t* ent = reinterpret_cast<uint32_t*>(wb + tw.ent);
     const dim3 pg((a.n_tiles + et::PK_TB - 1) / et::PK_TB, n_rg);
+    int64_t max_len = a.max_row_len > 0 ? a.max_row_len : 0;
+    OCF_CHECK(max_len > 0, "ocf_encoder_tiles: max_row_len (the longest batch row's view length) required");
+    const dim3 wg((unsigned)((max_len + et::PK_CHUNK - 1) / et::PK_CHUNK), (unsigned)a.B);
 #ifndef OCF_ET_NOPACK
     hipLaunchKernelGGL(et::pack_count_kernel, pg, dim3(et::BM), 0, s, a, cnt);
     hipLaunchKernelGGL(et::pack_scan_kernel, dim3(1), dim3(1024), 0, s, a, cnt, n_rg);
+    hipLaunchKernelGGL(et::pack_base_kernel, pg, dim3(et::BM), 0, s, a, cnt, base);
 #endif
     if (f16) {
 #ifndef OCF_ET_NOPACK
-      hipLaunchKernelGGL(et::pack_fill_kernel<_Float16>, pg, dim3(et::BM), 0, s, a, cnt, ent);
+      if (a.B) hipLaunchKernelGGL(et::pack_words_kernel<_Float16>, wg, dim3(256), 0, s, a, base, ent);
 #endif
       hipLaunchKernelGGL(et::enc_tiles_packed_kernel<_Float16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
                          tiles_per);
     } else {
-      hipLaunchKernelGGL(et::pack_fill_kernel<__bf16>, pg, dim3(et::BM), 0, s, a, cnt, ent);
+#ifndef OCF_ET_NOPACK
+      if (a.B) hipLaunchKernelGGL(et::pack_words_kernel<__bf16>, wg, dim3(256), 0, s, a, base, ent);
+#endif
       hipLaunchKernelGGL(et::enc_tiles_packed_kernel<__bf16>, dim3(grid), dim3(256), 0, s, a, cnt, ent, n_rg, n_hs,
                          tiles_per);
     }

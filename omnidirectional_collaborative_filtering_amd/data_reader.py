@@ -90,7 +90,8 @@ class _DeviceCSR:
             d = self.dev
             self._tiles[n_cols] = dict(t_col=torch.as_tensor(col_s, device=d), t_val=torch.as_tensor(val_s, device=d),
                                        t_lidx=torch.as_tensor(lidx_s, device=d), t_tptr=torch.as_tensor(tptr, device=d),
-                                       t_ntiles=tptr.shape[1] - 1)
+                                       t_ntiles=tptr.shape[1] - 1,
+                                       t_maxlen=int(self.lens.max()) if len(self.lens) else 0)
         return self._tiles[n_cols]
 
 

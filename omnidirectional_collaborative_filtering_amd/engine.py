@@ -50,10 +50,13 @@ FUSE_MAX_CHUNKS = 256
 # partials (O(chunks^2) per row).  Netflix (~22 chunks per row): 2.029 -> 1.997 ms/step with the separate launch
 # (profiles/r05_cfg/nf_base.jsonl); ML-20M (~3): the fused form
 FUSE_MEAN_CHUNKS = 8
-# the encoder as an MFMA contraction over 128-column tiles of W1 (ocf_encoder_tiles) instead of row gathers: when
-# a weight row carries this many batch entries on average (the gathers read a W1 row per entry, the tiles read
-# each tile once per 256 batch rows) on a weight of at least ENC_TILES_MIN_TILES tiles, 16-bit compute
-ENC_TILES_MIN_ENTRIES = 2.0
+# the encoder as an MFMA contraction over 128-column tiles of W1 (ocf_encoder_tiles) instead of row gathers, when
+# a weight row carries this many batch entries on average (the gathers read a W1 row per entry, the tiles read each
+# tile once per 256 batch rows) on a weight of at least ENC_TILES_MIN_TILES tiles, 16-bit compute.  Measured in
+# round 6 (tools/probes/enc_tiles_probe.py, profiles/r06_tiles/): pre-pass + tile kernel vs the gather encoder
+# Netflix 211 vs 207 us, the 8-way Netflix rank 196 vs 165, the 8-way ML-20M rank 88 vs 28 -- it does not win
+# anywhere yet, so the automatic choice never takes it (engine.enc_tiles = True forces it)
+ENC_TILES_MIN_ENTRIES = float("inf")
 ENC_TILES_MIN_TILES = 64
 ENC_TILES_WGS = 256           # workgroups to aim for (one per CU): splits = WGS / (row groups x hidden slices)
 DTYPES = {"float32": (_lib.DT_F32, torch.float32), "float16": (_lib.DT_F16, torch.float16),
@@ -931,6 +934,7 @@ class Engine:
         a.W, a.ldw, a.w_dtype = ptr(Wt), Wt.shape[1], wdt
         a.B, a.Bp, a.n_tiles, a.H, a.splits, a.part = self.B, self.Bp, self.n_tiles, Hp0, S, ptr(part)
         a.nnz, a.n_entries = t["t_col"].numel(), max(int(self.gt["E"]), 1)
+        a.max_row_len = max(int(t.get("t_maxlen", 0)), 1)
         nb = int(_lib.load().ocf_encoder_tiles_workspace(ctypes.byref(a)))
         if nb < 0:
             raise _lib.OcfError("ocf_encoder_tiles_workspace: bad arguments")

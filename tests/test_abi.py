@@ -57,7 +57,7 @@ STRUCTS = {
                                        "sp_rowent", "jr", "sp_nent", "dn_t", "ld_dn", "dn_rows"]),
     "OcfPairSync": (_lib.OcfPairSync, ["word", "count"]),
     "OcfEncTileArgs": (_lib.OcfEncTileArgs, ["rows", "xval", "ldw", "w_dtype", "B", "splits", "part", "nnz",
-                                             "n_entries", "work", "work_bytes"]),
+                                             "n_entries", "work", "work_bytes", "max_row_len"]),
     "OcfMlpStepArgs": (_lib.OcfMlpStepArgs, ["n_hidden", "Bp", "k_blocks", "hidden", "hidden_p", "x", "ld_x", "rows",
                                              "targets", "ld_t", "W", "b", "sW2", "sb2", "shadow", "shadow_blocked",
                                              "act", "compute_dtype", "opt", "stats", "work", "work_bytes", "barrier",
