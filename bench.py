@@ -71,63 +71,9 @@ def parse():
                          "numerics of a partial model); not a bench line")
     ap.add_argument("--emulate-comm", type=int, default=1,
                     help="with --emulate-shards: run the rank's collective code path with no-op collectives")
-    ap.add_argument("--sparse-dw", type=int, default=-1,
-                    help="weight-gradient GEMMs build their batch operand in LDS from the entries (-1: engine's "
-                         "choice by batch size)")
-    ap.add_argument("--gather", type=int, default=1,
-                    help="row-gather encoder/decoder for generator batches (0: dense MFMA GEMMs)")
-    ap.add_argument("--ws-max-k", type=int, default=0,
-                    help="largest batch K routed to the role-split dW kernel (0: library default)")
-    ap.add_argument("--rows-long", type=int, default=-1,
-                    help="row-stream dW kernel's LONG variant (entries as vectors): -1 library's choice (>= 4 "
-                         "entries per weight row), 0 never, 1 always")
-    ap.add_argument("--rows-small-waves", type=int, default=-1,
-                    help="row-stream dW kernel: 32 workgroups per 128-row tile when 12 would give fewer waves than "
-                         "this (-1: library default)")
-    ap.add_argument("--rows-dual", type=int, default=-1,
-                    help="small weights: both updates in one dual-row launch (1, library default) or two (0)")
-    ap.add_argument("--rows-dual-parts", type=int, default=-1,
-                    help="dual-row launch: workgroups per 128-row tile (0: library's choice by size, else 1..64)")
-    ap.add_argument("--rows-dual-pf", type=int, default=-2,
-                    help="dual-row launch: the next row's chain issued ahead (-1 library's choice, 0, 1)")
-    ap.add_argument("--rows-dual-large", type=int, default=-1,
-                    help="the dual-row launch on large weights too (1; with --reduce-in-decoder 1) or the pair launch (0)")
-    ap.add_argument("--reduce-in-decoder", type=int, default=-1,
-                    help="the hidden delta's row reduction in the decoder launch (1) or as dW_out jobs (0); -1: "
-                         "engine default (small weights)")
-    ap.add_argument("--rowlist-rg-work", type=int, default=0,
-                    help="row-list builds: (batches x row groups) to aim for (0: data_reader.ROWLIST_RG_WORK)")
-    ap.add_argument("--fuse-enc-dec", type=int, default=-1,
-                    help="the encoder and the decoder gather as one launch (ocf_gather_encdec; 0: two launches; -1: "
-                         "the engine's choice, large weights)")
     ap.add_argument("--enc-tiles", type=int, default=-1,
                     help="the encoder over column tiles on the matrix cores (ocf_encoder_tiles; 1), the row gathers (0), "
                          "or the engine's choice by entries per weight row (-1)")
-    ap.add_argument("--enc-tiles-pack", type=int, default=-1,
-                    help="ocf_encoder_tiles' packed pre-pass (1, library default) or the per-row entry chain (0)")
-    ap.add_argument("--gather-chunk", type=int, default=0,
-                    help="entries per row-gather chunk of large batches (0: data_reader.GATHER_CHUNK)")
-    ap.add_argument("--fold-reduce", type=int, default=1,
-                    help="the hidden delta's row reduction folded into a launch (decoder or dW_out; 0: its own "
-                         "ocf_rows_reduce launch)")
-    ap.add_argument("--fold-jobs", type=int, default=1,
-                    help="stats and bias updates folded into the dW_out launch (0: separate launches)")
-    ap.add_argument("--shadow-blocked", type=int, default=-1,
-                    help="half-width weight shadows 64x64-blocked (1) or row-major (0); -1: engine default")
-    ap.add_argument("--split-dw", type=int, default=1,
-                    help="feature parallel: output-layer weight update on a side stream, overlapping the input layer's")
-    ap.add_argument("--fuse-enc", type=int, default=1,
-                    help="single GPU, one hidden layer: the decoder gather applies the hidden layer's bias / "
-                         "activation / dropout to the encoder partials itself (0: separate row-reduce launch)")
-    ap.add_argument("--epoch-lists", type=int, default=1,
-                    help="weight-gradient row lists built per epoch by the generator (ocf_epoch_row_lists; the "
-                         "timed region includes building them for the timed batches) instead of per step")
-    ap.add_argument("--fused-mlp", type=int, default=1,
-                    help="small models (Jester, ML-100K, ML-1M): the whole step in one launch (ocf_mlp_step; 0: the "
-                         "layer-wise dense path / the row gathers)")
-    ap.add_argument("--row-skip", type=int, default=1,
-                    help="Adagrad: skip the optimizer traffic of weight rows without a batch entry (zero "
-                         "gradient, identity update; bit-identical)")
     ap.add_argument("--parallel", default="feature", choices=["feature", "dp"],
                     help="N>1: feature (column-sharded W1/W_out, 2 x [B,H] all-reduces per step) or dp "
                          "(replicated weights, gradient exchange)")
@@ -489,7 +435,6 @@ def jester_main(args):
     m.compile("rmsprop", "mean_squared_error", metrics=["mae", "accurate_MAE", "nMAE"])
     w0 = m.get_weights()
     e = om.engine
-    e.fused_mlp = bool(args.fused_mlp)
     split_at = int(n * 0.9)
     np.random.seed(42)
     idx = np.arange(split_at)
@@ -678,15 +623,10 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    from omnidirectional_collaborative_filtering_amd import data_reader as _dr
     from omnidirectional_collaborative_filtering_amd.data_reader import data_reader
     from omnidirectional_collaborative_filtering_amd.dataset import synthetic_fixed_split
     from omnidirectional_collaborative_filtering_amd.model import omni_model
 
-    if args.rowlist_rg_work > 0:
-        _dr.ROWLIST_RG_WORK = args.rowlist_rg_work
-    if args.gather_chunk > 0:
-        _dr.GATHER_CHUNK = args.gather_chunk
     t0 = time.time()
     data_full = synthetic_fixed_split(args.config, seed=0, skew=args.skew)
     N = data_full.num_cols
@@ -717,42 +657,8 @@ def main():
     m.compile(optim(args.optimizer, lr), "mean_squared_error", metrics=["mae", "accurate_MSE", "accurate_RMSE"])
     w0 = m.get_weights() if (rank == 0 and world == 1 and args.cpu_baseline) else None
     eng = om.engine
-    if args.sparse_dw >= 0:
-        eng.sparse_dw = bool(args.sparse_dw)
-    eng.use_sparse = bool(args.gather)
-    eng.row_skip = bool(args.row_skip)
-    eng.fold_jobs = bool(args.fold_jobs)
-    eng.fold_reduce = bool(args.fold_reduce)
-    if args.fuse_enc_dec >= 0:
-        eng.fuse_enc_dec = bool(args.fuse_enc_dec)
-    if args.reduce_in_decoder >= 0:
-        eng.reduce_in_decoder = bool(args.reduce_in_decoder)
     if args.enc_tiles >= 0:
         eng.enc_tiles = bool(args.enc_tiles)
-    eng.split_dw_streams = bool(args.split_dw)
-    eng.fuse_enc_epilogue = bool(args.fuse_enc)
-    eng.epoch_row_lists = bool(args.epoch_lists)
-    eng.fused_mlp = bool(args.fused_mlp)
-    if args.shadow_blocked >= 0 and eng.shadow_blocked != bool(args.shadow_blocked):
-        eng.shadow_blocked = bool(args.shadow_blocked)
-        eng._refresh_shadows()
-    from omnidirectional_collaborative_filtering_amd import _lib
-    if args.ws_max_k:
-        _lib.call("ocf_set_tuning", b"optim_ws_max_k", int(args.ws_max_k), None)
-    if args.rows_long >= 0:
-        _lib.call("ocf_set_tuning", b"rows_long", int(args.rows_long), None)
-    if args.rows_dual >= 0:
-        _lib.call("ocf_set_tuning", b"rows_dual", int(args.rows_dual), None)
-    if args.rows_dual_parts >= 0:
-        _lib.call("ocf_set_tuning", b"rows_dual_parts", int(args.rows_dual_parts), None)
-    if args.rows_dual_pf >= -1:
-        _lib.call("ocf_set_tuning", b"rows_dual_pf", int(args.rows_dual_pf), None)
-    if args.rows_dual_large >= 0:
-        _lib.call("ocf_set_tuning", b"rows_dual_large", int(args.rows_dual_large), None)
-    if args.enc_tiles_pack >= 0:
-        _lib.call("ocf_set_tuning", b"enc_tiles_pack", int(args.enc_tiles_pack), None)
-    if args.rows_small_waves >= 0:
-        _lib.call("ocf_set_tuning", b"rows_small_waves", int(args.rows_small_waves), None)
     gen = rd.data_gen(Bg, [1.0, 1.0], "train", True, None, -1, pass_through_input_training=True)
     gen._start()
     batches = list(range(gen.num_batches)) if (fp or world == 1) else shard_batches(gen.num_batches, rank, world)

@@ -34,6 +34,12 @@ constexpr int RG_MAX_H = 512;
 #define OCF_RG_U 4
 #endif
 constexpr int RG_U = OCF_RG_U;   // entries per group in flight
+#ifndef OCF_RG_UE
+#define OCF_RG_UE 4
+#endif
+// ... in the encoder chunks of the fused encoder -> decoder launch: that kernel's register allocation is the
+// decoder's (133 VGPRs at f16), so the encoder part can keep more entries in flight at no occupancy cost
+constexpr int RG_UE = OCF_RG_UE;
 #ifndef OCF_RG_UD
 #define OCF_RG_UD 4
 #endif
@@ -229,7 +235,7 @@ __device__ __forceinline__ void dec_zero_rows(const OcfRowsReduceArgs& r) {
 // contiguous bytes.
 // chunk c of the encoder.  wt (the fused encoder -> decoder launch, gather_encdec_kernel): the partial is stored
 // write-through and the chunk counts itself in enc_arrive[b] once its stores have landed
-template <typename WT, int G, int PPL>
+template <typename WT, int G, int PPL, int RG_U = ocf::RG_U>
 __device__ __forceinline__ void encoder_chunk(const OcfGatherArgs& a, const int c, float* red, uint32_t* enc_arrive) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
@@ -527,7 +533,7 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encdec_kernel(OcfGatherArgs
                                                                    OcfRowsReduceArgs jr, EncDecSync sy) {
   __shared__ float red[(RG_THREADS / G) * RG_MAX_H];
   const int bx = blockIdx.x;
-  if (bx < e.n_chunks) encoder_chunk<WT, G, PPL>(e, bx, red, sy.enc_arrive);
+  if (bx < e.n_chunks) encoder_chunk<WT, G, PPL, RG_UE>(e, bx, red, sy.enc_arrive);
   else decoder_chunk<WT, HT, G, PPL>(d, jr, bx - e.n_chunks, bx == e.n_chunks, red, sy);
 }
 

@@ -329,9 +329,6 @@ class Engine:
         # row lists serve every sparse first / last layer of up to 512 hidden units, fp32 and 16-bit).
 
         self.tb = None
-        self.fold_jobs = True       # stats + bias updates folded into the dW_out launch (no side stream)
-        # feature parallel: the output layer's weight update on the side stream (see _backward_gather)
-        self.split_dw_streams = True
         # one hidden layer, one GPU: the decoder gather applies the hidden layer's epilogue to the encoder's
         # chunk partials (no separate row-reduce launch between the two gathers)
         self.fuse_enc_epilogue = True
@@ -1095,7 +1092,7 @@ class Engine:
     def _folds(self):
         """single-GPU row-gather step with the fused optimizer: the stats finalisation and both
         bias updates ride in the output-layer dW launch instead of side-stream kernels"""
-        return (self.fold_jobs and self.gt is not None and self.comm is None and len(self.H) == 1
+        return (self.gt is not None and self.comm is None and len(self.H) == 1
                 and self.sparse_dw and self.tb is not None and self.trainable[1])
 
     def _flush_stats(self):
@@ -1239,7 +1236,7 @@ class Engine:
                 # the output layer's update needs only the deltas and h, not the summed dh: it runs
                 # while the all-reduce of the dh partials is in flight on the collective's stream
                 work = start(self.dhpre)
-                if self.side is not None and self.split_dw_streams:
+                if self.side is not None:
                     # ... on the side stream, so the input layer's update (main stream, after the
                     # all-reduce) fills the CUs the output layer's last tiles leave idle
                     self._fork()
@@ -1335,7 +1332,7 @@ class Engine:
             self._grad_ready(i, grads_out)
             db_last, parts_last = self.db_h[i - 1], parts_next
         jobs_in = None
-        if fused and L == 1 and self.comm is not None and self.fold_jobs and self.trainable[0]:
+        if fused and L == 1 and self.comm is not None and self.trainable[0]:
             # feature parallelism: the hidden-bias update from the δh partial rows rides in the input layer's
             # launch as a job (the same sums) instead of a kernel ahead of it on the critical path (8-way rank:
             # 512 partial rows, 40 us as a separate launch)
@@ -1474,13 +1471,13 @@ class Engine:
         key = (tok, self._bufgen, id(self.opt), self.opt.lr, self.opt.decay, getattr(self.opt, "epsilon", 0.0),
                self.row_skip, self.shadow_blocked, self.keep,
                self.seed, self.act, self.comm, self.dp_world, self.use_sparse, self.sparse_dw, self.epoch_row_lists,
-               self.epoch_scatter, self.fold_jobs, self.fold_reduce, self.fuse_enc_epilogue, self.l2,
+               self.epoch_scatter, self.fold_reduce, self.fuse_enc_epilogue, self.l2,
                tuple(self.trainable), self.grad_hook, self.master_sync, self.pair_dw, self.fuse_enc_dec)
         pl = self._plan
         if pl is not None and pl["key"] == key:
             return key
         if not (self.comm is None and self.dp_world == 1 and len(self.H) == 1 and self.sparse_ok and self.use_sparse
-                and self.sparse_dw and self.epoch_row_lists and self.epoch_scatter and self.fold_jobs and
+                and self.sparse_dw and self.epoch_row_lists and self.epoch_scatter and
                 self.fold_reduce and self.fuse_enc_epilogue and not self.l2 and all(self.trainable) and
                 self.grad_hook is None and self.master_sync is None):
             return None
@@ -1725,12 +1722,12 @@ class Engine:
             tok = gen._step_token = Engine._gen_tokens
         if not (self.comm is not None and getattr(self.comm, "start", None) is not None and self.dp_world == 1
                 and len(self.H) == 1 and self.sparse_ok and self.use_sparse and self.sparse_dw
-                and self.epoch_row_lists and self.epoch_scatter and self.fold_jobs and not self.l2
+                and self.epoch_row_lists and self.epoch_scatter and not self.l2
                 and all(self.trainable) and self.grad_hook is None and self.master_sync is None
                 and self.opt.kind != _lib.OPT_ADAM and not self.opt.decay):
             return None
         return (tok, self._bufgen, id(self.opt), self.opt.lr, getattr(self.opt, "epsilon", 0.0), self.row_skip,
-                self.shadow_blocked, self.keep, self.seed, self.act, id(self.comm), self.split_dw_streams,
+                self.shadow_blocked, self.keep, self.seed, self.act, id(self.comm),
                 self.side is not None)
 
     def _fast_rank_step(self, gen, bi):
