@@ -718,14 +718,18 @@ def main():
         gen.prepare_row_lists(eng.Np, [batches[(args.warmup + i) % len(batches)] for i in range(args.steps)])
     t_lists = time.perf_counter()
     # the dominant kernel's HIP events on every TIMER_EVERY-th timed step (TIMER_EVERY_SHORT-th for a kernel under
-    # 0.1 ms): each event record idles the stream ~6 us (measured: 0 vs 5.8 us launch gaps with and without), so
-    # sampling keeps the timing overhead at ~0.5 % of the step while still averaging over the whole timed region
+    # 0.1 ms): each event record idles the stream ~4.7 us even without its system-scope fence (rocprof trace,
+    # profiles/r06_events/), so sampling keeps the timing overhead small while still averaging over the whole timed
+    # region (every 4th vs every 10th step at ML-20M: 0.3821 vs 0.3820 ms, same box)
     sampled = {dom} if dom else None
     every = TIMER_EVERY if (not dom or phases[dom]["mean_ms"] >= 0.1) else TIMER_EVERY_SHORT
     t_first = None
+    # (the samples end each group of `every` steps: the first step of the window, issued while the GPU waits on
+    # the host, takes no timer bookkeeping)
+    first_sample = min(every, args.steps) - 1
     for i in range(args.steps):
         if dom:
-            eng.timer_only = sampled if i % every == 0 else {"-"}
+            eng.timer_only = sampled if i % every == first_sample else {"-"}
         nnz += step(args.warmup + i)
         if t_first is None:
             t_first = time.perf_counter()

@@ -734,6 +734,16 @@ int ocf_set_tuning(const char* key, int value, int* previous);
  * (Engine.take_stats at every epoch end), so a fault in the last launches of a run cannot go unseen. */
 int ocf_check_async(void);
 
+/* Timing events for measurement (bench.py's HIP-event timing of the dominant launch; no reference counterpart).
+ * ocf_timing_event_create makes an event with hipEventDisableSystemFence: recording it takes no system-scope
+ * cache write-back and invalidate.  With the default flags (torch.cuda.Event) every record idled the stream
+ * ~5.7 us and started the next launch on a flushed L2.  Such an event is only for ocf_event_elapsed_ms after a
+ * device synchronisation; it orders nothing.  *ev receives the hipEvent_t. */
+int ocf_timing_event_create(void** ev);
+int ocf_event_record(void* ev, void* stream);
+int ocf_event_elapsed_ms(void* start, void* stop, float* ms);
+int ocf_event_destroy(void* ev);
+
 int ocf_version(void);
 const char* ocf_last_error(void);
 

@@ -270,6 +270,10 @@ SIGNATURES = {
     "ocf_check_async": (I32, []),
     "ocf_encoder_tiles": (I32, [ctypes.POINTER(OcfEncTileArgs), P]),
     "ocf_encoder_tiles_workspace": (I64, [ctypes.POINTER(OcfEncTileArgs)]),
+    "ocf_timing_event_create": (I32, [ctypes.POINTER(P)]),
+    "ocf_event_record": (I32, [P, P]),
+    "ocf_event_elapsed_ms": (I32, [P, P, ctypes.POINTER(F32)]),
+    "ocf_event_destroy": (I32, [P]),
     "ocf_version": (I32, []),
     "ocf_last_error": (ctypes.c_char_p, []),
 }
@@ -301,6 +305,32 @@ def load(path: str = LIB_PATH):
 # encoder -> decoder hand-off counters (an encoder chunk that arrived after its row's decoder gave up leaves a
 # count behind; ocf.h ocf_gather_encdec)
 enc_wait_hooks = []
+
+
+class TimingEvent:
+    """A HIP event for timing only (ocf_timing_event_create: hipEventDisableSystemFence -- a record costs no
+    system-scope cache write-back / invalidate); the torch.cuda.Event surface the engine's timers use
+    (cuda_event, record, elapsed_time).  Read it after a device synchronisation."""
+    __slots__ = ("cuda_event",)
+
+    def __init__(self):
+        p = P()
+        call("ocf_timing_event_create", ctypes.byref(p))
+        self.cuda_event = p.value
+
+    def record(self, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        call("ocf_event_record", self.cuda_event, s.cuda_stream)
+
+    def elapsed_time(self, end):
+        ms = F32()
+        call("ocf_event_elapsed_ms", self.cuda_event, end.cuda_event, ctypes.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        if _lib is not None and self.cuda_event:
+            _lib.ocf_event_destroy(self.cuda_event)
 
 
 def call(name, *args):

@@ -281,6 +281,35 @@ extern "C" int ocf_sumsq(const float* x, int64_t n, float scale, float* ws, floa
   OCF_TRY_END
 }
 
+extern "C" int ocf_timing_event_create(void** ev) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(ev != nullptr, "ocf_timing_event_create: null pointer");
+  hipEvent_t e = nullptr;
+  OCF_HIP(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  *ev = e;
+  OCF_TRY_END
+}
+extern "C" int ocf_event_record(void* ev, void* stream) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(ev != nullptr, "ocf_event_record: null event");
+  OCF_HIP(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+  OCF_TRY_END
+}
+extern "C" int ocf_event_elapsed_ms(void* start, void* stop, float* ms) {
+  OCF_TRY_BEGIN
+  OCF_CHECK(start && stop && ms, "ocf_event_elapsed_ms: null pointer");
+  OCF_HIP(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  OCF_TRY_END
+}
+// (no pending-error check: a destructor's call must not consume an asynchronous error it cannot report)
+extern "C" int ocf_event_destroy(void* ev) {
+  if (ev && hipEventDestroy((hipEvent_t)ev) != hipSuccess) {
+    set_error("ocf_event_destroy: hipEventDestroy failed");
+    return 1;
+  }
+  return 0;
+}
+
 extern "C" int ocf_version(void) { return 1; }
 extern "C" const char* ocf_last_error(void) { return g_last_error.c_str(); }
 

@@ -423,9 +423,9 @@ class Engine:
         pool = self.__dict__.get("_ev_pool")
         if pool:
             return pool.pop()
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()                     # (creates the event; the library records it again where it is passed)
-        return e
+        # (hipEventDisableSystemFence: a torch.cuda.Event record idled the stream ~5.7 us for its system-scope
+        # cache write-back / invalidate and left the timed launch a cold L2)
+        return _lib.TimingEvent()
 
     class _Phase:
         def __init__(self, eng, name):
