@@ -706,12 +706,12 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     eng.enable_timers(dom is not None, only=[dom] if dom else None)
+    fused_step = dom == "mlp_step"          # a small model: dense arrays + ocf_mlp_step, no row lists
+    epoch_lists = eng.epoch_row_lists and eng.sparse_dw and eng.use_sparse and not fused_step
     torch.cuda.synchronize()
     paths0 = dict(eng.step_paths)
     t_start = time.perf_counter()
     nnz = 0
-    fused_step = dom == "mlp_step"          # a small model: dense arrays + ocf_mlp_step, no row lists
-    epoch_lists = eng.epoch_row_lists and eng.sparse_dw and eng.use_sparse and not fused_step
     if epoch_lists:
         # the timed batches' row lists, built inside the timed region (one launch sequence, as at the
         # start of every training epoch)

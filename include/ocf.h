@@ -122,7 +122,7 @@ int ocf_scatter_batch(const OcfScatterArgs* args, void* stream);
  * generator's seeds) and writes xval / tflag at ebase[s] - ebase0 .. ebase[s + 1] - ebase0; max_e = max entries
  * of a batch.  ebase0 lets sel / ebase point into epoch-wide device tables (a window of consecutive batches
  * needs no upload): 0 when ebase starts at 0.
- * Extension (no reference counterpart): the data_reader.py:95-200 batch assembly, per epoch. */
+ * B <= 4,096.  Extension (no reference counterpart): the data_reader.py:95-200 batch assembly, per epoch. */
 typedef struct OcfEpochScatterArgs {
   int n_sel; const int32_t* sel; const int64_t* ebase; int64_t max_e;
   const int64_t* keep_off; uint64_t stream_mul;

@@ -64,7 +64,7 @@ def main():
                 rec = {"tag": a.tag, "label": lab, "rep": rep, "ms_per_step": d.get("ms_per_step"),
                        "kernel": roof.get("kernel"), "kernel_mean_us": roof.get("kernel_mean_us"),
                        "frac": roof.get("frac"), "phases_ms": d.get("phases_ms"), "args": args, "env": env,
-                       "extra": {k: d[k] for k in ("configs", "masked_rmse", "value") if k in d}}
+                       "extra": {k: d[k] for k in ("configs", "masked_rmse", "value", "window_host_us") if k in d}}
                 f.write(json.dumps(rec) + "\n")
                 f.flush()
                 res[lab].append(rec)
