@@ -537,6 +537,250 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encdec_kernel(OcfGatherArgs
   else decoder_chunk<WT, HT, G, PPL>(d, jr, bx - e.n_chunks, bx == e.n_chunks, red, sy);
 }
 
+// The row-resident form of the encoder -> decoder launch (ocf_gather_encdec, 16-bit weights; tuning
+// "encdec_rowres"): ONE 1,024-thread workgroup per batch row runs the row's whole encoder sum, the hidden epilogue,
+// the decoder over the row's targets and the hidden delta's reduction, with the partial sums reduced in LDS -- no
+// chunk partials through memory, no per-row arrival counters, no workgroup waiting for another.  The chunked form
+// (gather_encdec_kernel) ran the row's encoder and decoder as ~3 + ~3 workgroups of 256 threads each with those
+// hand-offs, at 3 waves per SIMD.  Arithmetic per entry as in encoder_chunk / decoder_chunk; the sums run over the
+// row's entries in another order (per lane group, then over the groups in a fixed order), so the results equal the
+// chunked form's to fp32 rounding, not bit for bit.
+constexpr int RR_THREADS = 1024;
+constexpr int RR_WAVES = RR_THREADS / 64;
+#ifndef OCF_RR_UD
+#define OCF_RR_UD 2
+#endif
+#ifndef OCF_RR_UE
+#define OCF_RR_UE 4
+#endif
+constexpr int RR_UE = OCF_RR_UE;   // entries per group in flight in the encoder part
+// ... in the decoder part: 2 (115 VGPRs); 3 spilled 44 B per lane at the 1,024-thread workgroup's 128 VGPRs and
+// 4 148 B.  ML-20M, same box: chunked 0.3802, row-resident with 3 0.3770, with 2 0.3626 ms/step
+// (profiles/r06_rowres/)
+constexpr int RR_UD = OCF_RR_UD;
+
+// the groups' per-lane vectors summed into red[wave][x]: the groups of one wave by lane shuffles (a fixed xor
+// tree), then the waves' rows by the caller in wave order
+template <int G, int V, int E, int PPL>
+__device__ __forceinline__ void rr_wave_sums(float (&acc)[V], float (*red)[RG_MAX_H], int l, int lane, int w) {
+#pragma unroll
+  for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+  if (lane < G) {
+#pragma unroll
+    for (int i = 0; i < PPL; ++i)
+#pragma unroll
+      for (int k = 0; k < E; ++k) red[w][(l + G * i) * E + k] = acc[i * E + k];
+  }
+}
+__device__ __forceinline__ float rr_row_sum(const float (*red)[RG_MAX_H], int x) {
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int w = 0; w < RR_WAVES; w += 2) {
+    s0 += red[w][x];
+    s1 += red[w + 1][x];
+  }
+  return s0 + s1;
+}
+
+template <typename WT, typename HT, int G, int PPL>
+__global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs e, OcfGatherArgs d,
+                                                                   OcfRowsReduceArgs r) {
+  constexpr int E = EPc<WT>::v;
+  constexpr int V = PPL * E;
+  constexpr int NG = RR_THREADS / G;
+  __shared__ float red[RR_WAVES][RG_MAX_H];
+  __shared__ float h_sh[RG_MAX_H];
+  __shared__ float a_sh[RG_MAX_H];
+  __shared__ uint8_t mk_sh[RG_MAX_H];
+  __shared__ float st_sh[NG][3];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int grp = tid / G, l = tid % G;
+  const int H = d.H;
+  const int64_t rb = (int64_t)b * H;
+  if (d.zero_word && b == 0 && tid == 0) __hip_atomic_store(d.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int row = b < r.B ? d.rows[b] : -1;
+  const int64_t lb = b < r.B ? d.lboff[b] : 0;
+  const int n_e = row >= 0 ? (int)(d.lboff[b + 1] - lb) : 0;
+  if (n_e == 0) {            // padding rows, rows without entries: the reduction's outputs of an empty row
+    for (int x = tid; x < H; x += RR_THREADS) {
+      store_ct(r.h_out, r.h_dtype, rb + x, 0.f);
+      if (r.db_part) r.db_part[rb + x] = 0.f;
+    }
+    if (tid < 4) r.stats_part[(int64_t)b * 4 + tid] = 0.f;
+    if (tid == 0 && r.row_sse) r.row_sse[b] = 0.f;
+    return;
+  }
+  const int64_t s = d.rp[row];
+  // ---- encoder: hpre[x] = sum over the row's live inputs of x * W1[n][x]
+  {
+    const WT* W = reinterpret_cast<const WT*>(e.W);
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    float xv[RR_UE];
+    int nn[RR_UE];
+    auto idx = [&](int j) {
+#pragma unroll
+      for (int u = 0; u < RR_UE; ++u) {
+        const int ju = j + u * NG;
+        const bool ok = ju < n_e;
+        xv[u] = ok ? e.xval[lb + ju] : 0.f;
+        nn[u] = ok ? e.col[s + ju] : 0;
+      }
+    };
+    idx(grp);
+    for (int j = grp; j < n_e; j += NG * RR_UE) {
+      uint4 wv[RR_UE][PPL];
+      float xc[RR_UE];
+#pragma unroll
+      for (int u = 0; u < RR_UE; ++u) {
+        xc[u] = xv[u];
+#pragma unroll
+        for (int i = 0; i < PPL; ++i)
+          wv[u][i] = xv[u] != 0.f ? load_piece_raw<WT>(W, e.ldw, e.w_blocked, nn[u], l + G * i) : make_uint4(0, 0, 0, 0);
+      }
+      idx(j + NG * RR_UE);
+#pragma unroll
+      for (int u = 0; u < RR_UE; ++u)
+#pragma unroll
+        for (int i = 0; i < PPL; ++i) {
+          float f[E];
+          unpack_piece<WT>(wv[u][i], f);
+#pragma unroll
+          for (int k = 0; k < E; ++k) acc[i * E + k] += xc[u] * f[k];
+        }
+    }
+    rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
+  }
+  __syncthreads();
+  // ---- hidden epilogue (rows_reduce_kernel BIAS_ACT arithmetic): a, mask, h stored for the backward pass
+  {
+    BiasActParams p;
+    p.bias = d.bias_h; p.act = d.act; p.keep = d.keep; p.seed = d.seed; p.stream = d.stream; p.mask_in = nullptr;
+    p.mask_out = d.mask_out; p.a_out = d.a_out; p.h_out = const_cast<void*>(d.h); p.h_dtype = d.h_dtype; p.ld = H;
+    p.m_real = d.m_real; p.n_real = d.n_real;
+    for (int x = tid; x < H; x += RR_THREADS)
+      h_sh[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, rr_row_sum(red, x), &a_sh[x], &mk_sh[x]));
+  }
+  __syncthreads();
+  // ---- decoder: at every live target y = m (h . W_out[n] + b_out[n]), err = y - t, delta = err m;
+  //      dh[x] = sum of delta * W_out[n][x]
+  {
+    const WT* W = reinterpret_cast<const WT*>(d.W);
+    const float m = d.aux;
+    float acc[V];
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    float sse = 0.f, sae = 0.f, cnt = 0.f;
+    bool live[RR_UD];
+    int n[RR_UD];
+    float t[RR_UD];
+    auto idx = [&](int j) {
+#pragma unroll
+      for (int u = 0; u < RR_UD; ++u) {
+        const int ju = j + u * NG;
+        const bool ok = ju < n_e;
+        live[u] = ok && d.flag[lb + ju];
+        n[u] = ok ? d.col[s + ju] : 0;
+        t[u] = ok ? d.val[s + ju] : 0.f;
+      }
+    };
+    idx(grp);
+    for (int j = grp; j < n_e; j += NG * RR_UD) {
+      uint4 wv[RR_UD][PPL];
+      bool lv[RR_UD];
+      int nc[RR_UD];
+      float tc[RR_UD], bn[RR_UD];
+#pragma unroll
+      for (int u = 0; u < RR_UD; ++u) {
+        lv[u] = live[u];
+        nc[u] = n[u];
+        tc[u] = t[u];
+        bn[u] = live[u] ? d.bias[n[u]] : 0.f;
+#pragma unroll
+        for (int i = 0; i < PPL; ++i)
+          wv[u][i] = live[u] ? load_piece_raw<WT>(W, d.ldw, d.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+      }
+      idx(j + NG * RR_UD);
+      // the hidden row's pieces from LDS one at a time (held in registers for the whole loop they spilled)
+      float dot[RR_UD];
+#pragma unroll
+      for (int u = 0; u < RR_UD; ++u) dot[u] = 0.f;
+#pragma unroll
+      for (int i = 0; i < PPL; ++i) {
+        float hh[E];
+#pragma unroll
+        for (int k = 0; k < E; ++k) hh[k] = h_sh[(l + G * i) * E + k];
+#pragma unroll
+        for (int u = 0; u < RR_UD; ++u) {
+          float f[E];
+          unpack_piece<WT>(wv[u][i], f);
+#pragma unroll
+          for (int k = 0; k < E; ++k) dot[u] += hh[k] * f[k];
+        }
+      }
+#pragma unroll
+      for (int off = G / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int u = 0; u < RR_UD; ++u) dot[u] += __shfl_xor(dot[u], off, G);
+#pragma unroll
+      for (int u = 0; u < RR_UD; ++u) {
+        const int ju = j + u * NG;
+        if (ju >= n_e) break;
+        float dl = 0.f;
+        if (lv[u]) {
+          const float yh = m * (dot[u] + bn[u]);
+          const float err = yh - tc[u];
+          dl = err * m;
+          if (l == 0) {
+            sse += err * err;
+            sae += fabsf(err);
+            cnt += (tc[u] + yh != 0.f) ? 1.f : 0.f;
+            if (d.d_out) store_ct(d.d_out, d.d_dtype, (int64_t)b * d.ld_d + nc[u], dl);
+          }
+        }
+        if (l == 0 && d.delta_e) d.delta_e[lb + ju] = dl;
+#pragma unroll
+        for (int i = 0; i < PPL; ++i) {
+          float f[E];
+          unpack_piece<WT>(wv[u][i], f);
+#pragma unroll
+          for (int k = 0; k < E; ++k) acc[i * E + k] += dl * f[k];
+        }
+      }
+    }
+    if (l == 0) {
+      st_sh[grp][0] = sse;
+      st_sh[grp][1] = sae;
+      st_sh[grp][2] = cnt;
+    }
+    __syncthreads();                 // (every wave is done reading red's encoder sums: the epilogue's barrier)
+    rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
+  }
+  __syncthreads();
+  // ---- the hidden delta (rows_reduce_kernel GRAD_ACT arithmetic) and the row's stats
+  for (int x = tid; x < H; x += RR_THREADS) {
+    const float v = rr_row_sum(red, x);
+    float dv = 0.f;
+    if (x < r.n_real) {
+      dv = v;
+      if (r.keep < 1.f && r.mask_in) dv = dv * ((float)mk_sh[x] / r.keep);
+      dv = dv * act_grad(r.act, a_sh[x]);
+    }
+    store_ct(r.h_out, r.h_dtype, rb + x, dv);
+    if (r.db_part) r.db_part[rb + x] = dv * r.gscale;
+  }
+  if (tid < 4) {
+    float v = 0.f;
+    if (tid < 3)
+      for (int g = 0; g < NG; ++g) v += st_sh[g][tid];
+    r.stats_part[(int64_t)b * 4 + tid] = v;
+    if (tid == 0 && r.row_sse) r.row_sse[b] = v;
+  }
+}
+
 // per batch row: fixed-order sum of its chunk partials, then the layer epilogue
 __global__ void __launch_bounds__(256) rows_reduce_kernel(OcfRowsReduceArgs a) {
   const int b = blockIdx.x;
@@ -659,6 +903,19 @@ void launch_encdec(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
 #undef OCF_ED
 }
 
+template <typename WT, typename HT>
+void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& d, hipStream_t s) {
+  OcfRowsReduceArgs r = *d.jr;
+  const dim3 grid(r.Bp), blk(RR_THREADS);
+#define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r)
+  if (G == 32 && ppl == 2) OCF_RR(32, 2);
+  else if (G == 32 && ppl == 1) OCF_RR(32, 1);
+  else if (G == 16 && ppl == 1) OCF_RR(16, 1);
+  else if (G == 16 && ppl == 3) OCF_RR(16, 3);
+  else throw std::runtime_error("row gather (row-resident): unsupported H / weight dtype combination");
+#undef OCF_RR
+}
+
 void check_gather(const OcfGatherArgs& a, const char* who) {
   OCF_CHECK(a.rows && a.rp && a.col && a.lboff && a.ch_row && a.ch_j0 && a.ch_j1 && a.W && a.part,
             std::string(who) + ": null pointer");
@@ -727,6 +984,11 @@ extern "C" int ocf_gather_decoder(const OcfGatherArgs* args, void* stream) {
 
 namespace ocf {
 int g_encdec_max_polls = 1 << 22;   // ocf_gather_encdec's bounded wait (ocf_set_tuning "encdec_max_polls")
+// ocf_gather_encdec's row-resident form for 16-bit weights (ocf_set_tuning "encdec_rowres"; env OCF_ENCDEC_ROWRES)
+int g_encdec_rowres = [] {
+  const char* v = std::getenv("OCF_ENCDEC_ROWRES");
+  return v ? std::atoi(v) : 1;
+}();
 }
 
 extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* dec, uint32_t* enc_arrive,
@@ -751,11 +1013,17 @@ extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* 
                 r.row_cptr && r.h_out && r.a_in && r.stats_part && r.B <= r.Bp && (r.keep >= 1.f || r.mask_in),
             "ocf_gather_encdec: jr must be OCF_REDUCE_GRAD_ACT over the decoder's part / chunk_stats");
   if (d.n_chunks == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  int G, ppl;
+  if (g_encdec_rowres && d.w_dtype != OCF_F32 && r.Bp > 0) {   // one workgroup per batch row: no hand-offs
+    if (d.w_dtype == OCF_F16) { shape_or_throw<_Float16>(d, G, ppl); launch_rowres<_Float16, _Float16>(G, ppl, e, d, s); }
+    else { shape_or_throw<__bf16>(d, G, ppl); launch_rowres<__bf16, __bf16>(G, ppl, e, d, s); }
+    OCF_HIP(hipGetLastError());
+    return 0;
+  }
   EncDecSync sy{enc_arrive, async_error_word(), nullptr, 0, g_encdec_max_polls};
   sy.gen = next_encdec_generation();
   sy.gate = encdec_gate_word();
-  hipStream_t s = (hipStream_t)stream;
-  int G, ppl;
   if (d.w_dtype == OCF_F32) { shape_or_throw<float>(d, G, ppl); launch_encdec<float, float>(G, ppl, e, d, sy, s); }
   else if (d.w_dtype == OCF_F16) { shape_or_throw<_Float16>(d, G, ppl); launch_encdec<_Float16, _Float16>(G, ppl, e, d, sy, s); }
   else { shape_or_throw<__bf16>(d, G, ppl); launch_encdec<__bf16, __bf16>(G, ppl, e, d, sy, s); }

@@ -32,7 +32,7 @@ static void tuning() {
                     {"rows_dual_parts", 23, 99}, {"rows_dual_pf", -1, -99}, {"rows_dual_large", 1, -99},
                     {"rows_dual_count", 0, -99}, {"rows_small_waves", 4096, -99}, {"optim_ws", 1, -99},
                     {"pair_wait_polls", 1 << 22, 0}, {"encdec_max_polls", 1 << 22, 0}, {"mlp_max_polls", 1 << 22, 0},
-                    {"optim_ws_max_k", 256, -99}};
+                    {"optim_ws_max_k", 256, -99}, {"encdec_rowres", 1, -99}};
   for (const K& k : keys) {
     int prev = -12345;
     EXPECT(ocf_set_tuning(k.key, k.good, &prev) == 0, k.key);

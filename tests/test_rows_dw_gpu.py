@@ -585,6 +585,7 @@ def test_encdec_launch_bit_identical(gpu, cd, shape, B):
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     rows, cols, nnz, skew = shape
     out = []
+    prev = _rowres(0)                      # (the chunked form: the row-resident one sums in another order)
     for fused in (False, True):
         rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=5)
         om = om_ = omni_model(1, 500 if cd != "float32" else 200, cols, B, dense_activation="sigmoid",
@@ -600,6 +601,7 @@ def test_encdec_launch_bit_identical(gpu, cd, shape, B):
                     [s for sw, sb in eng.slots for s in sw + sb if s is not None] +
                     [t.clone() for t in eng.Wsh if t is not None]))
         del om_
+    _rowres(prev)
     assert out[0][0] == out[1][0]
     for a, b in zip(out[0][1], out[1][1]):
         assert torch.equal(a, b)
@@ -615,7 +617,14 @@ def test_encdec_gives_up_safely(gpu):
     from omnidirectional_collaborative_filtering_amd import optimizers as O
     from omnidirectional_collaborative_filtering_amd.model import omni_model
     lib = _lib.load()
+    prev_rr = _rowres(0)                   # (the chunked form's hand-off: the row-resident form has no wait)
+    try:
+        _gives_up_safely(lib, O, omni_model)
+    finally:
+        _rowres(prev_rr)
 
+
+def _gives_up_safely(lib, O, omni_model):
     def build():
         rd, gen = _gen_for(2000, 30000, 300000, 256, 0.5, seed=21)
         om = omni_model(1, 500, 30000, 256, dense_activation="sigmoid", use_causal_info=False,
@@ -663,3 +672,74 @@ def test_encdec_gives_up_safely(gpu):
     for x, y in zip(sa, sb):
         assert torch.equal(x, y)
     assert int(ea.enc_arrive.abs().sum()) == 0 and int(ea.row_arrive.abs().sum()) == 0
+
+
+def _rowres(on):
+    prev = _lib.ctypes.c_int32()
+    _lib.call("ocf_set_tuning", b"encdec_rowres", int(on), _lib.ctypes.byref(prev))
+    return prev.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd,shape,B", [("float16", (2000, 30000, 300000, 0.5), 256),   # large weights, skewed rows
+                                        ("bfloat16", (3706, 6040, 1000209, 0.0), 256),  # ML-1M: rows of 3+ chunks
+                                        ("float16", (2000, 30000, 300000, 0.0), 100)])   # padding rows
+def test_encdec_rowres_matches_chunked(gpu, cd, shape, B):
+    """ocf_gather_encdec's row-resident form (one 1,024-thread workgroup per batch row; "encdec_rowres") against
+    the chunked form on the same first step from the same state.  Only the order of the fp32 sums differs, so:
+    the activations within 1e-5; h (rounded to the compute dtype) equal but for rare one-ulp flips; the hidden
+    delta within two ulps of its dtype plus 1e-3 (f16) / 1e-2 (bf16) of its scale (a flipped h element moves
+    every delta of its row a little); the loss within 1e-5 relative; padding rows zero"""
+    from omnidirectional_collaborative_filtering_amd import optimizers as O
+    from omnidirectional_collaborative_filtering_amd.model import omni_model
+    rows, cols, nnz, skew = shape
+    out = []
+    prev = _rowres(0)
+    try:
+        for rr in (0, 1):
+            _rowres(rr)
+            rd, gen = _gen_for(rows, cols, nnz, B, skew, seed=5)
+            om = omni_model(1, 500, cols, B, dense_activation="sigmoid", use_causal_info=False,
+                            dropout_probability=0.2, compute_dtype=cd, seed=4)
+            eng = om.engine
+            eng.fuse_enc_dec = True
+            m = om.model
+            m.compile(O.Adagrad(lr=0.01, epsilon=1e-8), "mean_squared_error", metrics=["mae"])
+            h = m.fit_generator(gen, 1, epochs=1, verbose=0).history
+            torch.cuda.synchronize()
+            out.append((h["loss"][0], eng.a[0][:, :500].clone(), eng.h[0][:, :500].float().clone(),
+                        eng.dh[0][:, :500].float().clone()))
+            del om, eng, m
+    finally:
+        _rowres(prev)
+    (l0, a0, h0, d0), (l1, a1, h1, d1) = out
+    assert abs(l1 - l0) <= 1e-5 * abs(l0)
+    assert float((a1[:B] - a0[:B]).abs().max()) <= 1e-5
+    flips = (h1[:B] != h0[:B]).float().mean().item()
+    assert flips <= 2e-3, flips
+    ulp = 2.0 ** -10 if cd == "float16" else 2.0 ** -7
+    tol = 2 * ulp * d0.abs() + (1e-3 if cd == "float16" else 1e-2) * float(d0.abs().max())
+    bad = ((d1 - d0).abs() > tol)[:B]
+    assert int(bad.sum()) == 0, (int(bad.sum()), float((d1 - d0).abs().max()))
+    if B < d1.shape[0]:
+        assert float(d1[B:].abs().max()) == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cd", ["float16", "bfloat16"])
+def test_encdec_rowres_train_parity(gpu, cd):
+    """training through the row-resident launch against the oracle (tests/parity.py envelope and quantile bars):
+    three Adagrad steps with dropout 0.2 at a large-weight width"""
+    from omnidirectional_collaborative_filtering_amd.dataset import split_ratings, synthetic_ratings
+    from tests.parity import assert_low_precision, run_parity
+    rows, cols, nnz = 1500, 30000, 600000
+    r, c, v = synthetic_ratings(rows, cols, nnz, half_stars=True, seed=7)
+    data = split_ratings(r, c, v, rows, cols, rng=np.random.RandomState(7))
+    prev = _rowres(1)
+    try:
+        res = run_parity(cd, "adagrad", 1, "sigmoid", steps=3, B=256, H=500, dropout=0.2, data=data, envelope=True,
+                         sparse_oracle=True, eval_batches=2,
+                         model_hook=lambda om: setattr(om.engine, "fuse_enc_dec", True))
+    finally:
+        _rowres(prev)
+    assert_low_precision(res, 2e-3 if cd == "float16" else 1e-2)
