@@ -725,8 +725,8 @@ int ocf_mlp_step(const OcfMlpStepArgs* args, void* stream);
  *               tile kernel itself (0).
  *   "encdec_rowres": ocf_gather_encdec with 16-bit weights as one 1,024-thread workgroup per batch row (1: the
  *               row's encoder, hidden epilogue, decoder and delta reduction with LDS reductions, no hand-offs;
- *               results equal to fp32 summation order) or as the chunked launch (0); env OCF_ENCDEC_ROWRES sets
- *               the initial value.
+ *               results equal to fp32 summation order) or as the chunked launch (0); a negative value only
+ *               reports the setting; env OCF_ENCDEC_ROWRES sets the initial value (default 1).
  *   "pair_wait_polls", "encdec_max_polls", "mlp_max_polls": the bounded in-kernel waits of ocf_gemm_pair,
  *               ocf_gather_encdec and ocf_mlp_step (polls of ~64 cycles); the last two take a negative value as
  *               fault injection for tests (a give-up on workgroup 0 / batch row 0).

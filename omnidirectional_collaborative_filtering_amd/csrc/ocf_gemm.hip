@@ -288,9 +288,9 @@ extern "C" int ocf_set_tuning(const char* key, int value, int* previous) {
     if (previous) *previous = g_encdec_max_polls;
     OCF_CHECK(value != 0, "ocf_set_tuning: encdec_max_polls != 0");
     g_encdec_max_polls = value;
-  } else if (k == "encdec_rowres") {      // ocf_gather_encdec: one workgroup per batch row (16-bit weights)
+  } else if (k == "encdec_rowres") {      // ocf_gather_encdec: one workgroup per batch row (< 0: only report)
     if (previous) *previous = g_encdec_rowres;
-    g_encdec_rowres = value ? 1 : 0;
+    if (value >= 0) g_encdec_rowres = value ? 1 : 0;
   } else if (k == "mlp_max_polls") {      // ocf_mlp_step's bounded barrier wait (tests: < 0 injects a give-up)
     if (previous) *previous = g_mlp_max_polls;
     OCF_CHECK(value != 0, "ocf_set_tuning: mlp_max_polls != 0");

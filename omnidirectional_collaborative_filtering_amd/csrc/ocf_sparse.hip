@@ -909,9 +909,10 @@ void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
   const dim3 grid(r.Bp), blk(RR_THREADS);
 #define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r)
   if (G == 32 && ppl == 2) OCF_RR(32, 2);
+  else if (G == 64 && ppl == 2) OCF_RR(64, 2);
+  else if (G == 64 && ppl == 1) OCF_RR(64, 1);
   else if (G == 32 && ppl == 1) OCF_RR(32, 1);
   else if (G == 16 && ppl == 1) OCF_RR(16, 1);
-  else if (G == 16 && ppl == 3) OCF_RR(16, 3);
   else throw std::runtime_error("row gather (row-resident): unsupported H / weight dtype combination");
 #undef OCF_RR
 }
@@ -1015,9 +1016,16 @@ extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* 
   if (d.n_chunks == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   int G, ppl;
-  if (g_encdec_rowres && d.w_dtype != OCF_F32 && r.Bp > 0) {   // one workgroup per batch row: no hand-offs
+  // one workgroup per batch row: no hand-offs.  fp32 rows (2 KB at H = 512) as one 64-lane group per entry
+  // (32 lanes x 4 pieces would not fit the 1,024-thread workgroup's 128 VGPRs)
+  // (H = 384 at 16 bits, 16 lanes x 3 pieces, would spill: the chunked form)
+  bool rr = g_encdec_rowres && r.Bp > 0;
+  if (d.w_dtype == OCF_F32) rr = rr && d.H % 256 == 0;
+  else rr = rr && d.H != 384;
+  if (rr) {
     if (d.w_dtype == OCF_F16) { shape_or_throw<_Float16>(d, G, ppl); launch_rowres<_Float16, _Float16>(G, ppl, e, d, s); }
-    else { shape_or_throw<__bf16>(d, G, ppl); launch_rowres<__bf16, __bf16>(G, ppl, e, d, s); }
+    else if (d.w_dtype == OCF_BF16) { shape_or_throw<__bf16>(d, G, ppl); launch_rowres<__bf16, __bf16>(G, ppl, e, d, s); }
+    else launch_rowres<float, float>(64, d.H / 256, e, d, s);
     OCF_HIP(hipGetLastError());
     return 0;
   }

@@ -971,8 +971,8 @@ class Engine:
             xv = self.gt["xval"]
             g.xval = xv if isinstance(xv, int) else ptr(xv)
             if (self.comm is None and len(self.H) == 1 and self.fuse_enc_epilogue
-                    and tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS
-                    and tab["n_chunks"] <= FUSE_MEAN_CHUNKS * self.B):
+                    and (self._rowres() or (tab.get("max_chunks", 0) <= FUSE_MAX_CHUNKS
+                                            and tab["n_chunks"] <= FUSE_MEAN_CHUNKS * self.B))):
                 # the decoder gather applies bias / activation / dropout to these partials itself; the encoder's
                 # launch is deferred to the decoder's (one fused launch when the decoder can take it)
                 self._enc_fused = dict(enc_part=ptr(part), enc_cptr=tab["row_cptr"], keep=keep, stream=stream_id,
@@ -1041,7 +1041,10 @@ class Engine:
             self._dec_reduced = True
         if ef is not None:
             ea, et = ef["args"], ef["tab"]
-            fuse = self.fuse_enc_dec if self.fuse_enc_dec is not None else self.Np // TILE * 48 >= 8192
+            # (the row-resident form runs on any weight size: ML-1M bf16 0.0711 -> 0.0587 ms/step, ML-1M U 0.0549 ->
+            # 0.0441, same box, profiles/r06_rowres/; the chunked form only pays on large weights)
+            fuse = self.fuse_enc_dec if self.fuse_enc_dec is not None else (
+                self.Np // TILE * 48 >= 8192 or self._rowres())
             if (fuse and g.jr and et["ch_row"] == tab["ch_row"] and et["n_chunks"] == tab["n_chunks"]
                     and et["lboff"] == tab["lboff"]):
                 # (one launch: the caller's dec_gemm_mse phase times both, enc_gemm records nothing)
@@ -1636,8 +1639,21 @@ class Engine:
     def _fits(self, pl, f):
         # (every template fuses the encoder's epilogue into the decoder: _forward_gather's gates apply to it too)
         return (f[self._F_NCH] <= pl["cap_enc"] and f[self._F_NCH] <= pl["cap_dec"] and f[self._F_E] <= pl["cap_e"]
-                and f[self._F_MAXCH] <= FUSE_MAX_CHUNKS and f[self._F_NCH] <= FUSE_MEAN_CHUNKS * self.B
+                and (self._rowres() or (f[self._F_MAXCH] <= FUSE_MAX_CHUNKS
+                                        and f[self._F_NCH] <= FUSE_MEAN_CHUNKS * self.B))
                 and self.n_stats < self.stats_cap)
+
+    def _rowres(self):
+        """ocf_gather_encdec takes its row-resident form (the library's "encdec_rowres" switch, read when the
+        engine is built; fp32 at H % 256 == 0, 16-bit at H != 384): one workgroup per batch row, no chunk partials re-read, so the encoder's
+        epilogue rides in the decoder launch whatever the chunks per row"""
+        rr = self.__dict__.get("_rowres_on")
+        if rr is None:
+            prev = ctypes.c_int32(0)
+            _lib.call("ocf_set_tuning", b"encdec_rowres", -1, ctypes.byref(prev))
+            rr = self._rowres_on = bool(prev.value) and (self.Hp[-1] % 256 == 0 if self.cdt == _lib.DT_F32
+                                                          else self.Hp[-1] != 384)
+        return rr
 
     def _rewrite(self, pl, f, per):
         v = np.array(f, dtype=np.int64)

@@ -20,3 +20,15 @@ def gpu():
     from omnidirectional_collaborative_filtering_amd import _lib
     _lib.load()
     return torch.device("cuda")
+
+
+@pytest.fixture
+def chunked_encdec(gpu):
+    """ocf_gather_encdec in its chunked form for the test (tests comparing launch forms bit for bit against the
+    two-launch gathers: the row-resident form sums in another order)"""
+    import ctypes
+    from omnidirectional_collaborative_filtering_amd import _lib
+    prev = ctypes.c_int32()
+    _lib.call("ocf_set_tuning", b"encdec_rowres", 0, ctypes.byref(prev))
+    yield
+    _lib.call("ocf_set_tuning", b"encdec_rowres", prev.value, None)

@@ -329,7 +329,7 @@ def test_engine_row_skip_bit_identical(gpu, cd):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cd", ["float32", "float16"])
-def test_engine_fused_encoder_epilogue_bit_identical(gpu, cd):
+def test_engine_fused_encoder_epilogue_bit_identical(gpu, chunked_encdec, cd):
     """The hidden layer's bias / sigmoid / dropout applied inside the decoder gather (Engine.fuse_enc_epilogue)
     against the separate row-reduce launch: identical losses, weights, slots, shadows and test SSE."""
     from omnidirectional_collaborative_filtering_amd import optimizers as O

@@ -378,7 +378,7 @@ def test_rows_job_only_workgroups_stay_in_bounds(gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cd,B", [("float16", 128), ("float32", 128), ("bfloat16", 100)])
-def test_engine_fold_reduce_bit_identical(gpu, cd, B):
+def test_engine_fold_reduce_bit_identical(gpu, chunked_encdec, cd, B):
     """The decoder's δh row reduction as jobs of the dW_out launch (Engine.fold_reduce; the hidden-bias and
     stats jobs then ride in dW_in), or in the decoder launch by each row's last chunk (reduce_in_decoder:
     write-through partials and a per-row arrival counter; B = 100 leaves 28 padding rows for its zero-row
@@ -533,7 +533,7 @@ def test_rows_dual_bit_identical(gpu, cd, shape, skip, opt):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cd,opt,skip,H", [("float16", "adagrad", True, 500), ("bfloat16", "adam", False, 500),
                                            ("float32", "rmsprop", False, 200), ("float16", "adagrad", True, 512)])
-def test_rows_dual_large_bit_identical(gpu, cd, opt, skip, H):
+def test_rows_dual_large_bit_identical(gpu, chunked_encdec, cd, opt, skip, H):
     """The dual-row form on LARGE weights (235 row tiles: above the small-weight gate; ocf_set_tuning
     "rows_dual_large", the row reduction in the decoder) against the pair launch and against two launches:
     identical losses, weights, slots and shadows, and the dual launch really ran once per step"""
