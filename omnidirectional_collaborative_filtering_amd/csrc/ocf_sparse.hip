@@ -558,6 +558,9 @@ constexpr int RR_UE = OCF_RR_UE;   // entries per group in flight in the encoder
 // 4 148 B.  ML-20M, same box: chunked 0.3802, row-resident with 3 0.3770, with 2 0.3626 ms/step
 // (profiles/r06_rowres/)
 constexpr int RR_UD = OCF_RR_UD;
+#ifndef OCF_RR_GD64
+#define OCF_RR_GD64 0
+#endif
 
 // the groups' per-lane vectors summed into red[wave][x]: the groups of one wave by lane shuffles (a fixed xor
 // tree), then the waves' rows by the caller in wave order
@@ -584,17 +587,19 @@ __device__ __forceinline__ float rr_row_sum(const float (*red)[RG_MAX_H], int x)
   return s0 + s1;
 }
 
-template <typename WT, typename HT, int G, int PPL>
+template <typename WT, typename HT, int G, int PPL, int GD = G, int PPLD = PPL>
 __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs e, OcfGatherArgs d,
                                                                    OcfRowsReduceArgs r) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
   constexpr int NG = RR_THREADS / G;
+  constexpr int VD = PPLD * E;                 // the decoder part's lane groups (GD lanes x PPLD pieces)
+  constexpr int NGD = RR_THREADS / GD;
   __shared__ float red[RR_WAVES][RG_MAX_H];
   __shared__ float h_sh[RG_MAX_H];
   __shared__ float a_sh[RG_MAX_H];
   __shared__ uint8_t mk_sh[RG_MAX_H];
-  __shared__ float st_sh[NG][3];
+  __shared__ float st_sh[NGD][3];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int grp = tid / G, l = tid % G;
   const int H = d.H;
@@ -670,9 +675,10 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
   {
     const WT* W = reinterpret_cast<const WT*>(d.W);
     const float m = d.aux;
-    float acc[V];
+    const int grp = threadIdx.x / GD, l = threadIdx.x % GD;
+    float acc[VD];
 #pragma unroll
-    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    for (int k = 0; k < VD; ++k) acc[k] = 0.f;
     float sse = 0.f, sae = 0.f, cnt = 0.f;
     bool live[RR_UD];
     int n[RR_UD];
@@ -680,7 +686,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
     auto idx = [&](int j) {
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) {
-        const int ju = j + u * NG;
+        const int ju = j + u * NGD;
         const bool ok = ju < n_e;
         live[u] = ok && d.flag[lb + ju];
         n[u] = ok ? d.col[s + ju] : 0;
@@ -688,8 +694,8 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
       }
     };
     idx(grp);
-    for (int j = grp; j < n_e; j += NG * RR_UD) {
-      uint4 wv[RR_UD][PPL];
+    for (int j = grp; j < n_e; j += NGD * RR_UD) {
+      uint4 wv[RR_UD][PPLD];
       bool lv[RR_UD];
       int nc[RR_UD];
       float tc[RR_UD], bn[RR_UD];
@@ -700,19 +706,19 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         tc[u] = t[u];
         bn[u] = live[u] ? d.bias[n[u]] : 0.f;
 #pragma unroll
-        for (int i = 0; i < PPL; ++i)
-          wv[u][i] = live[u] ? load_piece_raw<WT>(W, d.ldw, d.w_blocked, n[u], l + G * i) : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < PPLD; ++i)
+          wv[u][i] = live[u] ? load_piece_raw<WT>(W, d.ldw, d.w_blocked, n[u], l + GD * i) : make_uint4(0, 0, 0, 0);
       }
-      idx(j + NG * RR_UD);
+      idx(j + NGD * RR_UD);
       // the hidden row's pieces from LDS one at a time (held in registers for the whole loop they spilled)
       float dot[RR_UD];
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) dot[u] = 0.f;
 #pragma unroll
-      for (int i = 0; i < PPL; ++i) {
+      for (int i = 0; i < PPLD; ++i) {
         float hh[E];
 #pragma unroll
-        for (int k = 0; k < E; ++k) hh[k] = h_sh[(l + G * i) * E + k];
+        for (int k = 0; k < E; ++k) hh[k] = h_sh[(l + GD * i) * E + k];
 #pragma unroll
         for (int u = 0; u < RR_UD; ++u) {
           float f[E];
@@ -722,12 +728,12 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         }
       }
 #pragma unroll
-      for (int off = G / 2; off > 0; off >>= 1)
+      for (int off = GD / 2; off > 0; off >>= 1)
 #pragma unroll
-        for (int u = 0; u < RR_UD; ++u) dot[u] += __shfl_xor(dot[u], off, G);
+        for (int u = 0; u < RR_UD; ++u) dot[u] += __shfl_xor(dot[u], off, GD);
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) {
-        const int ju = j + u * NG;
+        const int ju = j + u * NGD;
         if (ju >= n_e) break;
         float dl = 0.f;
         if (lv[u]) {
@@ -743,7 +749,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         }
         if (l == 0 && d.delta_e) d.delta_e[lb + ju] = dl;
 #pragma unroll
-        for (int i = 0; i < PPL; ++i) {
+        for (int i = 0; i < PPLD; ++i) {
           float f[E];
           unpack_piece<WT>(wv[u][i], f);
 #pragma unroll
@@ -757,7 +763,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
       st_sh[grp][2] = cnt;
     }
     __syncthreads();                 // (every wave is done reading red's encoder sums: the epilogue's barrier)
-    rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
+    rr_wave_sums<GD, VD, E, PPLD>(acc, red, l, lane, w);
   }
   __syncthreads();
   // ---- the hidden delta (rows_reduce_kernel GRAD_ACT arithmetic) and the row's stats
@@ -775,7 +781,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
   if (tid < 4) {
     float v = 0.f;
     if (tid < 3)
-      for (int g = 0; g < NG; ++g) v += st_sh[g][tid];
+      for (int g = 0; g < NGD; ++g) v += st_sh[g][tid];
     r.stats_part[(int64_t)b * 4 + tid] = v;
     if (tid == 0 && r.row_sse) r.row_sse[b] = v;
   }
@@ -908,7 +914,9 @@ void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
   OcfRowsReduceArgs r = *d.jr;
   const dim3 grid(r.Bp), blk(RR_THREADS);
 #define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r)
-  if (G == 32 && ppl == 2) OCF_RR(32, 2);
+  if (G == 32 && ppl == 2 && OCF_RR_GD64)   // (16-bit, H = 512: the decoder part as one 64-lane group per entry)
+    hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, 32, 2, 64, 1>), grid, blk, 0, s, e, d, r);
+  else if (G == 32 && ppl == 2) OCF_RR(32, 2);
   else if (G == 64 && ppl == 2) OCF_RR(64, 2);
   else if (G == 64 && ppl == 1) OCF_RR(64, 1);
   else if (G == 32 && ppl == 1) OCF_RR(32, 1);
