@@ -558,9 +558,9 @@ constexpr int RR_UE = OCF_RR_UE;   // entries per group in flight in the encoder
 // 4 148 B.  ML-20M, same box: chunked 0.3802, row-resident with 3 0.3770, with 2 0.3626 ms/step
 // (profiles/r06_rowres/)
 constexpr int RR_UD = OCF_RR_UD;
-#ifndef OCF_RR_GD64
-#define OCF_RR_GD64 0
-#endif
+// (the decoder part's lane groups are a template parameter, GD x PPLD: 64 lanes x 1 piece at 16 bits with 4 / 5
+// entries in flight measured slower than 32 x 2 with 2 -- ML-20M 0.3799 / 0.3775 vs 0.3667, ML-1M 0.0635 / 0.0631
+// vs 0.0591, Netflix 1.9549 vs 1.8555 ms/step, profiles/r06_rowres/rr_gd64_*)
 
 // the groups' per-lane vectors summed into red[wave][x]: the groups of one wave by lane shuffles (a fixed xor
 // tree), then the waves' rows by the caller in wave order
@@ -914,9 +914,7 @@ void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
   OcfRowsReduceArgs r = *d.jr;
   const dim3 grid(r.Bp), blk(RR_THREADS);
 #define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r)
-  if (G == 32 && ppl == 2 && OCF_RR_GD64)   // (16-bit, H = 512: the decoder part as one 64-lane group per entry)
-    hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, 32, 2, 64, 1>), grid, blk, 0, s, e, d, r);
-  else if (G == 32 && ppl == 2) OCF_RR(32, 2);
+  if (G == 32 && ppl == 2) OCF_RR(32, 2);
   else if (G == 64 && ppl == 2) OCF_RR(64, 2);
   else if (G == 64 && ppl == 1) OCF_RR(64, 1);
   else if (G == 32 && ppl == 1) OCF_RR(32, 1);
