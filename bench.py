@@ -802,6 +802,16 @@ def main():
         "dec_gemm_mse": P * w_b + Bg * H * 2 + Bg * Nl * 2,
         "dec_bwd_gemm": P * w_b + Bg * Nl * 2,
     }
+    if sparse_a and eng.use_sparse:
+        # the row gathers (encoder / decoder / both in one launch, ocf_gather_encdec): a weight row per entry
+        # (H real elements in the compute dtype) + the entry's index / value / flag / delta bytes; the decoder also
+        # writes the batch's a / mask / h / hidden-delta rows.  The one launch is timed as dec_gemm_mse (no
+        # enc_gemm phase then)
+        ent = nnz / args.steps / max(world, 1)
+        g_enc = ent * (H * w_b + 8)
+        g_dec = ent * (H * w_b + 13) + Bg * H * (4 + 1 + 2 * w_b)
+        alg["enc_gemm"] = g_enc
+        alg["dec_gemm_mse"] = g_dec + (g_enc if "enc_gemm" not in phases else 0)
     # the fused small-model step: the whole step in one launch, against its dense-update bytes and its flops
     # (forward, output layer, input-delta-free backward: 3 GEMMs of 2 B N H each way + the hidden delta)
     alg["mlp_step"] = P * 2 * (opt_b + 4 + sh_b) + Bg * Nl * 4 * 3

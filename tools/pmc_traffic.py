@@ -27,7 +27,8 @@ def per_dispatch(path, counter):
 
 
 def phase_of(name, seen):
-    if "gather_encdec" in name:           # the encoder and the decoder as one launch (ocf_gather_encdec)
+    if "gather_encdec" in name or "gather_rowres" in name:   # the encoder and the decoder as one launch
+                                          # (ocf_gather_encdec: chunked or row-resident)
         seen["gather"] = "dec"
         return "enc_dec"
     if "gather_encoder" in name:
