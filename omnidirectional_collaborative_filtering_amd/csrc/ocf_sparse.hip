@@ -577,6 +577,9 @@ __device__ __forceinline__ void rr_wave_sums(float (&acc)[V], float (*red)[RG_MA
       for (int k = 0; k < E; ++k) red[w][(l + G * i) * E + k] = acc[i * E + k];
   }
 }
+// a workgroup barrier for LDS hand-offs only: __syncthreads would also wait for this wave's outstanding global loads
+// (the decoder's first W_out rows, requested before the encoder's reduction to overlap it)
+__device__ __forceinline__ void rr_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ float rr_row_sum(const float (*red)[RG_MAX_H], int x) {
   float s0 = 0.f, s1 = 0.f;
 #pragma unroll
@@ -659,57 +662,83 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
     }
     rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
   }
-  __syncthreads();
+  // the decoder's first entries: indices and W_out rows requested now, in flight across the encoder's reduction
+  // and the hidden epilogue (they do not depend on h)
+  const int grpd = threadIdx.x / GD, ld_ = threadIdx.x % GD;
+  const WT* Wd = reinterpret_cast<const WT*>(d.W);
+  bool live[RR_UD];
+  int n[RR_UD];
+  float t[RR_UD];
+  // branch-free: every load issued (indices clamped to the row, results masked at use), so the compiler can count
+  // them and a wait for an early load does not wait for the rows requested after it
+  auto idx_d = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < RR_UD; ++u) {
+      const int ju = j + u * NGD;
+      const int jc = ju < n_e ? ju : n_e - 1;
+      const uint8_t fl = d.flag[lb + jc];
+      const int nn = d.col[s + jc];
+      live[u] = ju < n_e && fl;
+      n[u] = live[u] ? nn : 0;                 // (not a live target: row 0, an L2 hit, instead of its own row)
+      t[u] = d.val[s + jc];
+    }
+  };
+  uint4 wv[RR_UD][PPLD];
+  float bn[RR_UD];
+  auto load_d = [&]() {
+#pragma unroll
+    for (int u = 0; u < RR_UD; ++u) {
+      bn[u] = d.bias[n[u]];
+#pragma unroll
+      for (int i = 0; i < PPLD; ++i) wv[u][i] = load_piece_raw<WT>(Wd, d.ldw, d.w_blocked, n[u], ld_ + GD * i);
+    }
+  };
+  // (the epilogue's bias loads go first: a wait for them would otherwise also wait for the rows behind them)
+  const bool xl = tid < H;                       // (H <= 512 < RR_THREADS: one column per thread)
+  const float bh = xl && b < d.m_real && tid < d.n_real ? d.bias_h[tid] : 0.f;
+  idx_d(grpd);
+  load_d();
+  rr_lds_barrier();
   // ---- hidden epilogue (rows_reduce_kernel BIAS_ACT arithmetic): a, mask, h stored for the backward pass
-  {
-    BiasActParams p;
-    p.bias = d.bias_h; p.act = d.act; p.keep = d.keep; p.seed = d.seed; p.stream = d.stream; p.mask_in = nullptr;
-    p.mask_out = d.mask_out; p.a_out = d.a_out; p.h_out = const_cast<void*>(d.h); p.h_dtype = d.h_dtype; p.ld = H;
-    p.m_real = d.m_real; p.n_real = d.n_real;
-    for (int x = tid; x < H; x += RR_THREADS)
-      h_sh[x] = (float)CvtT<HT>::to(bias_act_value(p, b, x, rr_row_sum(red, x), &a_sh[x], &mk_sh[x]));
+  if (xl) {                      // bias_act_value's arithmetic with the bias already loaded
+    const int x = tid;
+    const int64_t ix = rb + x;
+    const bool live = b < d.m_real && x < d.n_real;
+    const float av = live ? act_apply(d.act, rr_row_sum(red, x) + bh) : 0.f;
+    float hvx = av;
+    a_sh[x] = av;
+    if (d.keep < 1.f) {
+      const uint8_t mk = (uint8_t)floorf(d.keep + philox_uniform(d.seed, d.stream, (uint64_t)ix));
+      hvx = (av / d.keep) * (float)mk;
+      if (d.mask_out) d.mask_out[ix] = mk;
+      mk_sh[x] = mk;
+    }
+    if (d.a_out) d.a_out[ix] = av;
+    store_ct(const_cast<void*>(d.h), d.h_dtype, ix, hvx);
+    h_sh[x] = (float)CvtT<HT>::to(hvx);
   }
-  __syncthreads();
+  rr_lds_barrier();
   // ---- decoder: at every live target y = m (h . W_out[n] + b_out[n]), err = y - t, delta = err m;
   //      dh[x] = sum of delta * W_out[n][x]
   {
-    const WT* W = reinterpret_cast<const WT*>(d.W);
     const float m = d.aux;
-    const int grp = threadIdx.x / GD, l = threadIdx.x % GD;
+    const int grp = grpd, l = ld_;
     float acc[VD];
 #pragma unroll
     for (int k = 0; k < VD; ++k) acc[k] = 0.f;
     float sse = 0.f, sae = 0.f, cnt = 0.f;
-    bool live[RR_UD];
-    int n[RR_UD];
-    float t[RR_UD];
-    auto idx = [&](int j) {
-#pragma unroll
-      for (int u = 0; u < RR_UD; ++u) {
-        const int ju = j + u * NGD;
-        const bool ok = ju < n_e;
-        live[u] = ok && d.flag[lb + ju];
-        n[u] = ok ? d.col[s + ju] : 0;
-        t[u] = ok ? d.val[s + ju] : 0.f;
-      }
-    };
-    idx(grp);
     for (int j = grp; j < n_e; j += NGD * RR_UD) {
-      uint4 wv[RR_UD][PPLD];
+      // this iteration's entries (their W_out rows were requested at the end of the previous one)
       bool lv[RR_UD];
       int nc[RR_UD];
-      float tc[RR_UD], bn[RR_UD];
+      float tc[RR_UD];
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) {
         lv[u] = live[u];
         nc[u] = n[u];
         tc[u] = t[u];
-        bn[u] = live[u] ? d.bias[n[u]] : 0.f;
-#pragma unroll
-        for (int i = 0; i < PPLD; ++i)
-          wv[u][i] = live[u] ? load_piece_raw<WT>(W, d.ldw, d.w_blocked, n[u], l + GD * i) : make_uint4(0, 0, 0, 0);
       }
-      idx(j + NGD * RR_UD);
+      idx_d(j + NGD * RR_UD);
       // the hidden row's pieces from LDS one at a time (held in registers for the whole loop they spilled)
       float dot[RR_UD];
 #pragma unroll
@@ -756,6 +785,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
           for (int k = 0; k < E; ++k) acc[i * E + k] += dl * f[k];
         }
       }
+      load_d();                        // the next iteration's rows (none past the row's end: live is false there)
     }
     if (l == 0) {
       st_sh[grp][0] = sse;
