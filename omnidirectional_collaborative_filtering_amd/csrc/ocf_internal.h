@@ -17,6 +17,10 @@ void check_async_errors();
 extern int g_mlp_max_polls;          // ocf_mlp_step's barrier wait (ocf_set_tuning "mlp_max_polls")
 extern int g_encdec_max_polls;       // ocf_gather_encdec's wait (ocf_set_tuning "encdec_max_polls")
 extern int g_encdec_rowres;          // ocf_gather_encdec's row-resident form (ocf_set_tuning "encdec_rowres")
+// a feature rank's gathers as row-resident launches (ocf_sparse.hip; ocf_rank_step phases 0 / 1): false = not
+// applicable, nothing launched
+bool rank_rowres_enc(const OcfGatherArgs& e, const OcfRowsReduceArgs& r, hipStream_t s);
+bool rank_rowres_dec(const OcfBiasActArgs& hb, const OcfGatherArgs& d, const OcfRowsReduceArgs& r, hipStream_t s);
 extern int g_enc_tiles_pack;         // ocf_encoder_tiles' pre-pass (ocf_set_tuning "enc_tiles_pack")
 // The encoder -> decoder hand-off's gate (ocf_gather_encdec): a device word a decoder chunk that gave up sets to
 // its launch's generation; the row-stream weight-update launches issued after that encdec launch (the same

@@ -545,8 +545,6 @@ __global__ void __launch_bounds__(RG_THREADS) gather_encdec_kernel(OcfGatherArgs
 // hand-offs, at 3 waves per SIMD.  Arithmetic per entry as in encoder_chunk / decoder_chunk; the sums run over the
 // row's entries in another order (per lane group, then over the groups in a fixed order), so the results equal the
 // chunked form's to fp32 rounding, not bit for bit.
-constexpr int RR_THREADS = 1024;
-constexpr int RR_WAVES = RR_THREADS / 64;
 #ifndef OCF_RR_UD
 #define OCF_RR_UD 2
 #endif
@@ -556,11 +554,16 @@ constexpr int RR_WAVES = RR_THREADS / 64;
 constexpr int RR_UE = OCF_RR_UE;   // entries per group in flight in the encoder part
 // ... in the decoder part: 2 (115 VGPRs); 3 spilled 44 B per lane at the 1,024-thread workgroup's 128 VGPRs and
 // 4 148 B.  ML-20M, same box: chunked 0.3802, row-resident with 3 0.3770, with 2 0.3626 ms/step
-// (profiles/r06_rowres/)
+// (profiles/r06_rowres/).  (64-lane groups x 1 piece at 16 bits with 4 / 5 entries in flight measured slower than
+// 32 x 2 with 2: ML-20M 0.3799 / 0.3775 vs 0.3667, ML-1M 0.0635 / 0.0631 vs 0.0591, Netflix 1.9549 vs 1.8555
+// ms/step, profiles/r06_rowres/rr_gd64_*)
 constexpr int RR_UD = OCF_RR_UD;
-// (the decoder part's lane groups are a template parameter, GD x PPLD: 64 lanes x 1 piece at 16 bits with 4 / 5
-// entries in flight measured slower than 32 x 2 with 2 -- ML-20M 0.3799 / 0.3775 vs 0.3667, ML-1M 0.0635 / 0.0631
-// vs 0.0591, Netflix 1.9549 vs 1.8555 ms/step, profiles/r06_rowres/rr_gd64_*)
+
+// what a row-resident launch does (gather_rowres_kernel MODE)
+enum { RR_FULL = 0,        // ocf_gather_encdec: encoder, hidden epilogue, decoder, hidden delta (GRAD_ACT)
+       RR_ENC_RAW = 1,     // a feature-parallel rank's phase 0: the encoder's row sums (RAW, before the all-reduce)
+       RR_DEC_RAW = 2 };   // ... phase 1: the hidden epilogue from the all-reduced sums, the decoder, the hidden
+                           // delta's row sums (RAW, before the all-reduce) and the row stats
 
 // the groups' per-lane vectors summed into red[wave][x]: the groups of one wave by lane shuffles (a fixed xor
 // tree), then the waves' rows by the caller in wave order
@@ -580,49 +583,75 @@ __device__ __forceinline__ void rr_wave_sums(float (&acc)[V], float (*red)[RG_MA
 // a workgroup barrier for LDS hand-offs only: __syncthreads would also wait for this wave's outstanding global loads
 // (the decoder's first W_out rows, requested before the encoder's reduction to overlap it)
 __device__ __forceinline__ void rr_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+template <int NW>
 __device__ __forceinline__ float rr_row_sum(const float (*red)[RG_MAX_H], int x) {
   float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-  for (int w = 0; w < RR_WAVES; w += 2) {
+  for (int w = 0; w < NW; w += 2) {
     s0 += red[w][x];
     s1 += red[w + 1][x];
   }
   return s0 + s1;
 }
+// ocf_splitk_bias_act's slab sum (ocf_elem.hip sum_slabs: the same order)
+__device__ __forceinline__ float rr_sum_slabs(const float* s, int splits, int64_t sstride) {
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= splits; k += 4) {
+    v0 += s[(int64_t)(k + 0) * sstride];
+    v1 += s[(int64_t)(k + 1) * sstride];
+    v2 += s[(int64_t)(k + 2) * sstride];
+    v3 += s[(int64_t)(k + 3) * sstride];
+  }
+  for (; k < splits; ++k) v0 += s[(int64_t)k * sstride];
+  return (v0 + v1) + (v2 + v3);
+}
 
-template <typename WT, typename HT, int G, int PPL, int GD = G, int PPLD = PPL>
-__global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs e, OcfGatherArgs d,
-                                                                   OcfRowsReduceArgs r) {
+// e: the encoder's gather arguments (RR_FULL, RR_ENC_RAW); d: the decoder's (RR_FULL, RR_DEC_RAW; its rows /
+// lboff / rp give the batch rows in every mode); r: the row reduction (GRAD_ACT for RR_FULL, RAW for the others);
+// hb: the hidden epilogue over the all-reduced slabs (RR_DEC_RAW)
+template <typename WT, typename HT, int G, int PPL, int T, int MODE>
+__global__ void __launch_bounds__(T) gather_rowres_kernel(OcfGatherArgs e, OcfGatherArgs d, OcfRowsReduceArgs r,
+                                                          OcfBiasActArgs hb) {
   constexpr int E = EPc<WT>::v;
   constexpr int V = PPL * E;
-  constexpr int NG = RR_THREADS / G;
-  constexpr int VD = PPLD * E;                 // the decoder part's lane groups (GD lanes x PPLD pieces)
-  constexpr int NGD = RR_THREADS / GD;
-  __shared__ float red[RR_WAVES][RG_MAX_H];
+  constexpr int NG = T / G;
+  constexpr int NW = T / 64;
+  constexpr int XPT = (RG_MAX_H + T - 1) / T;   // hidden columns per thread in the row loops
+  __shared__ float red[NW][RG_MAX_H];
   __shared__ float h_sh[RG_MAX_H];
   __shared__ float a_sh[RG_MAX_H];
   __shared__ uint8_t mk_sh[RG_MAX_H];
-  __shared__ float st_sh[NGD][3];
+  __shared__ float st_sh[NG][3];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int grp = tid / G, l = tid % G;
-  const int H = d.H;
+  const OcfGatherArgs& q = MODE == RR_ENC_RAW ? e : d;     // (the batch rows)
+  const int H = q.H;
   const int64_t rb = (int64_t)b * H;
-  if (d.zero_word && b == 0 && tid == 0) __hip_atomic_store(d.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int row = b < r.B ? d.rows[b] : -1;
-  const int64_t lb = b < r.B ? d.lboff[b] : 0;
-  const int n_e = row >= 0 ? (int)(d.lboff[b + 1] - lb) : 0;
-  if (n_e == 0) {            // padding rows, rows without entries: the reduction's outputs of an empty row
-    for (int x = tid; x < H; x += RR_THREADS) {
-      store_ct(r.h_out, r.h_dtype, rb + x, 0.f);
-      if (r.db_part) r.db_part[rb + x] = 0.f;
+  if (MODE == RR_FULL && d.zero_word && b == 0 && tid == 0)
+    __hip_atomic_store(d.zero_word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int row = b < r.B ? q.rows[b] : -1;
+  const int64_t lb = b < r.B ? q.lboff[b] : 0;
+  const int n_e = row >= 0 ? (int)(q.lboff[b + 1] - lb) : 0;
+  // (RR_DEC_RAW: the hidden epilogue runs for every row, as ocf_splitk_bias_act did)
+  if (n_e == 0 && MODE != RR_DEC_RAW) {   // padding rows, rows without entries: an empty row's outputs
+    for (int x = tid; x < H; x += T) {
+      if (MODE == RR_FULL) {
+        store_ct(r.h_out, r.h_dtype, rb + x, 0.f);
+        if (r.db_part) r.db_part[rb + x] = 0.f;
+      } else {
+        r.out[rb + x] = 0.f;
+      }
     }
-    if (tid < 4) r.stats_part[(int64_t)b * 4 + tid] = 0.f;
-    if (tid == 0 && r.row_sse) r.row_sse[b] = 0.f;
+    if (MODE == RR_FULL) {
+      if (tid < 4) r.stats_part[(int64_t)b * 4 + tid] = 0.f;
+      if (tid == 0 && r.row_sse) r.row_sse[b] = 0.f;
+    }
     return;
   }
-  const int64_t s = d.rp[row];
+  const int64_t s = n_e > 0 ? q.rp[row] : 0;
   // ---- encoder: hpre[x] = sum over the row's live inputs of x * W1[n][x]
-  {
+  if constexpr (MODE != RR_DEC_RAW) {
     const WT* W = reinterpret_cast<const WT*>(e.W);
     float acc[V];
 #pragma unroll
@@ -662,9 +691,35 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
     }
     rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
   }
+  if constexpr (MODE == RR_ENC_RAW) {
+    __syncthreads();
+    for (int x = tid; x < H; x += T) r.out[rb + x] = rr_row_sum<NW>(red, x);
+    return;
+  }
+  // the hidden epilogue's inputs, loaded before the decoder's first rows (a wait for them would otherwise also wait
+  // for the rows requested after them): the bias, and (RR_DEC_RAW) the all-reduced sums
+  BiasActParams p;
+  if constexpr (MODE == RR_FULL) {
+    p.bias = d.bias_h; p.act = d.act; p.keep = d.keep; p.seed = d.seed; p.stream = d.stream; p.mask_in = nullptr;
+    p.mask_out = d.mask_out; p.a_out = d.a_out; p.h_out = const_cast<void*>(d.h); p.h_dtype = d.h_dtype;
+    p.ld = H; p.m_real = d.m_real; p.n_real = d.n_real;
+  } else {
+    p.bias = hb.bias; p.act = hb.act; p.keep = hb.keep; p.seed = hb.seed; p.stream = hb.stream;
+    p.mask_in = hb.mask_in; p.mask_out = hb.mask_out; p.a_out = hb.a_out; p.h_out = hb.h_out; p.h_dtype = hb.h_dtype;
+    p.ld = hb.ld; p.m_real = hb.m_real; p.n_real = hb.n_real;
+  }
+  float bh[XPT], vin[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int x = tid + i * T;
+    const bool lv = x < H && b < p.m_real && x < p.n_real;
+    bh[i] = lv ? p.bias[x] : 0.f;
+    vin[i] = 0.f;
+    if constexpr (MODE == RR_DEC_RAW)
+      if (x < H) vin[i] = rr_sum_slabs(hb.slabs + (int64_t)b * hb.ld + x, hb.splits, hb.split_stride);
+  }
   // the decoder's first entries: indices and W_out rows requested now, in flight across the encoder's reduction
   // and the hidden epilogue (they do not depend on h)
-  const int grpd = threadIdx.x / GD, ld_ = threadIdx.x % GD;
   const WT* Wd = reinterpret_cast<const WT*>(d.W);
   bool live[RR_UD];
   int n[RR_UD];
@@ -674,47 +729,52 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
   auto idx_d = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RR_UD; ++u) {
-      const int ju = j + u * NGD;
+      const int ju = j + u * NG;
       const int jc = ju < n_e ? ju : n_e - 1;
-      const uint8_t fl = d.flag[lb + jc];
-      const int nn = d.col[s + jc];
+      const bool ok = n_e > 0;
+      const uint8_t fl = ok ? d.flag[lb + jc] : 0;
+      const int nn = ok ? d.col[s + jc] : 0;
       live[u] = ju < n_e && fl;
       n[u] = live[u] ? nn : 0;                 // (not a live target: row 0, an L2 hit, instead of its own row)
-      t[u] = d.val[s + jc];
+      t[u] = ok ? d.val[s + jc] : 0.f;
     }
   };
-  uint4 wv[RR_UD][PPLD];
+  uint4 wv[RR_UD][PPL];
   float bn[RR_UD];
   auto load_d = [&]() {
 #pragma unroll
     for (int u = 0; u < RR_UD; ++u) {
       bn[u] = d.bias[n[u]];
 #pragma unroll
-      for (int i = 0; i < PPLD; ++i) wv[u][i] = load_piece_raw<WT>(Wd, d.ldw, d.w_blocked, n[u], ld_ + GD * i);
+      for (int i = 0; i < PPL; ++i) wv[u][i] = load_piece_raw<WT>(Wd, d.ldw, d.w_blocked, n[u], l + G * i);
     }
   };
-  // (the epilogue's bias loads go first: a wait for them would otherwise also wait for the rows behind them)
-  const bool xl = tid < H;                       // (H <= 512 < RR_THREADS: one column per thread)
-  const float bh = xl && b < d.m_real && tid < d.n_real ? d.bias_h[tid] : 0.f;
-  idx_d(grpd);
+  idx_d(grp);
   load_d();
-  rr_lds_barrier();
-  // ---- hidden epilogue (rows_reduce_kernel BIAS_ACT arithmetic): a, mask, h stored for the backward pass
-  if (xl) {                      // bias_act_value's arithmetic with the bias already loaded
-    const int x = tid;
-    const int64_t ix = rb + x;
-    const bool live = b < d.m_real && x < d.n_real;
-    const float av = live ? act_apply(d.act, rr_row_sum(red, x) + bh) : 0.f;
+  if constexpr (MODE == RR_FULL) rr_lds_barrier();
+  // ---- hidden epilogue (bias_act_value's arithmetic with the bias already loaded): a, mask, h stored for the
+  //      backward pass
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int x = tid + i * T;
+    if (x >= H) break;
+    const int64_t ix = (int64_t)b * p.ld + x;
+    const bool lv = b < p.m_real && x < p.n_real;
+    float v = vin[i];
+    if constexpr (MODE == RR_FULL) v = rr_row_sum<NW>(red, x);
+    const float av = lv ? act_apply(p.act, v + bh[i]) : 0.f;
     float hvx = av;
     a_sh[x] = av;
-    if (d.keep < 1.f) {
-      const uint8_t mk = (uint8_t)floorf(d.keep + philox_uniform(d.seed, d.stream, (uint64_t)ix));
-      hvx = (av / d.keep) * (float)mk;
-      if (d.mask_out) d.mask_out[ix] = mk;
+    if (p.keep < 1.f) {
+      uint8_t mk;
+      if (p.mask_in) mk = p.mask_in[ix];
+      else mk = (uint8_t)floorf(p.keep + philox_uniform(p.seed, p.stream, (uint64_t)ix));
+      hvx = (av / p.keep) * (float)mk;
+      if (p.mask_out) p.mask_out[ix] = mk;
       mk_sh[x] = mk;
     }
-    if (d.a_out) d.a_out[ix] = av;
-    store_ct(const_cast<void*>(d.h), d.h_dtype, ix, hvx);
+    if (p.a_out) p.a_out[ix] = av;
+    if (p.h_out) store_ct(p.h_out, p.h_dtype, ix, hvx);
     h_sh[x] = (float)CvtT<HT>::to(hvx);
   }
   rr_lds_barrier();
@@ -722,12 +782,11 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
   //      dh[x] = sum of delta * W_out[n][x]
   {
     const float m = d.aux;
-    const int grp = grpd, l = ld_;
-    float acc[VD];
+    float acc[V];
 #pragma unroll
-    for (int k = 0; k < VD; ++k) acc[k] = 0.f;
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
     float sse = 0.f, sae = 0.f, cnt = 0.f;
-    for (int j = grp; j < n_e; j += NGD * RR_UD) {
+    for (int j = grp; j < n_e; j += NG * RR_UD) {
       // this iteration's entries (their W_out rows were requested at the end of the previous one)
       bool lv[RR_UD];
       int nc[RR_UD];
@@ -738,16 +797,16 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         nc[u] = n[u];
         tc[u] = t[u];
       }
-      idx_d(j + NGD * RR_UD);
+      idx_d(j + NG * RR_UD);
       // the hidden row's pieces from LDS one at a time (held in registers for the whole loop they spilled)
       float dot[RR_UD];
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) dot[u] = 0.f;
 #pragma unroll
-      for (int i = 0; i < PPLD; ++i) {
+      for (int i = 0; i < PPL; ++i) {
         float hh[E];
 #pragma unroll
-        for (int k = 0; k < E; ++k) hh[k] = h_sh[(l + GD * i) * E + k];
+        for (int k = 0; k < E; ++k) hh[k] = h_sh[(l + G * i) * E + k];
 #pragma unroll
         for (int u = 0; u < RR_UD; ++u) {
           float f[E];
@@ -757,12 +816,12 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         }
       }
 #pragma unroll
-      for (int off = GD / 2; off > 0; off >>= 1)
+      for (int off = G / 2; off > 0; off >>= 1)
 #pragma unroll
-        for (int u = 0; u < RR_UD; ++u) dot[u] += __shfl_xor(dot[u], off, GD);
+        for (int u = 0; u < RR_UD; ++u) dot[u] += __shfl_xor(dot[u], off, G);
 #pragma unroll
       for (int u = 0; u < RR_UD; ++u) {
-        const int ju = j + u * NGD;
+        const int ju = j + u * NG;
         if (ju >= n_e) break;
         float dl = 0.f;
         if (lv[u]) {
@@ -778,7 +837,7 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
         }
         if (l == 0 && d.delta_e) d.delta_e[lb + ju] = dl;
 #pragma unroll
-        for (int i = 0; i < PPLD; ++i) {
+        for (int i = 0; i < PPL; ++i) {
           float f[E];
           unpack_piece<WT>(wv[u][i], f);
 #pragma unroll
@@ -793,25 +852,29 @@ __global__ void __launch_bounds__(RR_THREADS) gather_rowres_kernel(OcfGatherArgs
       st_sh[grp][2] = cnt;
     }
     __syncthreads();                 // (every wave is done reading red's encoder sums: the epilogue's barrier)
-    rr_wave_sums<GD, VD, E, PPLD>(acc, red, l, lane, w);
+    rr_wave_sums<G, V, E, PPL>(acc, red, l, lane, w);
   }
   __syncthreads();
-  // ---- the hidden delta (rows_reduce_kernel GRAD_ACT arithmetic) and the row's stats
-  for (int x = tid; x < H; x += RR_THREADS) {
-    const float v = rr_row_sum(red, x);
-    float dv = 0.f;
-    if (x < r.n_real) {
-      dv = v;
-      if (r.keep < 1.f && r.mask_in) dv = dv * ((float)mk_sh[x] / r.keep);
-      dv = dv * act_grad(r.act, a_sh[x]);
+  // ---- the hidden delta (rows_reduce_kernel GRAD_ACT arithmetic; RR_DEC_RAW: the row sums) and the row's stats
+  for (int x = tid; x < H; x += T) {
+    const float v = rr_row_sum<NW>(red, x);
+    if constexpr (MODE == RR_DEC_RAW) {
+      r.out[rb + x] = v;
+    } else {
+      float dv = 0.f;
+      if (x < r.n_real) {
+        dv = v;
+        if (r.keep < 1.f && r.mask_in) dv = dv * ((float)mk_sh[x] / r.keep);
+        dv = dv * act_grad(r.act, a_sh[x]);
+      }
+      store_ct(r.h_out, r.h_dtype, rb + x, dv);
+      if (r.db_part) r.db_part[rb + x] = dv * r.gscale;
     }
-    store_ct(r.h_out, r.h_dtype, rb + x, dv);
-    if (r.db_part) r.db_part[rb + x] = dv * r.gscale;
   }
   if (tid < 4) {
     float v = 0.f;
     if (tid < 3)
-      for (int g = 0; g < NGD; ++g) v += st_sh[g][tid];
+      for (int g = 0; g < NG; ++g) v += st_sh[g][tid];
     r.stats_part[(int64_t)b * 4 + tid] = v;
     if (tid == 0 && r.row_sse) r.row_sse[b] = v;
   }
@@ -939,11 +1002,11 @@ void launch_encdec(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
 #undef OCF_ED
 }
 
-template <typename WT, typename HT>
-void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& d, hipStream_t s) {
-  OcfRowsReduceArgs r = *d.jr;
-  const dim3 grid(r.Bp), blk(RR_THREADS);
-#define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP>), grid, blk, 0, s, e, d, r)
+template <typename WT, typename HT, int T, int MODE>
+void launch_rowres_t(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& d, const OcfRowsReduceArgs& r,
+                     const OcfBiasActArgs& hb, hipStream_t s) {
+  const dim3 grid(r.Bp), blk(T);
+#define OCF_RR(GG, PP) hipLaunchKernelGGL((gather_rowres_kernel<WT, HT, GG, PP, T, MODE>), grid, blk, 0, s, e, d, r, hb)
   if (G == 32 && ppl == 2) OCF_RR(32, 2);
   else if (G == 64 && ppl == 2) OCF_RR(64, 2);
   else if (G == 64 && ppl == 1) OCF_RR(64, 1);
@@ -952,6 +1015,29 @@ void launch_rowres(int G, int ppl, const OcfGatherArgs& e, const OcfGatherArgs& 
   else throw std::runtime_error("row gather (row-resident): unsupported H / weight dtype combination");
 #undef OCF_RR
 }
+// T threads per row: 1,024 for ocf_gather_encdec's rows (hundreds of entries), 256 for a feature rank's rows of a
+// column shard (~1/G of them)
+template <int MODE>
+void launch_rowres(int dtype, int H, int T, const OcfGatherArgs& e, const OcfGatherArgs& d,
+                   const OcfRowsReduceArgs& r, const OcfBiasActArgs& hb, hipStream_t s) {
+  int G, ppl;
+  if (dtype == OCF_F32) {
+    G = 64;
+    ppl = H / 256;
+  } else if (!(dtype == OCF_F16 ? gather_shape<_Float16>(H, G, ppl) : gather_shape<__bf16>(H, G, ppl))) {
+    throw std::runtime_error("row gather (row-resident): unsupported H");
+  }
+  auto go = [&](auto wt) {
+    using WT = decltype(wt);
+    if (T == 256) launch_rowres_t<WT, WT, 256, MODE>(G, ppl, e, d, r, hb, s);
+    else launch_rowres_t<WT, WT, 1024, MODE>(G, ppl, e, d, r, hb, s);
+  };
+  if (dtype == OCF_F32) go(float{});
+  else if (dtype == OCF_F16) go(_Float16{});
+  else go(__bf16{});
+}
+// (H = 384 at 16 bits, 16 lanes x 3 pieces, would spill: the chunked forms)
+bool rowres_shape_ok(int dtype, int H) { return dtype == OCF_F32 ? H % 256 == 0 : H != 384; }
 
 void check_gather(const OcfGatherArgs& a, const char* who) {
   OCF_CHECK(a.rows && a.rp && a.col && a.lboff && a.ch_row && a.ch_j0 && a.ch_j1 && a.W && a.part,
@@ -1054,14 +1140,8 @@ extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* 
   int G, ppl;
   // one workgroup per batch row: no hand-offs.  fp32 rows (2 KB at H = 512) as one 64-lane group per entry
   // (32 lanes x 4 pieces would not fit the 1,024-thread workgroup's 128 VGPRs)
-  // (H = 384 at 16 bits, 16 lanes x 3 pieces, would spill: the chunked form)
-  bool rr = g_encdec_rowres && r.Bp > 0;
-  if (d.w_dtype == OCF_F32) rr = rr && d.H % 256 == 0;
-  else rr = rr && d.H != 384;
-  if (rr) {
-    if (d.w_dtype == OCF_F16) { shape_or_throw<_Float16>(d, G, ppl); launch_rowres<_Float16, _Float16>(G, ppl, e, d, s); }
-    else if (d.w_dtype == OCF_BF16) { shape_or_throw<__bf16>(d, G, ppl); launch_rowres<__bf16, __bf16>(G, ppl, e, d, s); }
-    else launch_rowres<float, float>(64, d.H / 256, e, d, s);
+  if (g_encdec_rowres && r.Bp > 0 && rowres_shape_ok(d.w_dtype, d.H)) {
+    launch_rowres<RR_FULL>(d.w_dtype, d.H, 1024, e, d, r, OcfBiasActArgs{}, s);
     OCF_HIP(hipGetLastError());
     return 0;
   }
@@ -1074,6 +1154,36 @@ extern "C" int ocf_gather_encdec(const OcfGatherArgs* enc, const OcfGatherArgs* 
   OCF_HIP(hipGetLastError());
   OCF_TRY_END
 }
+
+namespace ocf {
+// A feature-parallel rank's gathers in the row-resident form (ocf_rank_step phases 0 / 1, "encdec_rowres"):
+// phase 0's encoder + RAW row reduction as one launch, phase 1's hidden epilogue (ocf_splitk_bias_act) + decoder +
+// RAW row reduction + row stats as one launch.  false: the arguments do not fit the form (the caller issues the
+// separate launches).  Rows of a column shard are short (~1/G of a row): 256 threads per row when the chunk table
+// holds about one chunk per row.
+bool rank_rowres_enc(const OcfGatherArgs& e, const OcfRowsReduceArgs& r, hipStream_t s) {
+  if (!(g_encdec_rowres && rowres_shape_ok(e.w_dtype, e.H) && r.mode == OCF_REDUCE_RAW && r.out && r.H == e.H &&
+        e.xval && r.Bp > 0 && r.B <= r.Bp && e.n_chunks > 0))
+    return false;
+  check_gather(e, "ocf_rank_step (row-resident encoder)");
+  const int T = e.n_chunks <= 2 * r.B ? 256 : 1024;
+  launch_rowres<RR_ENC_RAW>(e.w_dtype, e.H, T, e, e, r, OcfBiasActArgs{}, s);
+  OCF_HIP(hipGetLastError());
+  return true;
+}
+bool rank_rowres_dec(const OcfBiasActArgs& hb, const OcfGatherArgs& d, const OcfRowsReduceArgs& r, hipStream_t s) {
+  if (!(g_encdec_rowres && rowres_shape_ok(d.w_dtype, d.H) && r.mode == OCF_REDUCE_RAW && r.out && r.H == d.H &&
+        r.stats_part && r.Bp > 0 && r.B <= r.Bp && d.n_chunks > 0 && !d.enc_part && !d.jr && d.flag && d.val &&
+        d.bias && hb.slabs && hb.splits >= 1 && hb.M == r.Bp && hb.N == d.H && hb.ld >= d.H && hb.bias &&
+        d.h_dtype == d.w_dtype && hb.h_dtype == d.w_dtype && (hb.keep >= 1.f || hb.mask_out || hb.mask_in)))
+    return false;
+  check_gather(d, "ocf_rank_step (row-resident decoder)");
+  const int T = d.n_chunks <= 2 * r.B ? 256 : 1024;
+  launch_rowres<RR_DEC_RAW>(d.w_dtype, d.H, T, d, d, r, hb, s);
+  OCF_HIP(hipGetLastError());
+  return true;
+}
+}  // namespace ocf
 
 extern "C" int ocf_rows_reduce(const OcfRowsReduceArgs* args, void* stream) {
   OCF_TRY_BEGIN

@@ -22,17 +22,22 @@ extern "C" int ocf_rank_step(const OcfRankStepArgs* a, int phase, void* stream) 
   switch (phase) {
     case 0:
       record(a->ev[0], s);
-      ok(ocf_gather_encoder(&a->enc, stream));
-      ok(ocf_rows_reduce(&a->enc_sum, stream));
+      if (!ocf::rank_rowres_enc(a->enc, a->enc_sum, s)) {     // (the row-resident form: one launch)
+        ok(ocf_gather_encoder(&a->enc, stream));
+        ok(ocf_rows_reduce(&a->enc_sum, stream));
+      }
       record(a->ev[1], s);
       break;
     case 1: {
       record(a->ev[2], s);
       const OcfBiasActArgs& h = a->hidden;
-      ok(ocf_splitk_bias_act(h.slabs, h.splits, h.split_stride, h.M, h.N, h.ld, h.bias, h.act, h.keep, h.seed,
-                             h.stream, h.mask_in, h.mask_out, h.a_out, h.h_out, h.h_dtype, h.m_real, h.n_real, stream));
-      ok(ocf_gather_decoder(&a->dec, stream));
-      ok(ocf_rows_reduce(&a->dec_sum, stream));
+      if (!ocf::rank_rowres_dec(h, a->dec, a->dec_sum, s)) {  // (the row-resident form: one launch)
+        ok(ocf_splitk_bias_act(h.slabs, h.splits, h.split_stride, h.M, h.N, h.ld, h.bias, h.act, h.keep, h.seed,
+                               h.stream, h.mask_in, h.mask_out, h.a_out, h.h_out, h.h_dtype, h.m_real, h.n_real,
+                               stream));
+        ok(ocf_gather_decoder(&a->dec, stream));
+        ok(ocf_rows_reduce(&a->dec_sum, stream));
+      }
       record(a->ev[3], s);
       const OcfStatsArgs& st = a->stats;
       if (side) order(a->fork[0], s, side);
