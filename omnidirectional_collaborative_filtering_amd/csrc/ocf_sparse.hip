@@ -726,17 +726,18 @@ __global__ void __launch_bounds__(T) gather_rowres_kernel(OcfGatherArgs e, OcfGa
   float t[RR_UD];
   // branch-free: every load issued (indices clamped to the row, results masked at use), so the compiler can count
   // them and a wait for an early load does not wait for the rows requested after it
+  // (an empty row, RR_DEC_RAW only: entry 0 of the tables stands in; nothing of it is used)
+  const int64_t lbq = n_e > 0 ? lb : 0;
   auto idx_d = [&](int j) {
 #pragma unroll
     for (int u = 0; u < RR_UD; ++u) {
       const int ju = j + u * NG;
-      const int jc = ju < n_e ? ju : n_e - 1;
-      const bool ok = n_e > 0;
-      const uint8_t fl = ok ? d.flag[lb + jc] : 0;
-      const int nn = ok ? d.col[s + jc] : 0;
+      const int jc = max(min(ju, n_e - 1), 0);
+      const uint8_t fl = d.flag[lbq + jc];
+      const int nn = d.col[s + jc];
       live[u] = ju < n_e && fl;
       n[u] = live[u] ? nn : 0;                 // (not a live target: row 0, an L2 hit, instead of its own row)
-      t[u] = ok ? d.val[s + jc] : 0.f;
+      t[u] = d.val[s + jc];
     }
   };
   uint4 wv[RR_UD][PPL];
