@@ -614,6 +614,12 @@ def side_configs():
 
 def main():
     args = parse()
+    if os.environ.get("OCF_TUNING"):
+        # experiment hook for tools/ab.py: "key=value,key=value" passed to ocf_set_tuning before any launch
+        from omnidirectional_collaborative_filtering_amd import _lib
+        for kv in os.environ["OCF_TUNING"].split(","):
+            k, _, v = kv.partition("=")
+            _lib.call("ocf_set_tuning", k.strip().encode(), int(v), None)
     if args.config == "jester":
         return jester_main(args)
     from omnidirectional_collaborative_filtering_amd.parallel import (DataParallel, feature_shard_range,

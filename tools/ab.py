@@ -8,7 +8,8 @@ every variant, then rep 2, ...), so box drift hits all of them alike.  One JSON 
 gpurun_out/ab/<tag>.jsonl (ms/step, the dominant kernel's event mean and frac, the warm-up phases); the
 summary (medians) is printed and written to gpurun_out/ab/<tag>_summary.json.  A failing run ends the
 script (no retries).  The bench's side legs (CPU baseline, test RMSE, fp32 mode, full epoch) are off unless
-a variant turns them back on.
+a variant turns them back on.  A variant's OCF_TUNING="key=value,..." is passed by bench.py to ocf_set_tuning
+before any launch (e.g. "long1|OCF_TUNING=rows_long=1").
 """
 import argparse
 import json
